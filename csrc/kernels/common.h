@@ -1,0 +1,89 @@
+// Shared CDNA4 (gfx950) helpers for the serverless_learn_amd kernels.
+//
+// Everything here targets wave64 / MFMA 16x16x32 bf16.  Fragment maps
+// (cdna_hip_programming.md §3, verified with asymmetric operands in
+// tests/test_kernels_gpu.py):
+//   A frag  : lane l holds A[row = l&15][k = 8*(l>>4) + j], j = 0..7
+//   B frag  : lane l holds B[k = 8*(l>>4) + j][col = l&15]
+//   C/D     : lane l holds C[row = 4*(l>>4) + r][col = l&15], r = 0..3
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+
+#define SL_LDS __attribute__((address_space(3)))
+
+namespace sl {
+
+__device__ __forceinline__ floatx4_t mfma16(const short8_t& a, const short8_t& b, const floatx4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)a, (bf16x8_t)b, c, 0, 0, 0);
+}
+
+// fp32 -> bf16 bits, round-to-nearest-even (NaN kept quiet).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ floatx4_t zero4() { return floatx4_t{0.f, 0.f, 0.f, 0.f}; }
+
+__device__ __forceinline__ short8_t zero8() {
+  short8_t z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = 0;
+  return z;
+}
+
+// 16-byte global load of 8 bf16.
+__device__ __forceinline__ short8_t ld8(const uint16_t* p) { return *reinterpret_cast<const short8_t*>(p); }
+
+// 16-byte LDS load of 8 bf16 (ds_read_b128).
+__device__ __forceinline__ short8_t lds8(const uint16_t* p) { return *reinterpret_cast<const short8_t*>(p); }
+
+// Two transposed LDS reads (ds_read_b64_tr_b16) that build a B fragment
+// from a row-major [k][n] bf16 image: rows k0..k0+7 of the lane's
+// 8-row group, column n0 + (lane&15).  `ld` is the row stride in elements.
+__device__ __forceinline__ short8_t lds_tr8(const uint16_t* base, int ld, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const uint16_t* a0 = base + (8 * g + q) * ld + 4 * p;
+  const uint16_t* a1 = a0 + 4 * ld;
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SL_LDS short4_t*)(a0));
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SL_LDS short4_t*)(a1));
+  short8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// Unpack 8 bytes of uint8 pixels, normalise (x*a + b) and pack to bf16x8.
+__device__ __forceinline__ short8_t u8x8_to_bf16(uint2 v, float a, float b) {
+  short8_t r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = (short)f2bf((float)((v.x >> (8 * j)) & 0xffu) * a + b);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[4 + j] = (short)f2bf((float)((v.y >> (8 * j)) & 0xffu) * a + b);
+  return r;
+}
+
+// XCD-aware bijective remap of a 1-D grid (cdna_hip_programming.md §5 T1):
+// consecutive logical tiles land on the same XCD so they share its L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace sl
+
+#define SL_CHECK_LAUNCH() \
+  do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)

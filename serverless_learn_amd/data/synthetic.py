@@ -1,0 +1,111 @@
+"""Seeded synthetic MNIST-shaped data and the shard record format.
+
+The reference's file server serves one "dummy file": 100,000,000 bytes from a
+default-seeded ``std::independent_bits_engine`` (/root/reference/src/file_server.cc:40,151-156),
+which workers read and discard (/root/reference/src/worker.cc:54-56).  Here a
+file is a *shard* of labelled MNIST-shaped records that a worker actually
+trains on.  Records are learnable (10 smooth class prototypes + noise), so the
+loss falls during a run and accuracy is meaningful, yet no dataset download is
+needed (there is no network).
+
+Shard wire/file layout (little-endian, all offsets from the file start):
+
+    0   8s   magic  b"SLSHARD1"
+    8   u32  version (1)
+    12  u32  kind    (1 = u8 images + u8 labels)
+    16  u64  n       number of records
+    24  u32  height  (28)
+    28  u32  width   (28)
+    32  u32  classes (10)
+    36  u32  shard_index
+    40  u32  num_shards
+    44  u32  reserved
+    48  u64  seed
+    56  u64  reserved
+    64  u8[n*height*width]  images, row-major, record-contiguous
+    ..  u8[n]               labels
+
+A 100,000,000-byte shard (the reference's file size) holds 127,388 records.
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+
+MAGIC = b"SLSHARD1"
+HEADER = struct.Struct("<8sIIQIIIIII QQ")
+HEADER_SIZE = 64
+assert HEADER.size == HEADER_SIZE
+RECORD_BYTES = 28 * 28 + 1
+REFERENCE_FILE_BYTES = 100_000_000  # /root/reference/src/file_server.cc:40
+
+
+def records_for_bytes(nbytes: int = REFERENCE_FILE_BYTES) -> int:
+    return (nbytes - HEADER_SIZE) // RECORD_BYTES
+
+
+def _prototypes(classes: int, h: int, w: int, seed: int) -> np.ndarray:
+    rng = np.random.default_rng(seed ^ 0x5EED)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    protos = np.zeros((classes, h, w), np.float32)
+    for c in range(classes):
+        for _ in range(3):
+            cy, cx = rng.uniform(5, h - 5), rng.uniform(5, w - 5)
+            sy, sx = rng.uniform(1.5, 4.0), rng.uniform(1.5, 4.0)
+            protos[c] += np.exp(-((yy - cy) ** 2 / (2 * sy * sy) + (xx - cx) ** 2 / (2 * sx * sx)))
+    protos /= protos.max(axis=(1, 2), keepdims=True)
+    return protos.reshape(classes, h * w)
+
+
+def make_mnist_like(n: int, seed: int = 0, classes: int = 10, h: int = 28, w: int = 28,
+                    noise: float = 1.0) -> tuple[np.ndarray, np.ndarray]:
+    """(images u8 [n, h*w], labels u8 [n]) -- deterministic in (n, seed)."""
+    rng = np.random.default_rng(seed)
+    protos = _prototypes(classes, h, w, 1234)  # shared by every shard: same task
+    labels = rng.integers(0, classes, size=n, dtype=np.uint8)
+    out = np.empty((n, h * w), np.uint8)
+    chunk = 16384
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        amp = rng.uniform(0.6, 1.0, size=(e - s, 1)).astype(np.float32)
+        img = protos[labels[s:e]] * amp + rng.standard_normal((e - s, h * w), dtype=np.float32) * noise
+        np.clip(img * 255.0, 0, 255, out=img)
+        out[s:e] = img.astype(np.uint8)
+    return out, labels
+
+
+def encode_shard(images: np.ndarray, labels: np.ndarray, shard_index: int = 0, num_shards: int = 1,
+                 seed: int = 0, h: int = 28, w: int = 28, classes: int = 10) -> bytes:
+    n = images.shape[0]
+    hdr = HEADER.pack(MAGIC, 1, 1, n, h, w, classes, shard_index, num_shards, 0, seed, 0)
+    return hdr + np.ascontiguousarray(images, np.uint8).tobytes() + np.ascontiguousarray(labels, np.uint8).tobytes()
+
+
+def decode_header(buf) -> dict:
+    mv = memoryview(buf)
+    if len(mv) < HEADER_SIZE:
+        raise ValueError("shard too short")
+    magic, ver, kind, n, h, w, classes, si, ns, _r, seed, _r2 = HEADER.unpack(bytes(mv[:HEADER_SIZE]))
+    if magic != MAGIC:
+        raise ValueError("bad shard magic")
+    return dict(version=ver, kind=kind, n=n, height=h, width=w, classes=classes,
+                shard_index=si, num_shards=ns, seed=seed)
+
+
+def decode_shard(buf) -> tuple[dict, np.ndarray, np.ndarray]:
+    """Zero-copy views (images [n, h*w], labels [n]) into ``buf``."""
+    hdr = decode_header(buf)
+    n, d = hdr["n"], hdr["height"] * hdr["width"]
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    need = HEADER_SIZE + n * d + n
+    if arr.size < need:
+        raise ValueError(f"shard truncated: {arr.size} < {need}")
+    images = arr[HEADER_SIZE:HEADER_SIZE + n * d].reshape(n, d)
+    labels = arr[HEADER_SIZE + n * d:need]
+    return hdr, images, labels
+
+
+def make_shard(n: int, shard_index: int = 0, num_shards: int = 1, seed: int = 0) -> bytes:
+    images, labels = make_mnist_like(n, seed=seed * 1000003 + shard_index)
+    return encode_shard(images, labels, shard_index, num_shards, seed)

@@ -1,0 +1,350 @@
+"""The flagship model: a 3-layer MLP (784-256-256-10) on MNIST-shaped data.
+
+The reference has no model at all -- its "model" is a ``std::vector<double>``
+that ``simulate_training`` bumps by one every 2 s
+(/root/reference/src/worker.cc:221-231) and that workers mix by gossip
+(/root/reference/src/worker.cc:81-100).  This module provides the real model
+that takes its place, in three forms:
+
+* :func:`param_layout` / :func:`init_params` -- the flat fp32 parameter vector.
+  A flat vector is what travels in the reference's ``Update{repeated double
+  delta}`` message (proto :81-83), what the checkpoint format stores and what
+  the data-parallel all-reduce moves in one bucket.
+* :class:`MLP` -- a ``torch.nn.Module`` view of that vector, used on CPU
+  workers (BASELINE config 1, "plumbing, no GPU") and as the fp32 reference
+  in numerics tests.
+* :class:`FusedMLPTrainer` -- the MI355X path: three hand-written HIP kernels
+  per step (csrc/kernels/mlp_fused.hip) on bf16 MFMA with fp32 master
+  weights, optionally wrapped in a hipGraph, with an RCCL all-reduce hook.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+D_IN = 784
+D_IN_PAD = 800
+HIDDEN = 256
+CLASSES = 10
+MNIST_MEAN = 0.1307
+MNIST_STD = 0.3081
+BLOCK_ROWS = 64  # batch rows per workgroup of the fused row kernel
+
+LAYOUT = (
+    ("fc1.weight", (HIDDEN, D_IN)),
+    ("fc1.bias", (HIDDEN,)),
+    ("fc2.weight", (HIDDEN, HIDDEN)),
+    ("fc2.bias", (HIDDEN,)),
+    ("fc3.weight", (CLASSES, HIDDEN)),
+    ("fc3.bias", (CLASSES,)),
+)
+
+
+def param_layout():
+    """[(name, shape, offset, numel)] of the flat parameter vector."""
+    out, off = [], 0
+    for name, shape in LAYOUT:
+        n = math.prod(shape)
+        out.append((name, shape, off, n))
+        off += n
+    return out
+
+
+N_PARAMS = sum(math.prod(s) for _, s in LAYOUT)  # 269,322
+
+
+def norm_coeffs(mean: float = MNIST_MEAN, std: float = MNIST_STD) -> tuple[float, float]:
+    """u8 pixel p -> (p/255 - mean)/std == p*a + b."""
+    return 1.0 / (255.0 * std), -mean / std
+
+
+def init_params(seed: int = 0, device="cpu") -> torch.Tensor:
+    """nn.Linear default init (U(-1/sqrt(fan_in), 1/sqrt(fan_in))) into a flat fp32 vector."""
+    g = torch.Generator().manual_seed(seed)
+    flat = torch.empty(N_PARAMS, dtype=torch.float32)
+    for name, shape, off, n in param_layout():
+        fan_in = shape[1] if len(shape) == 2 else (D_IN if name.startswith("fc1") else HIDDEN)
+        bound = 1.0 / math.sqrt(fan_in)
+        flat[off:off + n] = (torch.rand(n, generator=g) * 2 - 1) * bound
+    return flat.to(device)
+
+
+def views(flat: torch.Tensor) -> dict:
+    return {name: flat[off:off + n].view(shape) for name, shape, off, n in param_layout()}
+
+
+def normalize(x_u8: torch.Tensor) -> torch.Tensor:
+    a, b = norm_coeffs()
+    return x_u8.float() * a + b
+
+
+class MLP(nn.Module):
+    """nn.Module over a flat parameter vector (CPU path and fp32 reference)."""
+
+    def __init__(self, flat: torch.Tensor | None = None, seed: int = 0):
+        super().__init__()
+        if flat is None:
+            flat = init_params(seed)
+        self.flat = nn.Parameter(flat.clone().float())
+
+    def forward(self, x_u8: torch.Tensor) -> torch.Tensor:
+        v = views(self.flat)
+        h = normalize(x_u8.reshape(-1, D_IN))
+        h = F.relu(F.linear(h, v["fc1.weight"], v["fc1.bias"]))
+        h = F.relu(F.linear(h, v["fc2.weight"], v["fc2.bias"]))
+        return F.linear(h, v["fc3.weight"], v["fc3.bias"])
+
+
+def reference_grads(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor,
+                    grad_scale: float | None = None):
+    """fp32 autograd reference: (loss_sum, correct, grad_flat) with dZ scaled by grad_scale."""
+    w = flat.detach().clone().float().requires_grad_(True)
+    m = MLP.__new__(MLP)
+    nn.Module.__init__(m)
+    m.flat = w
+    logits = m(x_u8)
+    losses = F.cross_entropy(logits, y.long(), reduction="none")
+    scale = grad_scale if grad_scale is not None else 1.0 / x_u8.shape[0]
+    (losses.sum() * scale).backward()
+    correct = (logits.argmax(1) == y.long()).float().sum()
+    return losses.detach().sum(), correct.detach(), w.grad.detach()
+
+
+def sgd_update(flat, mom, grad, lr, momentum, weight_decay):
+    """torch.optim.SGD semantics (dampening 0, no nesterov), in place."""
+    d = grad + weight_decay * flat
+    if mom is not None:
+        mom.mul_(momentum).add_(d)
+        d = mom
+    flat.sub_(lr * d)
+
+
+@dataclass
+class StepStats:
+    loss: float
+    accuracy: float
+    samples: int
+
+
+class CPUTrainer:
+    """Plain-torch trainer with the same interface as FusedMLPTrainer (CPU workers)."""
+
+    def __init__(self, batch: int, lr: float = 0.05, momentum: float = 0.9,
+                 weight_decay: float = 0.0, seed: int = 0, world_size: int = 1,
+                 flat: torch.Tensor | None = None):
+        self.batch = batch
+        self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
+        self.world_size = world_size
+        self.params = (flat if flat is not None else init_params(seed)).clone().float()
+        self.mom = torch.zeros_like(self.params) if momentum > 0 else None
+        self.cursor = 0
+        self.x = self.y = None
+        self.allreduce = None  # callable(tensor) -> None (sum in place)
+        self._last = None
+
+    def load_shard(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> None:
+        assert x_u8.shape[0] >= self.batch
+        self.x, self.y = x_u8.reshape(-1, D_IN), y_u8.reshape(-1)
+        self.n_batches = self.x.shape[0] // self.batch
+
+    def step(self) -> None:
+        b = self.cursor % self.n_batches
+        xs = self.x[b * self.batch:(b + 1) * self.batch]
+        ys = self.y[b * self.batch:(b + 1) * self.batch]
+        loss, correct, g = reference_grads(self.params, xs, ys, 1.0 / (self.batch * self.world_size))
+        if self.allreduce is not None:
+            self.allreduce(g)
+        sgd_update(self.params, self.mom, g, self.lr, self.momentum, self.weight_decay)
+        self.cursor += 1
+        self._last = (float(loss), float(correct))
+
+    def stats(self) -> StepStats:
+        loss, correct = self._last
+        return StepStats(loss / self.batch, correct / self.batch, self.batch)
+
+    def get_flat(self) -> torch.Tensor:
+        return self.params.clone()
+
+    def set_flat(self, flat: torch.Tensor) -> None:
+        self.params.copy_(flat.to(self.params))
+
+
+def default_slices(batch: int) -> int:
+    s = max(1, min(16, batch // 1024))
+    while s > 1 and batch % (32 * s) != 0:
+        s -= 1
+    return s
+
+
+class FusedMLPTrainer:
+    """MI355X training engine for the MLP: 3 HIP launches per step.
+
+    Buffers are allocated once for a fixed per-GPU batch; the data shard stays
+    resident in HBM and a device-side cursor selects the batch, so a step has
+    no host work and replays from a hipGraph (:meth:`capture`).
+    """
+
+    def __init__(self, batch: int, device="cuda", lr: float = 0.05, momentum: float = 0.9,
+                 weight_decay: float = 0.0, seed: int = 0, world_size: int = 1,
+                 slices: int | None = None, flat: torch.Tensor | None = None):
+        from ..ops import _native
+
+        if batch % BLOCK_ROWS != 0:
+            raise ValueError(f"batch must be a multiple of {BLOCK_ROWS}")
+        self._n = _native
+        _native.lib()  # fail loudly if the HIP library cannot be loaded
+        dev = torch.device(device)
+        self.device = dev
+        self.batch = batch
+        self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
+        self.world_size = world_size
+        self.grad_scale = 1.0 / (batch * world_size)
+        self.slices = slices or default_slices(batch)
+        self.xa, self.xb = norm_coeffs()
+        n = N_PARAMS
+        self.n_pad = (n + 3) // 4 * 4
+        self.params = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
+        init = flat if flat is not None else init_params(seed)
+        self.params[:n].copy_(init.to(dev))
+        self.mom = torch.zeros_like(self.params) if momentum > 0 else None
+        bf = torch.bfloat16
+        self.w1h = torch.zeros(HIDDEN, D_IN_PAD, dtype=bf, device=dev)
+        self.w2h = torch.zeros(HIDDEN, HIDDEN, dtype=bf, device=dev)
+        self.w2th = torch.zeros(HIDDEN, HIDDEN, dtype=bf, device=dev)
+        self.w3h = torch.zeros(16, HIDDEN, dtype=bf, device=dev)
+        self.w3th = torch.zeros(HIDDEN, 32, dtype=bf, device=dev)
+        self.h1t = torch.empty(HIDDEN, batch, dtype=bf, device=dev)
+        self.h2t = torch.empty(HIDDEN, batch, dtype=bf, device=dev)
+        self.dh1t = torch.empty(HIDDEN, batch, dtype=bf, device=dev)
+        self.dh2t = torch.empty(HIDDEN, batch, dtype=bf, device=dev)
+        self.dzt = torch.empty(16, batch, dtype=bf, device=dev)
+        self.loss = torch.zeros(batch, dtype=torch.float32, device=dev)
+        self.correct = torch.zeros(batch, dtype=torch.float32, device=dev)
+        self.slab = torch.empty(self.slices, self.n_pad, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
+        self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.allreduce = None  # callable(grad_tensor) -> None, sums in place (RCCL)
+        self.x = self.y = None
+        self.n_batches = 1
+        self.graph = None
+        self.refresh_shadows()
+
+    # ---- data ----
+    def load_shard(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> None:
+        """Make a device-resident shard current ([N,784] u8 images, [N] u8 labels)."""
+        x = x_u8.reshape(-1, D_IN)
+        if x.shape[0] < self.batch:
+            raise ValueError("shard smaller than one batch")
+        self.x = x.to(self.device, non_blocking=True).contiguous()
+        self.y = y_u8.reshape(-1).to(self.device, non_blocking=True).to(torch.uint8).contiguous()
+        self.n_batches = self.x.shape[0] // self.batch
+        self.graph = None
+
+    # ---- kernels ----
+    def refresh_shadows(self) -> None:
+        n = self._n
+        n.call("sl_mlp_sgd", n.ptr(self.params), None, None, 0, 0, None, None, 0.0, 0.0, 0.0, 0,
+               n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
+               None, n.stream_ptr())
+
+    def _rows(self, train: bool = True):
+        n = self._n
+        n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
+               n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
+               n.ptr(self.params), self.xa, self.xb, self.grad_scale,
+               n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t),
+               n.ptr(self.loss), n.ptr(self.correct), None, 1 if train else 0, n.stream_ptr())
+
+    def _wgrad(self):
+        n = self._n
+        n.call("sl_mlp_wgrad", n.ptr(self.x), n.ptr(self.cursor), self.n_batches, self.batch, self.xa, self.xb,
+               n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t),
+               n.ptr(self.slab), self.slices, self.n_pad, n.stream_ptr())
+
+    def _sgd(self, mode: int, from_grad: bool, grad_out: bool, bump: bool = True):
+        n = self._n
+        n.call("sl_mlp_sgd", n.ptr(self.params), n.ptr(self.mom),
+               None if from_grad else n.ptr(self.slab), self.slices, self.n_pad,
+               n.ptr(self.grad) if from_grad else None, n.ptr(self.grad) if grad_out else None,
+               self.lr, self.momentum, self.weight_decay, mode,
+               n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
+               n.ptr(self.cursor) if bump else None, n.stream_ptr())
+
+    def compute_grads(self) -> torch.Tensor:
+        """Forward + backward only; returns the reduced (local) gradient."""
+        self._rows(True)
+        self._wgrad()
+        self._sgd(1, from_grad=False, grad_out=True, bump=False)
+        return self.grad[:N_PARAMS]
+
+    def step(self) -> None:
+        if self.graph is not None:
+            self.graph.replay()
+            return
+        self._step_eager()
+
+    def _step_eager(self) -> None:
+        self._rows(True)
+        self._wgrad()
+        if self.allreduce is None:
+            self._sgd(2, from_grad=False, grad_out=False)
+        else:
+            self._sgd(1, from_grad=False, grad_out=True, bump=False)
+            self.allreduce(self.grad)
+            self._sgd(2, from_grad=True, grad_out=False)
+
+    def capture(self, warmup: int = 2) -> None:
+        """Capture one step into a hipGraph (kernels only, or kernels + RCCL)."""
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step_eager()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_eager()
+        self.graph = g
+
+    # ---- eval / state ----
+    def stats(self) -> StepStats:
+        loss = float(self.loss.sum())
+        acc = float(self.correct.sum())
+        return StepStats(loss / self.batch, acc / self.batch, self.batch)
+
+    def evaluate(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> StepStats:
+        n = self._n
+        x = x_u8.reshape(-1, D_IN).to(self.device).contiguous()
+        y = y_u8.reshape(-1).to(self.device).to(torch.uint8).contiguous()
+        rows = x.shape[0] // BLOCK_ROWS * BLOCK_ROWS
+        loss = torch.zeros(rows, device=self.device)
+        corr = torch.zeros(rows, device=self.device)
+        n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
+               n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
+               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None,
+               n.ptr(loss), n.ptr(corr), None, 0, n.stream_ptr())
+        return StepStats(float(loss.mean()), float(corr.mean()), rows)
+
+    def logits(self, x_u8: torch.Tensor) -> torch.Tensor:
+        n = self._n
+        x = x_u8.reshape(-1, D_IN).to(self.device).contiguous()
+        rows = x.shape[0]
+        if rows % BLOCK_ROWS:
+            raise ValueError(f"rows must be a multiple of {BLOCK_ROWS}")
+        out = torch.empty(rows, CLASSES, device=self.device)
+        n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
+               n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
+               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None,
+               None, None, n.ptr(out), 0, n.stream_ptr())
+        return out
+
+    def get_flat(self) -> torch.Tensor:
+        return self.params[:N_PARAMS].clone()
+
+    def set_flat(self, flat: torch.Tensor) -> None:
+        self.params[:N_PARAMS].copy_(flat.to(self.params))
+        self.refresh_shadows()

@@ -1,0 +1,92 @@
+"""ctypes binding of ``libslkernels.so`` (the gfx950 HIP kernels).
+
+Every launcher takes raw device pointers plus the HIP stream and returns 0 on
+success (non-zero = hipError_t or an argument error).  Launchers are cheap to
+call and are captured into hipGraphs by ``torch.cuda.graph`` because they
+launch on the caller's current stream.
+
+There is deliberately NO silent fallback: on a machine with a GPU the ops
+raise if the extension is missing or fails, so a test can never pass on an
+eager PyTorch path while claiming to exercise the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from ..build import KERNELS_SO
+
+_lock = threading.Lock()
+_lib = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+
+# name -> argtypes (restype is always c_int unless listed in _RESTYPE)
+_SIGS: dict[str, list] = {
+    "sl_mlp_param_count": [],
+    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, P, P, P, P, P, P, P, P, I, P],
+    "sl_mlp_wgrad": [P, P, I, I, F, F, P, P, P, P, P, P, I, L, P],
+    "sl_mlp_sgd": [P, P, P, I, L, P, P, F, F, F, I, P, P, P, P, P, P, P],
+}
+_RESTYPE = {"sl_mlp_param_count": ctypes.c_long}
+
+
+def register(name: str, argtypes: list, restype=ctypes.c_int) -> None:
+    """Register a launcher signature (used by the op modules at import)."""
+    _SIGS[name] = argtypes
+    if restype is not ctypes.c_int:
+        _RESTYPE[name] = restype
+    if _lib is not None:
+        _bind(_lib, name)
+
+
+def _bind(lib, name):
+    fn = getattr(lib, name)
+    fn.argtypes = _SIGS[name]
+    fn.restype = _RESTYPE.get(name, ctypes.c_int)
+
+
+def available() -> bool:
+    return os.path.exists(KERNELS_SO)
+
+
+def lib():
+    """Load (building first if needed) the kernel library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(KERNELS_SO):
+                from ..build import build_kernels
+
+                build_kernels()
+            handle = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
+            for name in _SIGS:
+                _bind(handle, name)
+            _lib = handle
+    return _lib
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None passes a NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")

@@ -1,0 +1,96 @@
+"""Numerics of the fused MLP HIP kernels vs a plain PyTorch fp32 reference."""
+import pytest
+import torch
+
+from serverless_learn_amd.data.synthetic import make_mnist_like
+from serverless_learn_amd.models import mlp as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, seed=0):
+    x, y = make_mnist_like(n, seed=seed)
+    return torch.from_numpy(x), torch.from_numpy(y)
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+def test_logits_match_reference():
+    x, y = _data(256)
+    flat = M.init_params(1)
+    tr = M.FusedMLPTrainer(batch=256, flat=flat)
+    got = tr.logits(x).cpu()
+    ref = M.MLP(flat)(x).detach()
+    assert _rel(got, ref) < 3e-2, _rel(got, ref)
+    assert (got.argmax(1) == ref.argmax(1)).float().mean() > 0.97
+
+
+@pytest.mark.parametrize("batch", [64, 512, 2048])
+def test_gradients_match_reference(batch):
+    x, y = _data(batch, seed=3)
+    flat = M.init_params(2)
+    tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
+    tr.load_shard(x, y)
+    g = tr.compute_grads().cpu()
+    torch.cuda.synchronize()
+    loss, correct, gref = M.reference_grads(flat, x, y, 1.0 / batch)
+    for name, shape, off, n in M.param_layout():
+        a, b = g[off:off + n], gref[off:off + n]
+        cos = torch.nn.functional.cosine_similarity(a, b, dim=0)
+        assert cos > 0.995, (name, float(cos))
+        assert _rel(a, b) < 5e-2, (name, _rel(a, b))
+    st = tr.stats()
+    assert abs(st.loss - float(loss) / batch) < 2e-2
+    assert abs(st.accuracy - float(correct) / batch) < 0.05
+
+
+def test_sgd_step_matches_reference():
+    batch = 512
+    x, y = _data(batch, seed=5)
+    flat = M.init_params(4)
+    tr = M.FusedMLPTrainer(batch=batch, flat=flat, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    tr.load_shard(x, y)
+    tr.step()
+    got = tr.get_flat().cpu()
+    _, _, gref = M.reference_grads(flat, x, y, 1.0 / batch)
+    ref = flat.clone()
+    mom = torch.zeros_like(ref)
+    M.sgd_update(ref, mom, gref, 0.1, 0.9, 1e-4)
+    delta_got, delta_ref = got - flat, ref - flat
+    cos = torch.nn.functional.cosine_similarity(delta_got, delta_ref, dim=0)
+    assert cos > 0.995, float(cos)
+    assert int(tr.cursor.item()) == 1
+
+
+def test_cursor_walks_batches_and_training_converges():
+    batch = 1024
+    x, y = _data(batch * 4, seed=7)
+    tr = M.FusedMLPTrainer(batch=batch, lr=0.05, momentum=0.9)
+    tr.load_shard(x, y)
+    tr.step()
+    first = tr.stats().loss
+    for _ in range(60):
+        tr.step()
+    last = tr.stats()
+    assert last.loss < first * 0.5, (first, last.loss)
+    assert last.accuracy > 0.8
+    ev = tr.evaluate(*_data(1024, seed=99))
+    assert ev.accuracy > 0.7
+
+
+def test_graph_replay_equals_eager():
+    batch = 1024
+    x, y = _data(batch * 2, seed=11)
+    flat = M.init_params(9)
+    a = M.FusedMLPTrainer(batch=batch, flat=flat)
+    b = M.FusedMLPTrainer(batch=batch, flat=flat)
+    a.load_shard(x, y)
+    b.load_shard(x, y)
+    b.capture(warmup=0)
+    for _ in range(5):
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.get_flat(), b.get_flat())
