@@ -114,6 +114,34 @@ def reference_grads(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor,
     return losses.detach().sum(), correct.detach(), w.grad.detach()
 
 
+def reference_grads_bf16(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor, grad_scale: float):
+    """fp32 math with bf16 rounding at exactly the points the fused kernels round.
+
+    A tight check of csrc/kernels/mlp_fused.hip: any indexing/layout bug shows
+    up as an O(1) error, while legitimate differences are fp32 summation order.
+    Returns (loss_sum, correct, grad_flat).
+    """
+    r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    v = {k: t.detach().float() for k, t in views(flat).items()}
+    a, b = norm_coeffs()
+    xn = r(x_u8.reshape(-1, D_IN).float() * a + b)
+    w1, w2, w3 = r(v["fc1.weight"]), r(v["fc2.weight"]), r(v["fc3.weight"])
+    p1 = xn @ w1.t() + v["fc1.bias"]
+    h1 = r(torch.relu(p1))
+    p2 = h1 @ w2.t() + v["fc2.bias"]
+    h2 = r(torch.relu(p2))
+    z = h2 @ w3.t() + v["fc3.bias"]
+    yl = y.reshape(-1).long()
+    losses = torch.logsumexp(z, 1) - z.gather(1, yl[:, None])[:, 0]
+    dz = r((torch.softmax(z, 1) - F.one_hot(yl, CLASSES).float()) * grad_scale)
+    dh2 = r((dz @ w3) * (p2 > 0).float())
+    dh1 = r((dh2 @ w2) * (p1 > 0).float())
+    g = torch.cat([(dh1.t() @ xn).reshape(-1), dh1.sum(0), (dh2.t() @ h1).reshape(-1), dh2.sum(0),
+                   (dz.t() @ h2).reshape(-1), dz.sum(0)])
+    correct = (z.argmax(1) == yl).float().sum()
+    return losses.sum(), correct, g
+
+
 def sgd_update(flat, mom, grad, lr, momentum, weight_decay):
     """torch.optim.SGD semantics (dampening 0, no nesterov), in place."""
     d = grad + weight_decay * flat
