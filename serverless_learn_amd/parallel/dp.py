@@ -1,0 +1,245 @@
+"""Synchronous data parallelism over RCCL (new).
+
+The reference only mixes models by RPC gossip every 5 s.  Inside a node this
+framework aggregates gradients every step with an all-reduce over xGMI:
+``torch.distributed`` with backend ``"nccl"``, which on ROCm IS RCCL (one
+process per GPU).  CPU workers use ``"gloo"`` with identical semantics, which
+is how the multi-process logic is tested without a GPU.
+
+:class:`ElasticGroup` forms and re-forms the group from the membership the
+master disseminates in ``PeerList`` (epoch, rank, world size, rendezvous
+address of the master-hosted TCPStore).  Every epoch uses its own key prefix
+in the store, so only workers that agree on the epoch ever meet; a failed or
+timed-out rendezvous/collective marks the group broken and the worker waits
+for the next epoch (join/leave/eviction all bump it).  After a re-form, rank 0
+-- the longest-lived member, ranks follow join order -- broadcasts the model
+and optimizer state.
+
+:class:`GradBucketer` implements bucketed, backward-overlapped all-reduce for
+models with many parameter tensors (the ResNet-18-shaped CNN): gradients are
+packed into flat buckets as autograd produces them and each full bucket's
+all-reduce is launched asynchronously while backward continues.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import threading
+
+import torch
+import torch.distributed as dist
+
+from ..utils.log import Logger
+
+
+class GroupBroken(RuntimeError):
+    pass
+
+
+class ElasticGroup:
+    """A re-formable process group object (not torch's global default group).
+
+    Using the backend classes directly (``ProcessGroupNCCL`` = RCCL on ROCm,
+    ``ProcessGroupGloo`` on CPU) lets a worker drop a broken communicator and
+    build the next epoch's without touching global state -- and lets several
+    in-process workers (tests) each own a group.
+    """
+
+    def __init__(self, backend: str | None = None, device: torch.device | None = None, timeout_s: float = 60.0):
+        self.device = device or torch.device("cpu")
+        self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+        self.timeout = datetime.timedelta(seconds=timeout_s)
+        self.epoch = -1
+        self.rank = -1
+        self.world = 0
+        self.pg = None
+        self.broken = False
+        self.lock = threading.Lock()
+        self.log = Logger("dp")
+        self._stores = {}
+
+    @property
+    def active(self) -> bool:
+        return self.pg is not None
+
+    def _store(self, rendezvous: str):
+        st = self._stores.get(rendezvous)
+        if st is None:
+            host, port = rendezvous.rsplit(":", 1)
+            st = dist.TCPStore(host, int(port), is_master=False, timeout=self.timeout)
+            self._stores[rendezvous] = st
+        return st
+
+    def teardown(self) -> None:
+        pg, self.pg = self.pg, None
+        if pg is not None and self.backend == "nccl":
+            try:
+                pg.abort()  # ncclCommAbort: never block on a dead peer
+            except Exception as e:
+                self.log.warn("abort_failed", error=repr(e))
+
+    def reform(self, epoch: int, rank: int, world: int, rendezvous: str) -> bool:
+        """Join the group for ``epoch``. Returns True when the group is usable."""
+        with self.lock:
+            self.teardown()
+            self.epoch, self.rank, self.world = epoch, rank, world
+            self.broken = False
+            if world <= 1 or rank < 0 or not rendezvous:
+                return True  # single worker: nothing to reduce
+            try:
+                store = dist.PrefixStore(f"sl/epoch{epoch}", self._store(rendezvous))
+                if self.backend == "nccl":
+                    opts = dist.ProcessGroupNCCL.Options()
+                    opts._timeout = self.timeout
+                    pg = dist.ProcessGroupNCCL(store, rank, world, opts)
+                    pg.eager_connect_single_device(self.device)
+                else:
+                    pg = dist.ProcessGroupGloo(store, rank, world, self.timeout)
+                self.pg = pg
+                self.log.info("group_formed", epoch=epoch, rank=rank, world=world, backend=self.backend)
+                return True
+            except Exception as e:
+                self.broken = True
+                self.log.warn("group_form_failed", epoch=epoch, rank=rank, world=world, error=repr(e))
+                self.teardown()
+                return False
+
+    # ---- collectives -----------------------------------------------------
+    def _run(self, work) -> None:
+        try:
+            work.wait()
+        except Exception as e:
+            self.broken = True
+            raise GroupBroken(repr(e)) from e
+
+    def allreduce_(self, t: torch.Tensor, op=None) -> None:
+        if self.pg is None:
+            return
+        try:
+            if op is None:
+                work = self.pg.allreduce([t])
+            else:
+                o = dist.AllreduceOptions()
+                o.reduceOp = op
+                work = self.pg.allreduce([t], o)
+        except Exception as e:
+            self.broken = True
+            raise GroupBroken(repr(e)) from e
+        self._run(work)
+
+    def allreduce_async(self, t: torch.Tensor):
+        if self.pg is None:
+            return None
+        return self.pg.allreduce([t])
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
+        if self.pg is None:
+            return
+        o = dist.BroadcastOptions()
+        o.rootRank = src
+        try:
+            work = self.pg.broadcast([t], o)
+        except Exception as e:
+            self.broken = True
+            raise GroupBroken(repr(e)) from e
+        self._run(work)
+
+    def sync_state(self, tensors: list[torch.Tensor]) -> None:
+        """Rank 0 broadcasts model/optimizer state to every member (N2)."""
+        for t in tensors:
+            if t is not None:
+                self.broadcast_(t, 0)
+
+
+class GradBucketer:
+    """Bucketed all-reduce overlapped with backward (for multi-tensor models).
+
+    Buckets are filled in reverse registration order (the order autograd
+    produces gradients); ``bucket_bytes`` defaults to 8 MiB -- large enough
+    that each RCCL call runs at link bandwidth on xGMI (ring per-link bound,
+    SURVEY.md §5.8b), small enough that ResNet-18's ~45 MB of gradients form
+    several buckets whose all-reduce hides behind the remaining backward.
+    """
+
+    def __init__(self, params: list[torch.Tensor], group: ElasticGroup, bucket_bytes: int = 8 << 20,
+                 world_size: int = 1):
+        self.group = group
+        self.params = [p for p in params if p.requires_grad]
+        self.world_size = world_size
+        self.buckets: list[list[torch.Tensor]] = []
+        cur, size = [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            size += p.numel() * 4
+            if size >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.flat = [torch.zeros(sum(p.numel() for p in b), dtype=torch.float32, device=b[0].device)
+                     for b in self.buckets]
+        self._index = {}
+        for bi, b in enumerate(self.buckets):
+            off = 0
+            for p in b:
+                self._index[id(p)] = (bi, off)
+                off += p.numel()
+        self._pending = [0] * len(self.buckets)
+        self._works = []
+        self._hooks = []
+        self.comm_stream = torch.cuda.Stream(device=self.flat[0].device) if self.flat and self.flat[0].is_cuda else None
+
+    def attach(self) -> None:
+        for p in self.params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def detach(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+
+    def begin_step(self) -> None:
+        self._pending = [len(b) for b in self.buckets]
+        self._works = []
+
+    def _on_grad(self, p: torch.Tensor) -> None:
+        bi, off = self._index[id(p)]
+        self.flat[bi][off:off + p.numel()].copy_(p.grad.reshape(-1))
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self._launch(bi)
+
+    def _launch(self, bi: int) -> None:
+        if not self.group.active:
+            return
+        if self.comm_stream is not None:
+            self.comm_stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.comm_stream):
+                work = self.group.allreduce_async(self.flat[bi])
+        else:
+            work = self.group.allreduce_async(self.flat[bi])
+        self._works.append((bi, work))
+
+    def finish(self) -> None:
+        """Wait for every bucket and scatter the averaged gradients back."""
+        for bi, w in self._works:
+            try:
+                w.wait()
+            except Exception as e:
+                self.group.broken = True
+                raise GroupBroken(repr(e)) from e
+        if self.comm_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+        inv = 1.0 / max(1, self.world_size)
+        for bi, b in enumerate(self.buckets):
+            off = 0
+            for p in b:
+                n = p.numel()
+                p.grad.copy_(self.flat[bi][off:off + n].view_as(p.grad)).mul_(inv)
+                off += n
+
+
+def env_world() -> tuple[int, int, int]:
+    """(rank, local_rank, world) from torchrun-style environment variables."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))

@@ -1,0 +1,445 @@
+"""The worker: ingest, train, heartbeat, gossip -- an ephemeral member.
+
+Reference (/root/reference/src/worker.cc, 258 LoC): ``worker ADDR`` starts its
+gRPC service, a gossip thread (which divides by zero before any peer list
+arrives, :200/:244), a "training" thread that bumps an empty vector every 2 s
+(:221-231), then registers once without retry (:249-252).  ``ReceiveFile``
+reads and discards every chunk (:49-61); ``CheckUp`` overwrites the peer list
+(:64-77); ``ExchangeUpdates`` mixes the model (:81-100) -- all unsynchronized.
+
+Here a worker:
+* registers with retry/backoff, carrying an incarnation id (restart detection)
+  and its GPU count;
+* lands ``ReceiveFile`` chunks through the native pinned ring straight into
+  HBM (data shards) or host memory (checkpoints), then swaps the resident
+  shard into the trainer at a step boundary;
+* trains the real model: the fused HIP MLP on MI355X (FusedMLPTrainer) or the
+  torch reference on CPU, or -- ``model="simulate"`` -- the reference's
+  vector += 1 every ``simulated_train_interval_ms``;
+* synchronizes per ``sync``: ``allreduce`` (RCCL/gloo group re-formed from the
+  master's membership epochs, rank 0 broadcasting state after every re-form),
+  ``gossip`` (exact reference exchange, random peer, never % 0), ``ps`` (the
+  master's parameter server) or ``none``;
+* answers ``CheckUp`` with real feedback (step, samples/s, loss, bytes, epoch)
+  and checkpoints to the file server every ``checkpoint_every`` steps (rank 0).
+"""
+from __future__ import annotations
+
+import os
+import random
+import socket
+import threading
+import time
+
+import numpy as np
+import torch
+
+from .._core import core
+from ..ckpt import format as ckfmt
+from ..config import Config
+from ..data.synthetic import HEADER_SIZE, MAGIC as SHARD_MAGIC, decode_header
+from ..models import mlp as M
+from ..parallel.dp import ElasticGroup, GroupBroken
+from ..parallel.gossip import GossipState
+from ..proto import messages as pb
+from ..utils import trace
+from ..utils.fault import FaultInjector
+from ..utils.log import Logger
+from ..wire.codec import chunk_payload, decode_update, encode_update, iter_chunks
+from .file_server import FILE_NUM_MD, FILE_SIZE_MD
+from .transport import Channels, RpcFailure, RpcServer, metadata_dict
+
+
+# RCCL: a collective timeout must raise (so the group can re-form) rather than
+# tear the worker down -- the default handler aborts the process.
+os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+
+
+def resolve_device(spec: str) -> torch.device:
+    if spec == "auto":
+        return torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    return torch.device(spec)
+
+
+class Worker:
+    def __init__(self, addr: str, config: Config | None = None):
+        self.cfg = config or Config.from_env()
+        self.addr_requested = addr
+        self.addr = addr
+        self.log = Logger("worker", addr)
+        self.incarnation = (time.time_ns() ^ (os.getpid() << 20) ^ random.getrandbits(40)) & ((1 << 63) - 1)
+        self.device = resolve_device(self.cfg.device)
+        self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
+        self.fault = FaultInjector.from_env()
+        self.train_lock = threading.RLock()
+        self.view_lock = threading.Lock()
+        self.view = {"epoch": 0, "peers": [], "rank": -1, "world": 0, "rendezvous": "", "resume_file": 0}
+        self.trainer = None
+        self.gossip: GossipState | None = None
+        self.group = ElasticGroup(device=self.device, timeout_s=float(self.cfg.extra.get("dp_timeout_s", 30.0)))
+        self.step = 0
+        self.samples = 0
+        self.loss = float("nan")
+        self.rate = 0.0
+        self.bytes_ingested = 0
+        self.files_received: list[int] = []
+        self.state = "idle"
+        self.registered = threading.Event()
+        self.has_data = threading.Event()
+        self._pending_shard = None
+        self._stop = threading.Event()
+        self._threads: list[threading.Thread] = []
+        dev_index = self.device.index if self.device.type == "cuda" else -1
+        self.ring = core().IngestRing(4 << 20, 4, dev_index if dev_index is not None else 0)
+        self.ring_lock = threading.Lock()  # one transfer through the ring at a time
+        self.server: RpcServer | None = None
+        self.ckpt_slot = 0
+        if self.cfg.model == "simulate":
+            # the reference's model: an empty vector of doubles, grown by gossip
+            self.gossip = GossipState(torch.zeros(0, dtype=torch.float64), self.cfg.learn_rate,
+                                      self.cfg.gossip_compat, growable=True)
+
+    # ---- model -------------------------------------------------------------
+    def _ensure_trainer(self):
+        if self.trainer is not None or self.cfg.model == "simulate":
+            return
+        world = max(1, self.view["world"]) if self.cfg.sync == "allreduce" else 1
+        kw = dict(batch=self.cfg.batch, lr=self.cfg.lr, momentum=self.cfg.momentum,
+                  weight_decay=self.cfg.weight_decay, seed=self.cfg.seed, world_size=world)
+        if self.device.type == "cuda":
+            self.trainer = M.FusedMLPTrainer(device=self.device, **kw)
+        else:
+            self.trainer = M.CPUTrainer(**kw)
+        if self.cfg.sync in ("gossip", "ps"):
+            self.gossip = GossipState(self._flat_view(), self.cfg.learn_rate, self.cfg.gossip_compat)
+
+    def _flat_view(self) -> torch.Tensor:
+        return self.trainer.params[:M.N_PARAMS]
+
+    def _after_external_update(self):
+        if isinstance(self.trainer, M.FusedMLPTrainer):
+            self.trainer.refresh_shadows()
+
+    def _set_world(self, world: int):
+        """Gradient scale follows the group size (mean over the global batch)."""
+        t = self.trainer
+        if t is None:
+            return
+        t.world_size = world
+        if isinstance(t, M.FusedMLPTrainer):
+            t.grad_scale = 1.0 / (t.batch * world)
+            t.graph = None
+
+    # ---- RPC handlers --------------------------------------------------------
+    def _receive_file(self, requests, context) -> bytes:
+        md = metadata_dict(context)
+        file_num = int(md.get(FILE_NUM_MD, "0"))
+        size = int(md.get(FILE_SIZE_MD, "-1"))
+        t0 = time.perf_counter()
+        with self.ring_lock, trace.span("ingest", file_num=file_num):
+            it = iter(requests)
+            first = next(it, None)
+            if first is None:
+                return pb.ReceiveFileAck(ok=False).SerializeToString()
+            head = bytes(chunk_payload(first)[:HEADER_SIZE])
+            is_shard = head[:8] == SHARD_MAGIC
+            try:
+                if is_shard and size > 0 and self.device.type == "cuda":
+                    buf = torch.empty(size, dtype=torch.uint8, device=self.device)
+                    self.ring.begin(buf.data_ptr(), size, True)
+                    self.ring.feed_chunk(first)
+                    for msg in it:
+                        self.ring.feed_chunk(msg)
+                    got = self.ring.finish()
+                elif size > 0:
+                    arr = np.empty(size, dtype=np.uint8)
+                    self.ring.begin(arr.ctypes.data, size, False)
+                    self.ring.feed_chunk(first)
+                    for msg in it:
+                        self.ring.feed_chunk(msg)
+                    got = self.ring.finish()
+                    buf = arr
+                else:  # a reference-style sender: no size metadata
+                    parts = [bytes(chunk_payload(first))] + [bytes(chunk_payload(m)) for m in it]
+                    buf = np.frombuffer(b"".join(parts), dtype=np.uint8)
+                    got = buf.size
+            except Exception as e:
+                self.log.warn("ingest_failed", file_num=file_num, error=repr(e))
+                return pb.ReceiveFileAck(ok=False).SerializeToString()
+        dt = time.perf_counter() - t0
+        self.bytes_ingested += got
+        self.files_received.append(file_num)
+        kind = "data"
+        if is_shard:
+            hdr = decode_header(head)
+            n, d = hdr["n"], hdr["height"] * hdr["width"]
+            if isinstance(buf, np.ndarray):
+                buf = torch.from_numpy(buf)
+            x = buf[HEADER_SIZE:HEADER_SIZE + n * d].view(n, d)
+            y = buf[HEADER_SIZE + n * d:HEADER_SIZE + n * d + n]
+            with self.train_lock:
+                self._pending_shard = (x, y, file_num)
+            self.has_data.set()
+            kind = "shard"
+        elif ckfmt.looks_like_checkpoint(buf[:8].tobytes() if isinstance(buf, np.ndarray) else b""):
+            self._load_checkpoint(buf.tobytes())
+            kind = "checkpoint"
+        # else: opaque bytes (e.g. the reference dummy file) -- counted, then dropped, as worker.cc:54-56
+        self.log.info("received_file", file_num=file_num, kind=kind, bytes=got, s=round(dt, 4),
+                      mb_s=round(got / dt / 1e6, 1) if dt > 0 else 0, pinned=self.ring.pinned)
+        return pb.ReceiveFileAck(ok=True).SerializeToString()
+
+    def _check_up(self, request: bytes, context) -> bytes:
+        pl = pb.PeerList.FromString(request)
+        with self.view_lock:
+            self.view = {"epoch": pl.epoch, "peers": list(pl.peer_addrs), "rank": pl.rank,
+                         "world": pl.world_size, "rendezvous": pl.rendezvous, "resume_file": pl.resume_file}
+        fb = pb.FlowFeedback(step=self.step, samples_per_sec=self.rate,
+                             loss=self.loss if self.loss == self.loss else 0.0,
+                             bytes_ingested=self.bytes_ingested, epoch=self.group.epoch if self.group.epoch >= 0 else 0,
+                             state=self.state)
+        return fb.SerializeToString()
+
+    def _exchange_updates(self, request: bytes, context) -> bytes:
+        delta = decode_update(request, "float64")
+        with self.train_lock:
+            if self.gossip is None:
+                self._ensure_trainer()
+            if self.gossip is None:  # allreduce/none worker asked to gossip: mix anyway
+                self.gossip = GossipState(self._flat_view(), self.cfg.learn_rate, self.cfg.gossip_compat)
+            with trace.span("gossip_serve", n=int(delta.size)):
+                reply = self.gossip.serve(delta)
+            self._after_external_update()
+        return encode_update(reply)
+
+    # ---- checkpoints -----------------------------------------------------------
+    def _load_checkpoint(self, data: bytes) -> None:
+        meta, params, mom = ckfmt.decode(data)
+        with self.train_lock:
+            self._ensure_trainer()
+            if self.trainer is None:
+                return
+            if meta.get("step", 0) < self.step:
+                self.log.info("checkpoint_skipped", ckpt_step=meta.get("step"), step=self.step)
+                return
+            self.trainer.set_flat(torch.from_numpy(params))
+            if mom is not None and self.trainer.mom is not None:
+                self.trainer.mom[:M.N_PARAMS].copy_(torch.from_numpy(mom))
+            self.step = int(meta.get("step", 0))
+            if self.gossip is not None:
+                self.gossip.old.copy_(self._flat_view())
+        self.log.info("checkpoint_loaded", step=self.step, epoch=meta.get("epoch"))
+
+    def save_checkpoint(self) -> int:
+        with self.train_lock:
+            flat = self.trainer.get_flat().cpu().numpy()
+            mom = self.trainer.mom[:M.N_PARAMS].cpu().numpy() if self.trainer.mom is not None else None
+            meta = {"model": "mlp-784-256-256-10", "step": self.step, "epoch": self.group.epoch,
+                    "layout": [[n, list(s), o] for n, s, o, _ in M.param_layout()],
+                    "optimizer": {"lr": self.cfg.lr, "momentum": self.cfg.momentum}}
+        data = ckfmt.encode(flat, meta, mom)
+        file_num = ckfmt.CKPT_BASE + self.ckpt_slot
+        self.ckpt_slot ^= 1  # two alternating slots: never overwrite one being served
+        raw = self.channels.stream_unary(self.cfg.file_server_addr, "FileStore", "StoreFile", iter_chunks(data),
+                                         timeout=max(10.0, self.cfg.rpc_timeout_s),
+                                         metadata=((FILE_NUM_MD, str(file_num)),))
+        if not pb.PushOutcome.FromString(raw).ok:
+            raise RuntimeError("checkpoint upload rejected")
+        self.channels.unary(self.cfg.master_addr, "MasterControl", "ReportCheckpoint",
+                            pb.Push(recipient_addr=self.addr, file_num=file_num).SerializeToString())
+        self.log.info("checkpoint_saved", step=self.step, file_num=file_num, bytes=len(data))
+        return file_num
+
+    # ---- loops -------------------------------------------------------------------
+    def _register_loop(self) -> None:
+        delay = 0.1
+        info = pb.WorkerBirthInfo(addr=self.addr, num_gpus=1 if self.device.type == "cuda" else 0,
+                                  hostname=socket.gethostname(), incarnation=self.incarnation)
+        while not self._stop.is_set():
+            try:
+                raw = self.channels.unary(self.cfg.master_addr, "Master", "RegisterBirth", info.SerializeToString())
+                if pb.RegisterBirthAck.FromString(raw).ok:
+                    self.registered.set()
+                    self.log.info("registered", master=self.cfg.master_addr)
+                    return
+            except RpcFailure as e:
+                self.log.warn("register_retry", error=e.code.name if e.code else "", delay=delay)
+            self._stop.wait(delay)
+            delay = min(delay * 2, 5.0)
+
+    def _maybe_regroup(self) -> None:
+        with self.view_lock:
+            v = dict(self.view)
+        if v["epoch"] == 0 or v["rank"] < 0:
+            return
+        if v["epoch"] == self.group.epoch and not self.group.broken:
+            return
+        self.state = "regrouping"
+        with trace.span("regroup", epoch=v["epoch"], world=v["world"]):
+            ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"])
+            if not ok:
+                self._stop.wait(0.2)
+                return
+            self._set_world(max(1, v["world"]))
+            if self.trainer is not None and self.group.active:
+                t = self.trainer
+                try:
+                    self.group.sync_state([t.params, t.mom])
+                    step = torch.tensor([self.step], dtype=torch.int64, device=t.params.device)
+                    self.group.broadcast_(step, 0)
+                    self.step = int(step.item())
+                except GroupBroken as e:
+                    self.log.warn("state_sync_failed", error=str(e))
+                    return
+                self._after_external_update()
+                t.allreduce = self.group.allreduce_
+            elif self.trainer is not None:
+                self.trainer.allreduce = None
+        self.state = "training"
+
+    def _train_loop(self) -> None:
+        if self.cfg.model == "simulate":
+            return self._simulate_loop()
+        t_last, s_last = time.perf_counter(), 0
+        ready_epoch = -1
+        while not self._stop.is_set():
+            with self.train_lock:
+                if self._pending_shard is not None:
+                    self._ensure_trainer()
+                    x, y, fnum = self._pending_shard
+                    self._pending_shard = None
+                    self.trainer.load_shard(x, y)
+                    self.log.info("shard_loaded", file_num=fnum, records=int(x.shape[0]))
+            have_data = self.trainer is not None and self.trainer.x is not None
+            if self.cfg.sync == "allreduce":
+                self._maybe_regroup()
+                if self.view["world"] > 1:
+                    if not self.group.active:
+                        self._stop.wait(0.05)
+                        continue
+                    if ready_epoch != self.group.epoch:
+                        # every member must have data before the first lock-step collective
+                        flag = torch.ones(1) if have_data else torch.zeros(1)
+                        if self.group.backend == "nccl":
+                            flag = flag.to(self.device)
+                        try:
+                            self.group.allreduce_(flag)
+                        except GroupBroken:
+                            continue
+                        if int(flag.item()) == self.group.world:
+                            ready_epoch = self.group.epoch
+                        else:
+                            self.state = "waiting_for_data"
+                            self._stop.wait(0.1)
+                            continue
+            if not have_data:
+                self.state = "idle"
+                self.has_data.wait(0.2)
+                self.has_data.clear()
+                continue
+            try:
+                with self.train_lock, trace.span("step", step=self.step):
+                    self.trainer.step()
+            except GroupBroken as e:
+                self.log.warn("collective_failed", error=str(e), epoch=self.group.epoch)
+                continue
+            self.step += 1
+            self.samples += self.trainer.batch
+            self.state = "training"
+            self.fault.on_step(self.step)
+            if self.cfg.log_every and self.step % self.cfg.log_every == 0:
+                st = self.trainer.stats()
+                now = time.perf_counter()
+                self.rate = (self.samples - s_last) / max(1e-9, now - t_last)
+                t_last, s_last = now, self.samples
+                self.loss = st.loss
+                self.log.info("train", step=self.step, loss=round(st.loss, 4), acc=round(st.accuracy, 4),
+                              samples_per_sec=round(self.rate, 1), epoch=self.group.epoch)
+            if (self.cfg.checkpoint_every and self.step % self.cfg.checkpoint_every == 0
+                    and (self.group.rank <= 0)):
+                try:
+                    self.save_checkpoint()
+                except Exception as e:
+                    self.log.warn("checkpoint_failed", error=repr(e))
+            if self.cfg.max_steps and self.step >= self.cfg.max_steps:
+                self.state = "done"
+                return
+
+    def _simulate_loop(self) -> None:
+        """The reference's training: every model element += 1 every 2 s (worker.cc:221-231)."""
+        while not self._stop.wait(self.cfg.simulated_train_interval_ms / 1000.0):
+            with self.gossip.lock:
+                self.gossip.model += 1.0
+            self.step += 1
+
+    def _gossip_loop(self) -> None:
+        while not self._stop.wait(self.cfg.gossip_interval):
+            self.gossip_once()
+
+    def gossip_once(self) -> bool:
+        """One exchange with a random peer (or the master for sync=ps). False if nothing to do."""
+        if self.gossip is None:
+            return False
+        if self.cfg.sync == "ps":
+            target, service = self.cfg.master_addr, "Master"
+        else:
+            with self.view_lock:
+                peers = [p for p in self.view["peers"] if p != self.addr]
+            if not peers:  # the reference computes rand() % 0 here (worker.cc:200)
+                return False
+            target, service = random.choice(peers), "Worker"
+        with trace.span("gossip", peer=target):
+            with self.train_lock:
+                delta = self.gossip.make_delta()
+            try:
+                raw = self.channels.unary(target, service, "ExchangeUpdates", encode_update(delta))
+            except RpcFailure as e:  # the reference applies the reply even on failure (worker.cc:153-165)
+                self.log.warn("gossip_failed", peer=target, error=e.code.name if e.code else "")
+                return False
+            reply = decode_update(raw, "float64")
+            with self.train_lock:
+                self.gossip.absorb(reply, delta)
+                self._after_external_update()
+        return True
+
+    # ---- lifecycle ---------------------------------------------------------------
+    def start(self) -> "Worker":
+        self.server = RpcServer(self.addr_requested, max_workers=16, max_message_bytes=self.cfg.max_message_bytes)
+        handlers = {"ReceiveFile": self._receive_file, "CheckUp": self._check_up,
+                    "ExchangeUpdates": self._exchange_updates}
+        self.server.add_service("Worker", {k: self.fault.wrap(k, v) for k, v in handlers.items()})
+        self.server.start()
+        self.addr = self.server.addr
+        self.log.addr = self.addr
+        loops = [self._register_loop, self._train_loop]
+        if self.cfg.sync in ("gossip", "ps") or self.cfg.model == "simulate":
+            loops.append(self._gossip_loop)
+        for fn in loops:
+            t = threading.Thread(target=fn, daemon=True, name="sl-worker-" + fn.__name__)
+            t.start()
+            self._threads.append(t)
+        self.log.info("serving", device=str(self.device), sync=self.cfg.sync, model=self.cfg.model)
+        return self
+
+    def leave(self) -> None:
+        """Graceful departure: deregister so the group re-forms immediately."""
+        try:
+            self.channels.unary(self.cfg.master_addr, "MasterControl", "Deregister",
+                                pb.WorkerBirthInfo(addr=self.addr, incarnation=self.incarnation).SerializeToString())
+        except RpcFailure:
+            pass
+
+    def stop(self, leave: bool = True) -> None:
+        if leave:
+            self.leave()
+        self._stop.set()
+        self.has_data.set()
+        for t in self._threads:
+            t.join(timeout=10)
+        self.group.teardown()
+        if self.server:
+            self.server.stop()
+        self.channels.close()
+
+    def wait(self) -> None:
+        self.server.wait()

@@ -1,0 +1,73 @@
+"""End-to-end plumbing on CPU (BASELINE config 1) plus elastic behaviour."""
+import numpy as np
+import pytest
+import torch
+
+from serverless_learn_amd.runtime.local_cluster import LocalCluster, fast_config
+
+pytestmark = pytest.mark.slow
+
+
+@pytest.fixture
+def cluster(request):
+    kw = getattr(request, "param", {})
+    c = LocalCluster(fast_config(**kw))
+    yield c
+    c.stop()
+
+
+def test_single_worker_registers_ingests_and_trains(cluster):
+    w = cluster.add_worker(sync="none")
+    assert cluster.wait_for(lambda: w.registered.is_set(), 10)
+    assert cluster.wait_for(lambda: w.step >= 40, 60), w.step
+    assert 0 in w.files_received and w.bytes_ingested > 0
+    assert cluster.wait_for(lambda: w.addr in cluster.master.feedback and cluster.master.feedback[w.addr]["step"] > 0, 10)
+    st = w.trainer.stats()
+    assert st.accuracy > 0.5, st
+
+
+def test_allreduce_workers_stay_identical(cluster):
+    a = cluster.add_worker(sync="allreduce", batch=512, max_steps=150)
+    b = cluster.add_worker(sync="allreduce", batch=512, max_steps=150)
+    assert cluster.wait_for(lambda: a.state == "done" and b.state == "done", 120), (a.step, b.step, a.state, b.state)
+    assert a.step == b.step == 150
+    assert a.group.world == 2 and b.group.world == 2
+    assert torch.equal(a.trainer.params, b.trainer.params)
+    # distinct shards per rank
+    assert set(a.files_received) != set(b.files_received) or len(a.files_received) > 1
+
+
+def test_eviction_bumps_epoch_and_survivors_regroup(cluster):
+    ws = [cluster.add_worker(sync="allreduce", batch=256) for _ in range(3)]
+    assert cluster.wait_for(lambda: all(w.group.world == 3 and w.step > 20 for w in ws), 60), \
+        [(w.group.world, w.step) for w in ws]
+    victim = ws[2]
+    epoch_before = cluster.master.registry.epoch()
+    victim.fault.kill_step = None
+    victim._stop.set()
+    victim.server.stop(grace=0)  # crash: no Deregister
+    survivors = ws[:2]
+    assert cluster.wait_for(lambda: cluster.master.registry.epoch() > epoch_before, 20)
+    assert victim.addr not in cluster.master.registry.members()
+    steps = [w.step for w in survivors]
+    assert cluster.wait_for(lambda: all(w.group.world == 2 for w in survivors), 60), \
+        [(w.group.world, w.group.epoch, w.state) for w in survivors]
+    assert cluster.wait_for(lambda: all(w.step > s + 20 for w, s in zip(survivors, steps)), 60)
+
+
+def test_gossip_workers_exchange(cluster):
+    a = cluster.add_worker(sync="gossip")
+    b = cluster.add_worker(sync="gossip")
+    assert cluster.wait_for(lambda: a.gossip is not None and b.gossip is not None
+                            and a.gossip.exchanges + b.gossip.exchanges >= 6, 60)
+    assert a.step > 0 and b.step > 0
+
+
+def test_checkpoint_then_new_worker_resumes(cluster):
+    a = cluster.add_worker(sync="none", checkpoint_every=25)
+    assert cluster.wait_for(lambda: cluster.master.latest_ckpt != 0 and a.step >= 50, 60)
+    b = cluster.add_worker(sync="none")
+    assert cluster.wait_for(lambda: b.step >= 25, 60)
+    from serverless_learn_amd.ckpt.format import CKPT_BASE
+
+    assert any(f >= CKPT_BASE for f in b.files_received)
