@@ -23,17 +23,16 @@ __device__ __forceinline__ floatx4_t mfma16(const short8_t& a, const short8_t& b
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)a, (bf16x8_t)b, c, 0, 0, 0);
 }
 
-// fp32 -> bf16 bits, round-to-nearest-even (NaN kept quiet).
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
+// fp32 -> bf16 bits, round-to-nearest-even.  A plain cast lowers to the
+// hardware v_cvt_pk_bf16_f32 on gfx950 (keeps NaN a NaN; MI355X_MICROARCH.md
+// "Correctness boundaries"), far cheaper than integer rounding on the bits.
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 __device__ __forceinline__ floatx4_t zero4() { return floatx4_t{0.f, 0.f, 0.f, 0.f}; }

@@ -62,6 +62,36 @@ struct MlpRowArgs {
   float *loss, *correct, *logits;
 };
 
+// Fully unrolled K loop with a 4-deep register ring for the per-wave B
+// operand (weights, streamed from L2): the load for step s+4 is issued right
+// after step s's MFMAs, so ~4 x 16 MFMAs (~1000 cycles) cover the L2 latency
+// even at one wave per SIMD (the row kernel is LDS-limited to 1 WG per CU).
+template <int NSTEPS, class LoadB, class Step>
+__device__ __forceinline__ void kloop_ring4(LoadB&& loadb, Step&& step) {
+  short8_t r0[4], r1[4], r2[4], r3[4];
+  loadb(r0, 0);
+  if (NSTEPS > 1) loadb(r1, 1);
+  if (NSTEPS > 2) loadb(r2, 2);
+  if (NSTEPS > 3) loadb(r3, 3);
+#pragma unroll
+  for (int s = 0; s < NSTEPS; s += 4) {
+    step(s, r0);
+    if (s + 4 < NSTEPS) loadb(r0, s + 4);
+    if (s + 1 < NSTEPS) {
+      step(s + 1, r1);
+      if (s + 5 < NSTEPS) loadb(r1, s + 5);
+    }
+    if (s + 2 < NSTEPS) {
+      step(s + 2, r2);
+      if (s + 6 < NSTEPS) loadb(r2, s + 6);
+    }
+    if (s + 3 < NSTEPS) {
+      step(s + 3, r3);
+      if (s + 7 < NSTEPS) loadb(r3, s + 7);
+    }
+  }
+}
+
 __device__ __forceinline__ long batch_base(const int* cursor, int n_batches, int batch) {
   const long b = cursor ? (long)(*cursor % n_batches) : 0;
   return b * batch;
@@ -119,23 +149,20 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
   {
     const uint16_t* wb = a.w1h + (long)(cw + lr) * D_INP + 8 * lg;
     const uint16_t* xa_ = XS + lr * XS_LD + 8 * lg;
-    short8_t bc[4], bn[4];
+    kloop_ring4<D_INP / 32>(
+        [&](short8_t (&r)[4], int st) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) bc[n] = ld8(wb + n * 16 * D_INP);
-    for (int k0 = 0; k0 < D_INP; k0 += 32) {
-      const int kn = (k0 + 32 < D_INP) ? k0 + 32 : k0;
+          for (int n = 0; n < 4; ++n) r[n] = ld8(wb + n * 16 * D_INP + st * 32);
+        },
+        [&](int st, short8_t (&b)[4]) {
+          short8_t af[4];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) bn[n] = ld8(wb + n * 16 * D_INP + kn);
-      short8_t af[4];
+          for (int m = 0; m < 4; ++m) af[m] = lds8(xa_ + m * 16 * XS_LD + st * 32);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) af[m] = lds8(xa_ + m * 16 * XS_LD + k0);
+          for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], bc[n], acc[m][n]);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bc[n] = bn[n];
-    }
+            for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
+        });
   }
   uint64_t mask1 = 0;
 #pragma unroll
@@ -166,18 +193,20 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
   {
     const uint16_t* wb = a.w2h + (long)(cw + lr) * HID + 8 * lg;
     const uint16_t* ha = H1S + lr * HS_LD + 8 * lg;
-#pragma unroll 2
-    for (int k0 = 0; k0 < HID; k0 += 32) {
-      short8_t bf[4], af[4];
+    kloop_ring4<HID / 32>(
+        [&](short8_t (&r)[4], int st) {
 #pragma unroll
-      for (int n = 0; n < 4; ++n) bf[n] = ld8(wb + n * 16 * HID + k0);
+          for (int n = 0; n < 4; ++n) r[n] = ld8(wb + n * 16 * HID + st * 32);
+        },
+        [&](int st, short8_t (&b)[4]) {
+          short8_t af[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) af[m] = lds8(ha + m * 16 * HS_LD + k0);
+          for (int m = 0; m < 4; ++m) af[m] = lds8(ha + m * 16 * HS_LD + st * 32);
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
+          for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
-    }
+            for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
+        });
   }
   uint64_t mask2 = 0;
 #pragma unroll
@@ -290,18 +319,20 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
   {
     const uint16_t* wb = a.w2th + (long)(cw + lr) * HID + 8 * lg;
     const uint16_t* ha = DHS + lr * HS_LD + 8 * lg;
-#pragma unroll 2
-    for (int k0 = 0; k0 < HID; k0 += 32) {
-      short8_t bf[4], af[4];
+    kloop_ring4<HID / 32>(
+        [&](short8_t (&r)[4], int st) {
 #pragma unroll
-      for (int n = 0; n < 4; ++n) bf[n] = ld8(wb + n * 16 * HID + k0);
+          for (int n = 0; n < 4; ++n) r[n] = ld8(wb + n * 16 * HID + st * 32);
+        },
+        [&](int st, short8_t (&b)[4]) {
+          short8_t af[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) af[m] = lds8(ha + m * 16 * HS_LD + k0);
+          for (int m = 0; m < 4; ++m) af[m] = lds8(ha + m * 16 * HS_LD + st * 32);
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
+          for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
-    }
+            for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
+        });
   }
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
@@ -318,18 +349,26 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
 
 // ---------------------------------------------------------------------------
 // Weight-gradient grouped split-K GEMM:  G[m][n] = sum_b At[m][b] * Bop[b][n]
+//
+// Workgroup tile 64 (m) x 128 (n), 4 waves of 32 x 64 (2 x 4 MFMA tiles), one
+// K slice of the batch per workgroup.  Grid order is slice-major after the
+// XCD remap, so every tile of one slice -- which all read the same batch
+// columns of dH1/dH2/dZ and the same input rows -- runs on one XCD and shares
+// its L2.  Operands stream through a 2-deep register ring (global) and, for
+// the u8 input, a double-buffered LDS tile read back transposed with
+// ds_read_b64_tr_b16.
 // ---------------------------------------------------------------------------
 struct WgProblem {
   const uint16_t* at;  // [m_real][ldk] bf16, batch-contiguous
   const uint16_t* bt;  // mode 0: [n_real][ldk] bf16, batch-contiguous
   int mode;            // 0: bf16 operand, 1: u8 input rows normalised on the fly
   int m_real, n_real;  // column n_real is the virtual all-ones column (bias grad)
-  int tiles_m, tiles_n;
+  int tiles_m, tiles_n, tile_base;
   long w_off, b_off;   // flat destinations of dW and db
 };
 struct WgArgs {
   WgProblem p[3];
-  int tile_start[4];
+  int total_tiles;
   int slices, k_slice, ldk;
   const uint8_t* x;
   const int* cursor;
@@ -339,30 +378,30 @@ struct WgArgs {
   long slab_stride;
 };
 
-constexpr int XT_LD = 72;  // [32 k][64 n] bf16 X tile, 144-B rows (8-B aligned tr reads)
+constexpr int WG_TN = 128;
+constexpr int XT_LD = WG_TN + 8;  // [32 k][128 n] bf16 X tile; 272-B rows (8-B aligned tr reads)
 
 __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t xs[2][32 * XT_LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  int pi = 0;
-  while (pi < 2 && bid >= a.tile_start[pi + 1]) ++pi;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int s = logical / a.total_tiles;
+  const int t = logical - s * a.total_tiles;
+  const int pi = t >= a.p[2].tile_base ? 2 : (t >= a.p[1].tile_base ? 1 : 0);
   const WgProblem& P = a.p[pi];
-  const int local = bid - a.tile_start[pi];
-  const int s = local % a.slices;
-  const int t = local / a.slices;
-  const int tm = t / P.tiles_n, tn = t - tm * P.tiles_n;
+  const int lt = t - P.tile_base;
+  const int tm = lt / P.tiles_n, tn = lt - tm * P.tiles_n;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = tm * 64 + wm * 32, n0 = tn * 64 + wn * 32;
+  const int m0 = tm * 64 + wm * 32, n0 = tn * WG_TN + wn * 64;
   const int kb = s * a.k_slice;
-  const int nsteps = a.k_slice / 32;
+  const int nsteps = a.k_slice / 32;  // even (host guarantees k_slice % 64 == 0)
 
-  floatx4_t acc[2][2];
+  floatx4_t acc[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
 
   const uint16_t* ap[2];
   bool av[2];
@@ -372,68 +411,98 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgArgs a) {
     av[i] = row < P.m_real;
     ap[i] = P.at + (long)(av[i] ? row : 0) * a.ldk + kb + 8 * lg;
   }
+  auto load_a = [&](short8_t (&r)[2], int ks) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r[i] = av[i] ? ld8(ap[i] + ks * 32) : zero8();
+  };
+  auto mma = [&](const short8_t (&af)[2], const short8_t (&bf)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+  };
 
   short8_t ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
 
   if (P.mode == 0) {
-    const uint16_t* bp[2];
-    int bk[2];  // 0 = load, 1 = ones, 2 = zero
+    const uint16_t* bp[4];
+    int bk[4];  // 0 = load, 1 = ones, 2 = zero
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < 4; ++j) {
       const int n = n0 + j * 16 + lr;
       bk[j] = n < P.n_real ? 0 : (n == P.n_real ? 1 : 2);
       bp[j] = P.bt + (long)(n < P.n_real ? n : 0) * a.ldk + kb + 8 * lg;
     }
-    for (int ks = 0; ks < nsteps; ++ks) {
-      const int k = ks * 32;
-      short8_t af[2], bf[2];
+    auto load_b = [&](short8_t (&r)[4], int ks) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = av[i] ? ld8(ap[i] + k) : zero8();
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = bk[j] == 0 ? ld8(bp[j] + k) : (bk[j] == 1 ? ones : zero8());
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+      for (int j = 0; j < 4; ++j) r[j] = bk[j] == 0 ? ld8(bp[j] + ks * 32) : (bk[j] == 1 ? ones : zero8());
+    };
+    short8_t a0[2], a1[2], b0[4], b1[4];
+    load_a(a0, 0);
+    load_b(b0, 0);
+    load_a(a1, 1);
+    load_b(b1, 1);
+    for (int ks = 0; ks < nsteps; ks += 2) {
+      mma(a0, b0);
+      if (ks + 2 < nsteps) { load_a(a0, ks + 2); load_b(b0, ks + 2); }
+      mma(a1, b1);
+      if (ks + 3 < nsteps) { load_a(a1, ks + 3); load_b(b1, ks + 3); }
     }
   } else {
-    // u8 input rows, 32 batch rows x 64 features per stage, transposed reads.
+    // u8 input rows: 32 batch rows x 128 features per stage (16 B per thread)
     const long xrow0 = batch_base(a.cursor, a.n_batches, a.ldk) + kb;
-    const int sr = tid >> 3, sc = (tid & 7) * 8;
-    const int col = tn * 64 + sc;
-    auto load_x = [&](int ks) -> uint2 {
-      if (col < D_IN) return *reinterpret_cast<const uint2*>(a.x + (xrow0 + ks * 32 + sr) * D_IN + col);
-      return make_uint2(0, 0);
+    const int sr = tid >> 3, sc = (tid & 7) * 16;
+    const int col = tn * WG_TN + sc;
+    auto load_x = [&](int ks) -> uint4 {
+      if (col < D_IN) return *reinterpret_cast<const uint4*>(a.x + (xrow0 + ks * 32 + sr) * D_IN + col);
+      return make_uint4(0, 0, 0, 0);
     };
-    auto store_x = [&](uint16_t* dst, uint2 v) {
-      short8_t r;
+    auto store_x = [&](uint16_t* dst, uint4 v) {
+      short8_t lo, hi;
       if (col < D_IN) {
-        r = u8x8_to_bf16(v, a.xa, a.xb);
+        lo = u8x8_to_bf16(make_uint2(v.x, v.y), a.xa, a.xb);
+        hi = u8x8_to_bf16(make_uint2(v.z, v.w), a.xa, a.xb);
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = (col + j == D_IN) ? (short)0x3f80 : (short)0;
+        for (int j = 0; j < 8; ++j) {
+          lo[j] = (col + j == D_IN) ? (short)0x3f80 : (short)0;
+          hi[j] = (col + 8 + j == D_IN) ? (short)0x3f80 : (short)0;
+        }
       }
-      *reinterpret_cast<short8_t*>(dst + sr * XT_LD + sc) = r;
+      *reinterpret_cast<short8_t*>(dst + sr * XT_LD + sc) = lo;
+      *reinterpret_cast<short8_t*>(dst + sr * XT_LD + sc + 8) = hi;
     };
-    uint2 xr = load_x(0);
-    store_x(xs[0], xr);
+    uint4 x0 = load_x(0);
+    uint4 x1 = nsteps > 1 ? load_x(1) : x0;
+    store_x(xs[0], x0);
+    short8_t a0[2], a1[2];
+    load_a(a0, 0);
+    load_a(a1, 1);
     __syncthreads();
-    for (int ks = 0; ks < nsteps; ++ks) {
-      const int cur = ks & 1;
-      if (ks + 1 < nsteps) xr = load_x(ks + 1);
-      const int k = ks * 32;
-      short8_t af[2], bf[2];
+    for (int ks = 0; ks < nsteps; ks += 2) {
+      // even step: compute from xs[0] while x1 (step ks+1) waits in registers
+      if (ks + 2 < nsteps) x0 = load_x(ks + 2);
+      {
+        short8_t bf[4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = av[i] ? ld8(ap[i] + k) : zero8();
+        for (int j = 0; j < 4; ++j) bf[j] = lds_tr8(xs[0] + wn * 64 + j * 16, XT_LD, lane);
+        mma(a0, bf);
+      }
+      if (ks + 2 < nsteps) load_a(a0, ks + 2);
+      store_x(xs[1], x1);
+      __syncthreads();
+      // odd step: compute from xs[1]
+      if (ks + 3 < nsteps) x1 = load_x(ks + 3);
+      {
+        short8_t bf[4];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = lds_tr8(xs[cur] + wn * 32 + j * 16, XT_LD, lane);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-      if (ks + 1 < nsteps) store_x(xs[cur ^ 1], xr);
+        for (int j = 0; j < 4; ++j) bf[j] = lds_tr8(xs[1] + wn * 64 + j * 16, XT_LD, lane);
+        mma(a1, bf);
+      }
+      if (ks + 3 < nsteps) load_a(a1, ks + 3);
+      if (ks + 2 < nsteps) store_x(xs[0], x0);
       __syncthreads();
     }
   }
@@ -442,7 +511,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgArgs a) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < 4; ++j) {
       const int n = n0 + j * 16 + lr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -563,20 +632,25 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
 int sl_mlp_wgrad(const uint8_t* x, const int* cursor, int n_batches, int batch, float xa, float xb,
                  const uint16_t* h1t, const uint16_t* h2t, const uint16_t* dzt, const uint16_t* dh2t,
                  const uint16_t* dh1t, float* slab, int slices, long slab_stride, hipStream_t stream) {
-  if (batch <= 0 || slices <= 0 || batch % (32 * slices) != 0) return -1;
+  if (batch <= 0 || slices <= 0 || batch % (64 * slices) != 0) return -1;
   WgArgs a;
+  const int tn_in = (D_IN + 1 + WG_TN - 1) / WG_TN, tn_h = (HID + 1 + WG_TN - 1) / WG_TN;
   // dW1|db1 = dH1^T [256 x B] . [X | 1]  (u8 operand)
-  a.p[0] = WgProblem{dh1t, nullptr, 1, HID, D_IN, HID / 64, (D_IN + 1 + 63) / 64, P_W1, P_B1};
+  a.p[0] = WgProblem{dh1t, nullptr, 1, HID, D_IN, HID / 64, tn_in, 0, P_W1, P_B1};
   // dW2|db2 = dH2^T . [H1 | 1]
-  a.p[1] = WgProblem{dh2t, h1t, 0, HID, HID, HID / 64, (HID + 1 + 63) / 64, P_W2, P_B2};
+  a.p[1] = WgProblem{dh2t, h1t, 0, HID, HID, HID / 64, tn_h, 0, P_W2, P_B2};
   // dW3|db3 = dZ^T . [H2 | 1]
-  a.p[2] = WgProblem{dzt, h2t, 0, NC, HID, 1, (HID + 1 + 63) / 64, P_W3, P_B3};
-  a.tile_start[0] = 0;
-  for (int i = 0; i < 3; ++i) a.tile_start[i + 1] = a.tile_start[i] + a.p[i].tiles_m * a.p[i].tiles_n * slices;
+  a.p[2] = WgProblem{dzt, h2t, 0, NC, HID, 1, tn_h, 0, P_W3, P_B3};
+  int base = 0;
+  for (int i = 0; i < 3; ++i) {
+    a.p[i].tile_base = base;
+    base += a.p[i].tiles_m * a.p[i].tiles_n;
+  }
+  a.total_tiles = base;
   a.slices = slices; a.k_slice = batch / slices; a.ldk = batch;
   a.x = x; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.xa = xa; a.xb = xb;
   a.slab = slab; a.slab_stride = slab_stride;
-  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(a.tile_start[3]), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }

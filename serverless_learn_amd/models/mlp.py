@@ -203,7 +203,7 @@ class CPUTrainer:
 
 def default_slices(batch: int) -> int:
     s = max(1, min(16, batch // 1024))
-    while s > 1 and batch % (32 * s) != 0:
+    while s > 1 and batch % (64 * s) != 0:
         s -= 1
     return s
 

@@ -72,7 +72,7 @@ def test_sgd_flat_kernel_matches_torch():
     w_ref -= 0.1 * m_ref
     torch.testing.assert_close(w, w_ref, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(mom, m_ref, rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(shadow.float(), w_ref.bfloat16().float(), rtol=0, atol=0)
+    torch.testing.assert_close(shadow.float(), w.bfloat16().float(), rtol=0, atol=0)
 
 
 def test_gpu_worker_trains_from_pushed_shard():
