@@ -9,10 +9,14 @@ RANK/LOCAL_RANK/WORLD_SIZE); each rank is one worker that
      in-process file server streams it as 1 MB ``Chunk``s to the worker's
      ``ReceiveFile`` handler, which lands it in a pinned host buffer and
      hipMemcpyAsync's it into HBM; ``--ingest local`` skips gRPC),
-  2. trains the 784-256-256-10 MLP with the fused HIP kernels (bf16 MFMA,
-     fp32 master weights, momentum SGD) -- every timed step is a full
-     forward + backward + (RCCL all-reduce) + optimizer step,
+  2. trains the model with the hand-written HIP kernels (bf16 MFMA, fp32
+     master weights, momentum SGD) -- every timed step is a full forward +
+     backward + (RCCL all-reduce) + optimizer step,
   3. reports whole-job samples/s = global_batch * steps / max-over-ranks time.
+
+``--model resnet18`` runs BASELINE config 4 instead (ResNet-18-shaped CNN on
+synthetic CIFAR-shaped 32x32x3 data, implicit-GEMM convolutions), with the
+gradient all-reduce bucketed and overlapped with backward.
 
 Weak scaling: the per-GPU batch is fixed as N grows.  The reference publishes
 no number; ``vs_baseline`` is against the reference's derived
@@ -32,22 +36,31 @@ sys.path.insert(0, ROOT)
 
 REF_CEILING_PER_WORKER = 25478.0
 METRIC = "samples/sec (whole node), 3-layer MLP on synthetic MNIST, 1/2/4/8 workers"
+METRIC_CNN = "samples/sec (whole node), ResNet-18-shaped CNN on synthetic CIFAR-shaped data, 1/2/4/8 workers"
 
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=16384, help="per-GPU batch (multiple of 64)")
-    ap.add_argument("--shard-batches", type=int, default=8, help="batches resident per worker shard")
-    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--model", choices=["mlp", "resnet18"], default="mlp")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (MLP: multiple of 64)")
+    ap.add_argument("--shard-batches", type=int, default=None, help="batches resident per worker shard")
+    ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--ingest", choices=["grpc", "local"], default="grpc")
-    ap.add_argument("--model", choices=["mlp"], default="mlp")
+    ap.add_argument("--bucket-mb", type=float, default=16.0, help="CNN all-reduce bucket size")
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    mlp = a.model == "mlp"
+    a.steps = a.steps if a.steps is not None else (200 if mlp else 30)
+    a.warmup = a.warmup if a.warmup is not None else (20 if mlp else 5)
+    a.batch = a.batch or (16384 if mlp else 256)
+    a.shard_batches = a.shard_batches or (8 if mlp else 4)
+    a.lr = a.lr if a.lr is not None else (0.05 if mlp else 0.1)
+    return a
 
 
 def main(argv=None) -> int:
@@ -55,7 +68,6 @@ def main(argv=None) -> int:
     import torch
     import torch.distributed as dist
 
-    from serverless_learn_amd.models.mlp import FusedMLPTrainer, N_PARAMS
     from serverless_learn_amd.data.synthetic import decode_shard, make_shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -69,6 +81,8 @@ def main(argv=None) -> int:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
 
+    mlp = args.model == "mlp"
+    dataset = "synthetic-mnist" if mlp else "synthetic-cifar"
     B = args.batch
     n_records = B * args.shard_batches
 
@@ -77,24 +91,38 @@ def main(argv=None) -> int:
     if args.ingest == "grpc":
         from serverless_learn_amd.runtime.local_cluster import fetch_shard_via_grpc
 
-        host_buf = fetch_shard_via_grpc(n_records=n_records, shard_index=rank, num_shards=world, seed=0)
+        host_buf = fetch_shard_via_grpc(n_records=n_records, shard_index=rank, num_shards=world, seed=0,
+                                        dataset=dataset)
     else:
-        host_buf = make_shard(n_records, shard_index=rank, num_shards=world, seed=0)
-    hdr, images, labels = decode_shard(host_buf)
+        host_buf = make_shard(n_records, shard_index=rank, num_shards=world, seed=0, dataset=dataset)
+    hdr, images, labels = decode_shard(bytearray(host_buf))
     x = torch.from_numpy(images).pin_memory().to(dev, non_blocking=True)
     y = torch.from_numpy(labels.copy()).pin_memory().to(dev, non_blocking=True)
     torch.cuda.synchronize()
     t_ingest = time.perf_counter() - t_ingest
 
     # ---- 2. engine ----------------------------------------------------------
-    tr = FusedMLPTrainer(batch=B, device=dev, lr=args.lr, momentum=args.momentum,
-                         world_size=world, seed=0)
+    if mlp:
+        from serverless_learn_amd.models.mlp import FusedMLPTrainer, N_PARAMS
+
+        tr = FusedMLPTrainer(batch=B, device=dev, lr=args.lr, momentum=args.momentum, world_size=world, seed=0)
+        n_params, model_name = N_PARAMS, "mlp-784-256-256-10"
+    else:
+        from serverless_learn_amd.models.resnet_engine import FusedResNetTrainer
+
+        tr = FusedResNetTrainer(batch=B, device=dev, lr=args.lr, momentum=args.momentum, world_size=world, seed=0)
+        n_params, model_name = tr.spec.n_logical, "resnet18-cifar (11.17M params)"
     if world > 1:
         # identical start: broadcast rank 0's weights
         flat = tr.get_flat()
         dist.broadcast(flat, 0)
         tr.set_flat(flat)
-        tr.allreduce = lambda g: dist.all_reduce(g)
+        if mlp:
+            tr.allreduce = lambda g: dist.all_reduce(g)
+        else:
+            tr.bucket_bytes = int(args.bucket_mb * (1 << 20))
+            tr.bucket_hook = lambda view: dist.all_reduce(view, async_op=True)
+            tr.bucket_wait = lambda handles: [h.wait() for h in handles]
     tr.load_shard(x, y)
 
     use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
@@ -128,7 +156,7 @@ def main(argv=None) -> int:
     global_batch = B * world
     value = global_batch * args.steps / elapsed
     out = {
-        "metric": METRIC,
+        "metric": METRIC if mlp else METRIC_CNN,
         "value": round(value, 1),
         "unit": "samples/s",
         "n_gpus": world,
@@ -139,10 +167,10 @@ def main(argv=None) -> int:
         "scaling": "weak",
         "vs_baseline": round(value / (REF_CEILING_PER_WORKER * world), 2),
         "dtype": "bf16",
-        "data": "synthetic (seeded MNIST-shaped u8 shards, random-init weights)",
+        "data": f"synthetic (seeded {'MNIST' if mlp else 'CIFAR'}-shaped u8 shards, random-init weights)",
         "config": {
-            "model": "mlp-784-256-256-10",
-            "params": N_PARAMS,
+            "model": model_name,
+            "params": n_params,
             "global_batch": global_batch,
             "per_gpu_batch": B,
             "seq_len": None,

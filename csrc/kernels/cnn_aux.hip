@@ -1,0 +1,466 @@
+// Memory-bound companions of the implicit-GEMM convolutions for the
+// ResNet-18-shaped CNN (K6, K10, K11, K12, K4 of SURVEY.md §2.5).  All
+// activations are NHWC bf16 with C a multiple of 8, so every kernel moves
+// 16 B (8 channels) per thread per access; per-channel reductions keep a
+// thread's 8 channels in registers, fold rows through LDS and finish with one
+// fp32 atomic per channel per workgroup.
+//
+//   input_norm      u8 [N][H][W][3] -> bf16 [N][H][W][8] ((x/255 - mean_c)/std_c, pad channels 0),
+//                   batch chosen by a device cursor (hipGraph replay)
+//   bn_finalize     conv-epilogue sums -> scale/shift/mean/rstd, running-stat update
+//   bn_apply        y = relu?(x*scale + shift + r), r = 0 | res | res*rscale + rshift
+//   bn_bwd_reduce   dz = dy*1[y>0]; per-channel sum(dz), sum(dz*x) (+ dz out for the skip)
+//   bn_bwd_finalize -> dgamma, dbeta (into the flat gradient) and dx = a*dz + b*x + c coefficients
+//   bn_bwd_apply    dx = a*dz + b*x + c
+//   maxpool / avgpool fwd+bwd, softmax cross-entropy (loss, correct, dlogits, dbias)
+#include "common.h"
+
+using namespace sl;
+
+__device__ __forceinline__ void unpack8(const short8_t& v, float (&f)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = bf2f((uint16_t)v[j]);
+}
+__device__ __forceinline__ short8_t pack8(const float (&f)[8]) {
+  short8_t v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(f[j]);
+  return v;
+}
+
+static int blocks_for(long items, int cap = 4096) {
+  long b = (items + 255) / 256;
+  if (b > cap) b = cap;
+  return b < 1 ? 1 : (int)b;
+}
+
+// ---------------------------------------------------------------------------
+// Batch `cursor % n_batches` of a device-resident u8 shard -> normalised bf16
+// (and its labels), so a captured step replays on fresh data with no host work.
+__global__ __launch_bounds__(256) void input_norm_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ lab,
+                                                         const int* __restrict__ cursor, int n_batches, int batch,
+                                                         long img_pixels, uint16_t* __restrict__ y,
+                                                         uint8_t* __restrict__ lab_out, float a0, float a1, float a2,
+                                                         float b0, float b1, float b2) {
+  const long b = cursor ? (long)(*cursor % n_batches) : 0;
+  const long pixels = (long)batch * img_pixels;
+  const uint8_t* src = x + b * pixels * 3;
+  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < pixels; p += (long)gridDim.x * blockDim.x) {
+    const uint8_t* s = src + p * 3;
+    float f[8] = {s[0] * a0 + b0, s[1] * a1 + b1, s[2] * a2 + b2, 0.f, 0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<short8_t*>(y + p * 8) = pack8(f);
+    if (lab_out && p < batch) lab_out[p] = lab[b * batch + p];
+  }
+}
+
+__global__ void cursor_bump_kernel(int* cursor) { *cursor += 1; }
+
+// coef layout [4][C]: scale, shift, mean, rstd
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* __restrict__ coef,
+                                   float* __restrict__ run_mean, float* __restrict__ run_var, int C, float count,
+                                   float eps, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float mean = stats[c] / count;
+  const float var = fmaxf(stats[C + c] / count - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + eps);
+  const float sc = gamma[c] * rstd;
+  coef[c] = sc;
+  coef[C + c] = beta[c] - mean * sc;
+  coef[2 * C + c] = mean;
+  coef[3 * C + c] = rstd;
+  if (run_mean) {
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * (count / fmaxf(count - 1.f, 1.f));
+  }
+}
+
+// mode: 0 = none, 1 = identity residual, 2 = residual through its own BN (rcoef)
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const float* __restrict__ coef,
+                                                       const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ rcoef, uint16_t* __restrict__ y,
+                                                       long rows, int C, int relu, int mode) {
+  const int cpr = C >> 3;
+  const long total = rows * cpr;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(q % cpr) * 8;
+    float f[8];
+    unpack8(ld8(x + q * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * coef[c0 + j] + coef[C + c0 + j];
+    if (mode) {
+      float r[8];
+      unpack8(ld8(res + q * 8), r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += mode == 2 ? r[j] * rcoef[c0 + j] + rcoef[C + c0 + j] : r[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    *reinterpret_cast<short8_t*>(y + q * 8) = pack8(f);
+  }
+}
+
+// Per-channel sums of dz = dy*1[y>0] and dz*x.  Thread layout: TPR = C/8
+// threads per row, 256/TPR rows per pass; partials folded through LDS.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
+                                                            const uint16_t* __restrict__ y,
+                                                            const uint16_t* __restrict__ x,
+                                                            uint16_t* __restrict__ dz_out, float* __restrict__ sums,
+                                                            long rows, int C) {
+  __shared__ float part[256][17];
+  const int tpr = C >> 3, rpp = 256 / tpr;
+  const int tid = threadIdx.x;
+  const int cg = tid % tpr, rsub = tid / tpr;
+  float s[8] = {0.f}, d[8] = {0.f};
+  if (rsub < rpp) {
+    for (long r = (long)blockIdx.x * rpp + rsub; r < rows; r += (long)gridDim.x * rpp) {
+      const long off = r * C + cg * 8;
+      float g[8], xv[8];
+      unpack8(ld8(dy + off), g);
+      if (y) {
+        float yv[8];
+        unpack8(ld8(y + off), yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      }
+      if (dz_out) *reinterpret_cast<short8_t*>(dz_out + off) = pack8(g);
+      unpack8(ld8(x + off), xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += g[j];
+        d[j] += g[j] * xv[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    part[tid][j] = s[j];
+    part[tid][8 + j] = d[j];
+  }
+  __syncthreads();
+  // fold the rpp row-groups: thread t < 2*C handles one (quantity, channel)
+  for (int t = tid; t < 2 * C; t += 256) {
+    const int qsel = t / C, c = t - qsel * C;
+    const int g = c >> 3, j = c & 7;
+    float acc = 0.f;
+    for (int r = 0; r < rpp; ++r) acc += part[r * tpr + g][qsel * 8 + j];
+    atomicAdd(sums + qsel * C + c, acc);
+  }
+}
+
+// dcoef layout [3][C]: a, b, c with dx = a*dz + b*x + c.  grad_gamma/beta += (flat gradient).
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ coef,
+                                       float* __restrict__ dcoef, float* __restrict__ grad_gamma,
+                                       float* __restrict__ grad_beta, int C, float count) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float s0 = sums[c], s1 = sums[C + c];
+  const float sc = coef[c], mean = coef[2 * C + c], rstd = coef[3 * C + c];
+  const float sdxh = rstd * (s1 - mean * s0);  // sum(dz * xhat)
+  const float b = -sc * rstd * sdxh / count;
+  dcoef[c] = sc;
+  dcoef[C + c] = b;
+  dcoef[2 * C + c] = -sc * s0 / count - b * mean;
+  if (grad_gamma) grad_gamma[c] += sdxh;
+  if (grad_beta) grad_beta[c] += s0;
+}
+
+// dx = a*dz + b*x + c; dz = dy*1[y>0] recomputed (or read directly when y == null)
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
+                                                           const uint16_t* __restrict__ y,
+                                                           const uint16_t* __restrict__ x,
+                                                           const float* __restrict__ dcoef,
+                                                           uint16_t* __restrict__ dx, long rows, int C) {
+  const int cpr = C >> 3;
+  const long total = rows * cpr;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(q % cpr) * 8;
+    float g[8], xv[8];
+    unpack8(ld8(dy + q * 8), g);
+    if (y) {
+      float yv[8];
+      unpack8(ld8(y + q * 8), yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    }
+    unpack8(ld8(x + q * 8), xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = dcoef[c0 + j] * g[j] + dcoef[C + c0 + j] * xv[j] + dcoef[2 * C + c0 + j];
+    *reinterpret_cast<short8_t*>(dx + q * 8) = pack8(g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Max pool (KxK, stride s, pad p) with a per-output argmax tap (u8) for backward.
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ arg, int N, int H, int W, int C,
+                                                          int OH, int OW, int K, int s, int p) {
+  const int cpr = C >> 3;
+  const long total = (long)N * OH * OW * cpr;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(q % cpr) * 8;
+    const long pix = q / cpr;
+    const int ow = (int)(pix % OW);
+    const int oh = (int)((pix / OW) % OH);
+    const int n = (int)(pix / ((long)OW * OH));
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int kh = 0; kh < K; ++kh)
+      for (int kw = 0; kw < K; ++kw) {
+        const int ih = oh * s - p + kh, iw = ow * s - p + kw;
+        if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) continue;
+        float v[8];
+        unpack8(ld8(x + (((long)n * H + ih) * W + iw) * C + c0), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > best[j]) { best[j] = v[j]; bi[j] = (uint8_t)(kh * K + kw); }
+      }
+    *reinterpret_cast<short8_t*>(y + pix * C + c0) = pack8(best);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) arg[pix * C + c0 + j] = bi[j];
+  }
+}
+
+// Gather form: each input pixel sums the gradients of the windows whose argmax it is.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ arg, uint16_t* __restrict__ dx,
+                                                          int N, int H, int W, int C, int OH, int OW, int K, int s,
+                                                          int p) {
+  const int cpr = C >> 3;
+  const long total = (long)N * H * W * cpr;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(q % cpr) * 8;
+    const long pix = q / cpr;
+    const int w = (int)(pix % W);
+    const int h = (int)((pix / W) % H);
+    const int n = (int)(pix / ((long)W * H));
+    float acc[8] = {0.f};
+    for (int kh = 0; kh < K; ++kh) {
+      const int th = h + p - kh;
+      if (th < 0 || th % s) continue;
+      const int oh = th / s;
+      if (oh >= OH) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int tw = w + p - kw;
+        if (tw < 0 || tw % s) continue;
+        const int ow = tw / s;
+        if (ow >= OW) continue;
+        const long o = (((long)n * OH + oh) * OW + ow) * C + c0;
+        float g[8];
+        unpack8(ld8(dy + o), g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (arg[o + j] == (uint8_t)(kh * K + kw)) acc[j] += g[j];
+      }
+    }
+    *reinterpret_cast<short8_t*>(dx + pix * C + c0) = pack8(acc);
+  }
+}
+
+// Global average pool [N][HW][C] -> [N][C]; backward broadcasts dy/HW.
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                          int N, int HW, int C) {
+  const int cpr = C >> 3;
+  const long total = (long)N * cpr;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(q / cpr), c0 = (int)(q % cpr) * 8;
+    float acc[8] = {0.f};
+    for (int i = 0; i < HW; ++i) {
+      float v[8];
+      unpack8(ld8(x + ((long)n * HW + i) * C + c0), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= 1.f / HW;
+    *reinterpret_cast<short8_t*>(y + (long)n * C + c0) = pack8(acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx,
+                                                          int N, int HW, int C) {
+  const int cpr = C >> 3;
+  const long total = (long)N * HW * cpr;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const long pix = q / cpr;
+    const int c0 = (int)(q % cpr) * 8;
+    const int n = (int)(pix / HW);
+    float g[8];
+    unpack8(ld8(dy + (long)n * C + c0), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] *= 1.f / HW;
+    *reinterpret_cast<short8_t*>(dx + pix * C + c0) = pack8(g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Softmax cross-entropy over fp32 logits [N][ncls] (ncls <= 16); one row per
+// 16-lane group.  dlogits (bf16, [N][ldd], zero beyond ncls) are scaled by
+// grad_scale; the bias gradient (sum over rows of dlogits) is folded per
+// workgroup and added atomically.
+__global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict__ z, const uint8_t* __restrict__ lab,
+                                                         float* __restrict__ loss, float* __restrict__ correct,
+                                                         uint16_t* __restrict__ dz, int ldd, float* __restrict__ dbias,
+                                                         int N, int ncls, float grad_scale) {
+  __shared__ float bsum[16][16];
+  const int tid = threadIdx.x, c = tid & 15, grp = tid >> 4;
+  const int row = blockIdx.x * 16 + grp;
+  float dv = 0.f;
+  if (row < N) {
+    const float v = c < ncls ? z[(long)row * ncls + c] : -INFINITY;
+    float mx = v;
+    mx = fmaxf(mx, __shfl_xor(mx, 1));
+    mx = fmaxf(mx, __shfl_xor(mx, 2));
+    mx = fmaxf(mx, __shfl_xor(mx, 4));
+    mx = fmaxf(mx, __shfl_xor(mx, 8));
+    const float e = c < ncls ? __expf(v - mx) : 0.f;
+    float s = e;
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    s += __shfl_xor(s, 8);
+    int l = lab[row];
+    l = l < ncls ? l : 0;
+    const float zl = __shfl(v, (tid & 63 & ~15) | l);
+    int idx = v == mx ? c : 16;
+    idx = min(idx, __shfl_xor(idx, 1));
+    idx = min(idx, __shfl_xor(idx, 2));
+    idx = min(idx, __shfl_xor(idx, 4));
+    idx = min(idx, __shfl_xor(idx, 8));
+    if (c == 0) {
+      if (loss) loss[row] = mx + __logf(s) - zl;
+      if (correct) correct[row] = idx == l ? 1.f : 0.f;
+    }
+    dv = c < ncls ? (e / s - (c == l ? 1.f : 0.f)) * grad_scale : 0.f;
+    if (c < ldd) dz[(long)row * ldd + c] = f2bf(dv);
+  }
+  bsum[grp][c] = dv;
+  __syncthreads();
+  if (dbias && tid < ncls) {
+    float acc = 0.f;
+    for (int g2 = 0; g2 < 16; ++g2) acc += bsum[g2][tid];
+    atomicAdd(dbias + tid, acc);
+  }
+}
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int sl_input_norm(const uint8_t* x, const uint8_t* lab, const int* cursor, int n_batches, int batch,
+                  long img_pixels, uint16_t* y, uint8_t* lab_out, float m0, float m1, float m2, float s0, float s1,
+                  float s2, hipStream_t stream) {
+  const float mean[3] = {m0, m1, m2}, stdv[3] = {s0, s1, s2};
+  float a[3], b[3];
+  for (int i = 0; i < 3; ++i) {
+    a[i] = 1.f / (255.f * stdv[i]);
+    b[i] = -mean[i] / stdv[i];
+  }
+  if (n_batches < 1 || batch < 1) return -1;
+  hipLaunchKernelGGL(input_norm_kernel, dim3(blocks_for((long)batch * img_pixels)), dim3(256), 0, stream, x, lab,
+                     cursor, n_batches, batch, img_pixels, y, lab_out, a[0], a[1], a[2], b[0], b[1], b[2]);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_cursor_bump(int* cursor, hipStream_t stream) {
+  hipLaunchKernelGGL(cursor_bump_kernel, dim3(1), dim3(1), 0, stream, cursor);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_bn_finalize(const float* stats, const float* gamma, const float* beta, float* coef, float* run_mean,
+                   float* run_var, int C, float count, float eps, float momentum, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, stats, gamma, beta, coef,
+                     run_mean, run_var, C, count, eps, momentum);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_bn_apply(const uint16_t* x, const float* coef, const uint16_t* res, const float* rcoef, uint16_t* y, long rows,
+                int C, int relu, int mode, hipStream_t stream) {
+  if (C & 7) return -1;
+  if (mode && !res) return -2;
+  if (mode == 2 && !rcoef) return -2;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, x, coef, res, rcoef, y,
+                     rows, C, relu, mode);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, uint16_t* dz_out, float* sums,
+                     long rows, int C, hipStream_t stream) {
+  if ((C & 7) || C > 2048 || (C & (C - 1))) return -1;
+  const int rpp = 256 / (C / 8);
+  long blocks = (rows + rpp * 8 - 1) / (rpp * 8);  // >= 8 rows per thread
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, dz_out, sums, rows, C);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_bn_bwd_finalize(const float* sums, const float* coef, float* dcoef, float* grad_gamma, float* grad_beta, int C,
+                       float count, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, sums, coef, dcoef,
+                     grad_gamma, grad_beta, C, count);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* dcoef, uint16_t* dx,
+                    long rows, int C, hipStream_t stream) {
+  if (C & 7) return -1;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, dy, y, x, dcoef,
+                     dx, rows, C);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int OH, int OW, int K,
+                   int s, int p, hipStream_t stream) {
+  if ((C & 7) || K * K > 255) return -1;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks_for((long)N * OH * OW * (C / 8))), dim3(256), 0, stream, x, y,
+                     arg, N, H, W, C, OH, OW, K, s, p);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int OH, int OW,
+                   int K, int s, int p, hipStream_t stream) {
+  if (C & 7) return -1;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks_for((long)N * H * W * (C / 8))), dim3(256), 0, stream, dy, arg,
+                     dx, N, H, W, C, OH, OW, K, s, p);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t stream) {
+  if (C & 7) return -1;
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(blocks_for((long)N * (C / 8))), dim3(256), 0, stream, x, y, N, HW, C);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t stream) {
+  if (C & 7) return -1;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(blocks_for((long)N * HW * (C / 8))), dim3(256), 0, stream, dy, dx, N,
+                     HW, C);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_softmax_ce(const float* z, const uint8_t* lab, float* loss, float* correct, uint16_t* dz, int ldd,
+                  float* dbias, int N, int ncls, float grad_scale, hipStream_t stream) {
+  if (ncls > 16 || ldd > 16 || ldd < ncls) return -1;
+  hipLaunchKernelGGL(softmax_ce_kernel, dim3((N + 15) / 16), dim3(256), 0, stream, z, lab, loss, correct, dz, ldd,
+                     dbias, N, ncls, grad_scale);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

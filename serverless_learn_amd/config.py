@@ -34,7 +34,7 @@ class Config:
     # --- data plane (file_server.cc:40,46) ---
     chunk_size: int = 1_000_000
     dummy_file_length: int = 100_000_000
-    dataset: str = "synthetic-mnist"   # or "reference-dummy" (byte-exact reference file 0)
+    dataset: str = "synthetic-mnist"   # | "synthetic-cifar" | "reference-dummy" (byte-exact reference file 0)
     shard_records: int = 127_388       # records per shard: a 100,000,000-byte shard
     num_shards: int = 0                # 0 = one shard per worker
     push_policy: str = "on_change"     # "on_change" | "periodic" (reference: re-push every interval)
@@ -48,7 +48,7 @@ class Config:
     sync: str = "allreduce"            # allreduce | gossip | ps | none
     gossip_compat: bool = False        # reproduce the reference's alpha^2 echo exactly
     device: str = "auto"               # auto | cpu | cuda[:N]
-    model: str = "mlp"                 # mlp | simulate (reference: vector += 1)
+    model: str = "mlp"                 # mlp | resnet18 | simulate (reference: vector += 1)
     batch: int = 1024
     lr: float = 0.05
     momentum: float = 0.9

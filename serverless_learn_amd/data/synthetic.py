@@ -19,10 +19,10 @@ Shard wire/file layout (little-endian, all offsets from the file start):
     32  u32  classes (10)
     36  u32  shard_index
     40  u32  num_shards
-    44  u32  reserved
+    44  u32  channels (0 or 1 = grey [n][h*w]; 3 = colour NHWC [n][h][w][3])
     48  u64  seed
     56  u64  reserved
-    64  u8[n*height*width]  images, row-major, record-contiguous
+    64  u8[n*height*width*channels]  images, row-major (HWC), record-contiguous
     ..  u8[n]               labels
 
 A 100,000,000-byte shard (the reference's file size) holds 127,388 records.
@@ -75,10 +75,40 @@ def make_mnist_like(n: int, seed: int = 0, classes: int = 10, h: int = 28, w: in
     return out, labels
 
 
+def make_cifar_like(n: int, seed: int = 0, classes: int = 10, hw: int = 32,
+                    noise: float = 0.6) -> tuple[np.ndarray, np.ndarray]:
+    """(images u8 [n, hw, hw, 3] NHWC, labels u8 [n]) -- CIFAR-shaped, learnable, deterministic.
+
+    Each class is a colour-tinted sum of Gaussian blobs (shared prototypes, so
+    every shard is the same task); records add amplitude jitter, a random
+    circular shift of up to 3 pixels and Gaussian noise.
+    """
+    rng = np.random.default_rng(seed)
+    base = _prototypes(classes, hw, hw, 4321).reshape(classes, hw, hw)
+    tint = np.random.default_rng(99).uniform(0.3, 1.0, size=(classes, 3)).astype(np.float32)
+    protos = base[..., None] * tint[:, None, None, :]  # [classes, hw, hw, 3]
+    labels = rng.integers(0, classes, size=n, dtype=np.uint8)
+    out = np.empty((n, hw, hw, 3), np.uint8)
+    chunk = 4096
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        m = e - s
+        amp = rng.uniform(0.6, 1.0, size=(m, 1, 1, 1)).astype(np.float32)
+        img = protos[labels[s:e]] * amp
+        dy, dx = rng.integers(-3, 4, size=2)
+        img = np.roll(img, (int(dy), int(dx)), axis=(1, 2))
+        img += rng.standard_normal(img.shape, dtype=np.float32) * (noise * 0.5)
+        np.clip(img * 200.0 + 28.0, 0, 255, out=img)
+        out[s:e] = img.astype(np.uint8)
+    return out, labels
+
+
 def encode_shard(images: np.ndarray, labels: np.ndarray, shard_index: int = 0, num_shards: int = 1,
-                 seed: int = 0, h: int = 28, w: int = 28, classes: int = 10) -> bytes:
+                 seed: int = 0, h: int = 28, w: int = 28, classes: int = 10, channels: int = 1) -> bytes:
     n = images.shape[0]
-    hdr = HEADER.pack(MAGIC, 1, 1, n, h, w, classes, shard_index, num_shards, 0, seed, 0)
+    kind = 1 if channels <= 1 else 2
+    hdr = HEADER.pack(MAGIC, 1, kind, n, h, w, classes, shard_index, num_shards, channels if channels > 1 else 0,
+                      seed, 0)
     return hdr + np.ascontiguousarray(images, np.uint8).tobytes() + np.ascontiguousarray(labels, np.uint8).tobytes()
 
 
@@ -86,17 +116,17 @@ def decode_header(buf) -> dict:
     mv = memoryview(buf)
     if len(mv) < HEADER_SIZE:
         raise ValueError("shard too short")
-    magic, ver, kind, n, h, w, classes, si, ns, _r, seed, _r2 = HEADER.unpack(bytes(mv[:HEADER_SIZE]))
+    magic, ver, kind, n, h, w, classes, si, ns, ch, seed, _r2 = HEADER.unpack(bytes(mv[:HEADER_SIZE]))
     if magic != MAGIC:
         raise ValueError("bad shard magic")
     return dict(version=ver, kind=kind, n=n, height=h, width=w, classes=classes,
-                shard_index=si, num_shards=ns, seed=seed)
+                shard_index=si, num_shards=ns, seed=seed, channels=max(1, ch))
 
 
 def decode_shard(buf) -> tuple[dict, np.ndarray, np.ndarray]:
-    """Zero-copy views (images [n, h*w], labels [n]) into ``buf``."""
+    """Zero-copy views (images [n, h*w*channels], labels [n]) into ``buf``."""
     hdr = decode_header(buf)
-    n, d = hdr["n"], hdr["height"] * hdr["width"]
+    n, d = hdr["n"], hdr["height"] * hdr["width"] * hdr["channels"]
     arr = np.frombuffer(buf, dtype=np.uint8)
     need = HEADER_SIZE + n * d + n
     if arr.size < need:
@@ -106,6 +136,10 @@ def decode_shard(buf) -> tuple[dict, np.ndarray, np.ndarray]:
     return hdr, images, labels
 
 
-def make_shard(n: int, shard_index: int = 0, num_shards: int = 1, seed: int = 0) -> bytes:
+def make_shard(n: int, shard_index: int = 0, num_shards: int = 1, seed: int = 0, dataset: str = "synthetic-mnist") -> bytes:
+    """Shard ``shard_index`` of a seeded synthetic dataset (``synthetic-mnist`` or ``synthetic-cifar``)."""
+    if dataset == "synthetic-cifar":
+        images, labels = make_cifar_like(n, seed=seed * 1000003 + shard_index)
+        return encode_shard(images.reshape(n, -1), labels, shard_index, num_shards, seed, h=32, w=32, channels=3)
     images, labels = make_mnist_like(n, seed=seed * 1000003 + shard_index)
     return encode_shard(images, labels, shard_index, num_shards, seed)

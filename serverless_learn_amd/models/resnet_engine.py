@@ -1,0 +1,311 @@
+"""MI355X training engine for the ResNet-18-shaped CNN (BASELINE config 4).
+
+A static execution plan, not an autograd graph: every activation, gradient
+and statistics buffer is allocated once for the fixed per-GPU batch, and a
+step is a fixed sequence of hand-written HIP kernels (csrc/kernels/conv.hip,
+cnn_aux.hip, elementwise.hip) -- so it can be captured whole in a hipGraph
+and replayed with zero host work (the data batch is chosen by a device-side
+cursor, like the MLP engine).
+
+Per step:
+  forward   input_norm -> [conv (+BN stats in the epilogue) -> bn_finalize ->
+            bn_apply(+residual, ReLU)] x 20 -> avgpool -> fc (fp32 logits) ->
+            softmax-CE (loss, dlogits, dbias)
+  backward  per block, in reverse: bn_bwd_reduce/finalize/apply (ReLU mask
+            fused), conv wgrad (split-K, fp32 atomics straight into the flat
+            gradient) and dgrad (residual gradient fused into its epilogue)
+  comms     optional: the flat gradient is laid out in forward order, so
+            when a block's backward is done its whole parameter range is final
+            -> a bucket hook can launch RCCL all-reduce of that range while
+            backward continues
+  update    one multi-tensor SGD launch over the flat vector (fp32 master,
+            momentum, weight decay, bf16 shadow) + one launch that re-lays the
+            bf16 conv weights out for dgrad.
+"""
+from __future__ import annotations
+
+import torch
+
+from .mlp import StepStats
+from .resnet import CIFAR_MEAN, CIFAR_STD, BlockSpec, BNSpec, ConvSpec, init_params, resnet18_spec
+
+LOGIT_LD = 16  # dlogits row stride (classes padded for 16-B gathers)
+
+
+class _BN:
+    def __init__(self, spec: BNSpec, params, grad, arena, off, dev):
+        c = spec.c
+        self.spec = spec
+        self.gamma = params[spec.g_off:spec.g_off + c]
+        self.beta = params[spec.b_off:spec.b_off + c]
+        self.ggamma = grad[spec.g_off:spec.g_off + c]
+        self.gbeta = grad[spec.b_off:spec.b_off + c]
+        self.stats = arena[off:off + 2 * c]
+        self.sums = arena[off + 2 * c:off + 4 * c]
+        self.coef = torch.zeros(4 * c, device=dev)
+        self.dcoef = torch.zeros(3 * c, device=dev)
+        self.run_mean = torch.zeros(c, device=dev)
+        self.run_var = torch.ones(c, device=dev)
+
+
+class _Conv:
+    def __init__(self, spec: ConvSpec, params, shadow, grad, dev, ld_out=None):
+        self.spec = spec
+        self.w = shadow[spec.off:spec.off + spec.numel]
+        self.g = grad[spec.off:spec.off + spec.numel]
+        self.ldt = ld_out or spec.cout  # dgrad source channels
+        self.wt = torch.zeros(spec.cin * spec.k * spec.k * self.ldt, dtype=torch.bfloat16, device=dev)
+
+
+class FusedResNetTrainer:
+    def __init__(self, batch: int, device="cuda", lr: float = 0.05, momentum: float = 0.9,
+                 weight_decay: float = 5e-4, seed: int = 0, world_size: int = 1, stem: str = "cifar",
+                 classes: int = 10, flat: torch.Tensor | None = None, bn_momentum: float = 0.1,
+                 in_hw: int | None = None):
+        from ..ops import _native
+        from ..ops import cnn as K
+        from ..ops import optim as O
+
+        _native.lib()
+        self.K, self.O = K, O
+        self.spec = spec = resnet18_spec(stem, classes, in_hw)
+        dev = self.device = torch.device(device)
+        self.batch = B = batch
+        self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
+        self.world_size = world_size
+        self.grad_scale = 1.0 / (batch * world_size)
+        self.bn_momentum = bn_momentum
+        n = spec.n_flat
+        self.params = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.params.copy_((flat if flat is not None else init_params(spec, seed)).to(dev))
+        self.mom = torch.zeros_like(self.params) if momentum > 0 else None
+        self.grad = torch.zeros_like(self.params)
+        self.shadow = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        bns = list(spec.bns())
+        self.arena = torch.zeros(sum(4 * b.c for b in bns), device=dev)
+        off = 0
+        self.bn = {}
+        for b in bns:
+            self.bn[b.name] = _BN(b, self.params, self.grad, self.arena, off, dev)
+            off += 4 * b.c
+        self.conv = {c.name: _Conv(c, self.params, self.shadow, self.grad, dev) for c in spec.convs()}
+        self.fc_w = self.shadow[spec.fc_w:spec.fc_w + classes * 512]
+        self.fc_b = self.params[spec.fc_b:spec.fc_b + classes]
+        self.fc_gw = self.grad[spec.fc_w:spec.fc_w + classes * 512]
+        self.fc_gb = self.grad[spec.fc_b:spec.fc_b + classes]
+        self.fc_wt = torch.zeros(512 * LOGIT_LD, dtype=torch.bfloat16, device=dev)
+
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        hw = spec.in_hw
+        self.x0 = torch.empty(B, hw, hw, 8, **bf)
+        self.labels = torch.zeros(B, dtype=torch.uint8, device=dev)
+        # ---- stem buffers ----
+        sc = spec.stem_conv
+        s_hw = K.out_size(hw, sc.k, sc.stride, sc.pad)
+        self.c0 = torch.empty(B, s_hw, s_hw, 64, **bf)
+        self.a0 = torch.empty_like(self.c0)
+        self.dc0 = torch.empty_like(self.c0)
+        self.da0 = torch.empty_like(self.c0)
+        cur = self.a0
+        if spec.stem == "imagenet":
+            p_hw = K.out_size(s_hw, 3, 2, 1)
+            self.p0 = torch.empty(B, p_hw, p_hw, 64, **bf)
+            self.p0_arg = torch.empty(B, p_hw, p_hw, 64, dtype=torch.uint8, device=dev)
+            self.dp0 = torch.empty_like(self.p0)
+            cur = self.p0
+        # ---- residual blocks ----
+        self.blocks = []
+        for blk in spec.blocks:
+            st = {"spec": blk, "x": cur}
+            h = cur.shape[1]
+            oh = K.out_size(h, 3, blk.conv1.stride, 1)
+            shp = (B, oh, oh, blk.conv1.cout)
+            for name in ("c1", "a1", "c2", "y", "dz", "dc2", "da1", "dc1"):
+                st[name] = torch.empty(shp, **bf)
+            if blk.down is not None:
+                st["cs"] = torch.empty(shp, **bf)
+                st["dcs"] = torch.empty(shp, **bf)
+                st["dxs"] = torch.empty_like(cur)
+            st["dx"] = torch.empty_like(cur)
+            self.blocks.append(st)
+            cur = st["y"]
+        self.feat_in = cur
+        self.feat = torch.empty(B, 1, 1, 512, **bf)
+        self.dfeat = torch.empty_like(self.feat)
+        self.dfeat_in = torch.empty_like(cur)
+        self.logits = torch.empty(B, classes, device=dev)
+        self.dlogits = torch.zeros(B, 1, 1, LOGIT_LD, **bf)
+        self.loss = torch.zeros(B, device=dev)
+        self.correct = torch.zeros(B, device=dev)
+        self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.x = self.y = None
+        self.graph = None
+        self.bucket_hook = None   # callable(flat_view) -> handle, launched during backward
+        self.bucket_wait = None   # callable(handles) -> None, before the optimizer
+        self.allreduce = None     # callable(grad) -> None (simple, non-overlapped)
+        self.bucket_bytes = 16 << 20
+
+        items = [(c.w, c.wt, c.spec.cout, c.spec.k * c.spec.k, c.spec.cin, c.ldt)
+                 for c in self.conv.values() if c.spec.name != "stem"]
+        items.append((self.fc_w, self.fc_wt, classes, 1, 512, LOGIT_LD))
+        self.wt = K.WeightTransposer(items, dev)
+        self.refresh_shadows()
+
+    # ------------------------------------------------------------------
+    def refresh_shadows(self) -> None:
+        self.O.to_bf16(self.params, self.shadow)
+        self.wt()
+
+    def load_shard(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> None:
+        hw = self.spec.in_hw
+        x = x_u8.reshape(-1, hw, hw, 3)
+        if x.shape[0] < self.batch:
+            raise ValueError("shard smaller than one batch")
+        self.x = x.to(self.device, non_blocking=True).contiguous()
+        self.y = y_u8.reshape(-1).to(self.device, non_blocking=True).to(torch.uint8).contiguous()
+        self.graph = None
+
+    # ------------------------------------------------------------------
+    def _conv_bn(self, x, conv: _Conv, bn: _BN, out):
+        K = self.K
+        c = conv.spec
+        K.conv_fwd(x, conv.w, c.cout, c.k, c.stride, c.pad, y=out, stats=bn.stats)
+        K.bn_finalize(bn.stats, bn.gamma, bn.beta, bn.coef, bn.run_mean, bn.run_var,
+                      out.numel() // c.cout, momentum=self.bn_momentum)
+
+    def forward(self, train: bool = True):
+        K, spec = self.K, self.spec
+        self.arena.zero_()
+        K.input_norm(self.x, self.y, self.cursor, self.batch, self.x0, self.labels, CIFAR_MEAN, CIFAR_STD)
+        sbn = self.bn[spec.stem_bn.name]
+        self._conv_bn(self.x0, self.conv["stem"], sbn, self.c0)
+        K.bn_apply(self.c0, sbn.coef, self.a0, relu=True)
+        if spec.stem == "imagenet":
+            K.maxpool_fwd(self.a0, self.p0, self.p0_arg)
+        for st in self.blocks:
+            blk: BlockSpec = st["spec"]
+            b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
+            self._conv_bn(st["x"], self.conv[blk.conv1.name], b1, st["c1"])
+            K.bn_apply(st["c1"], b1.coef, st["a1"], relu=True)
+            self._conv_bn(st["a1"], self.conv[blk.conv2.name], b2, st["c2"])
+            if blk.down is not None:
+                bd = self.bn[blk.dbn.name]
+                self._conv_bn(st["x"], self.conv[blk.down.name], bd, st["cs"])
+                K.bn_apply(st["c2"], b2.coef, st["y"], relu=True, res=st["cs"], rcoef=bd.coef)
+            else:
+                K.bn_apply(st["c2"], b2.coef, st["y"], relu=True, res=st["x"])
+        K.avgpool_fwd(self.feat_in, self.feat)
+        K.conv_fwd(self.feat, self.fc_w, spec.classes, 1, 1, 0, yf=self.logits, bias=self.fc_b)
+        K.softmax_ce(self.logits, self.labels, self.loss, self.correct, self.dlogits.view(self.batch, LOGIT_LD),
+                     self.fc_gb if train else None, self.grad_scale)
+
+    def backward(self):
+        K, spec = self.K, self.spec
+        handles = []
+        pending_from = spec.n_flat  # grad[pending_from:] is final and not yet reduced
+        bucket_elems = self.bucket_bytes // 4
+
+        def maybe_bucket(lo, force=False):
+            nonlocal pending_from
+            if self.bucket_hook is None:
+                return
+            if force or (pending_from - lo) >= bucket_elems:
+                handles.append(self.bucket_hook(self.grad[lo:pending_from]))
+                pending_from = lo
+
+        K.conv_wgrad(self.feat, self.dlogits, spec.classes, 1, 1, 0, self.fc_gw)
+        K.conv_dgrad(self.dlogits, self.fc_wt, 512, 1, 1, 0, self.dfeat)
+        K.avgpool_bwd(self.dfeat.view(self.batch, 512), self.dfeat_in)
+        dy = self.dfeat_in
+        for st in reversed(self.blocks):
+            blk: BlockSpec = st["spec"]
+            c1, c2 = self.conv[blk.conv1.name], self.conv[blk.conv2.name]
+            b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
+            n1 = st["c1"].numel() // blk.conv1.cout
+            # y = relu(bn2(c2) + sc): dz = dy * 1[y > 0] feeds bn2 and the shortcut
+            K.bn_bwd_reduce(dy, st["y"], st["c2"], b2.sums, dz_out=st["dz"])
+            K.bn_bwd_finalize(b2.sums, b2.coef, b2.dcoef, b2.ggamma, b2.gbeta, n1)
+            add = st["dz"]
+            if blk.down is not None:
+                cd, bd = self.conv[blk.down.name], self.bn[blk.dbn.name]
+                K.bn_bwd_reduce(st["dz"], None, st["cs"], bd.sums)
+                K.bn_bwd_finalize(bd.sums, bd.coef, bd.dcoef, bd.ggamma, bd.gbeta, n1)
+                K.bn_bwd_apply(st["dz"], None, st["cs"], bd.dcoef, st["dcs"])
+                K.conv_wgrad(st["x"], st["dcs"], blk.down.cout, 1, blk.down.stride, 0, cd.g)
+                K.conv_dgrad(st["dcs"], cd.wt, blk.down.cin, 1, blk.down.stride, 0, st["dxs"])
+                add = st["dxs"]
+            K.bn_bwd_apply(st["dz"], None, st["c2"], b2.dcoef, st["dc2"])
+            K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g)
+            K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"])
+            K.bn_bwd_reduce(st["da1"], st["a1"], st["c1"], b1.sums)
+            K.bn_bwd_finalize(b1.sums, b1.coef, b1.dcoef, b1.ggamma, b1.gbeta, n1)
+            K.bn_bwd_apply(st["da1"], st["a1"], st["c1"], b1.dcoef, st["dc1"])
+            K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g)
+            K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, st["dx"], add=add)
+            dy = st["dx"]
+            maybe_bucket(blk.conv1.off)
+        # stem
+        sbn = self.bn[spec.stem_bn.name]
+        if spec.stem == "imagenet":
+            K.maxpool_bwd(dy, self.p0_arg, self.da0)
+            dy = self.da0
+        n0 = self.c0.numel() // 64
+        K.bn_bwd_reduce(dy, self.a0, self.c0, sbn.sums)
+        K.bn_bwd_finalize(sbn.sums, sbn.coef, sbn.dcoef, sbn.ggamma, sbn.gbeta, n0)
+        K.bn_bwd_apply(dy, self.a0, self.c0, sbn.dcoef, self.dc0)
+        sc = spec.stem_conv
+        K.conv_wgrad(self.x0, self.dc0, 64, sc.k, sc.stride, sc.pad, self.conv["stem"].g)
+        maybe_bucket(0, force=True)
+        return handles
+
+    def _step_eager(self) -> None:
+        self.grad.zero_()
+        self.forward(train=True)
+        handles = self.backward()
+        if self.bucket_wait is not None:
+            self.bucket_wait(handles)
+        if self.allreduce is not None:
+            self.allreduce(self.grad)
+        self.O.sgd_flat(self.params, self.grad, self.mom, self.lr, self.momentum, self.weight_decay,
+                        shadow=self.shadow)
+        self.wt()
+        self.K.cursor_bump(self.cursor)
+
+    def step(self) -> None:
+        if self.graph is not None:
+            self.graph.replay()
+            return
+        self._step_eager()
+
+    def capture(self, warmup: int = 2) -> None:
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step_eager()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_eager()
+        self.graph = g
+
+    # ------------------------------------------------------------------
+    def compute_grads(self) -> torch.Tensor:
+        """Forward + backward on the current batch (no update, no cursor bump)."""
+        self.grad.zero_()
+        self.forward(train=True)
+        self.backward()
+        return self.grad
+
+    def stats(self) -> StepStats:
+        return StepStats(float(self.loss.sum()) / self.batch, float(self.correct.sum()) / self.batch, self.batch)
+
+    def get_flat(self) -> torch.Tensor:
+        return self.params.clone()
+
+    def set_flat(self, flat: torch.Tensor) -> None:
+        self.params.copy_(flat.to(self.params))
+        self.refresh_shadows()
+
+    def running_stats(self) -> dict:
+        return {name: (b.run_mean, b.run_var) for name, b in self.bn.items()}

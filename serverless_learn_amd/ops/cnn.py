@@ -1,0 +1,187 @@
+"""ctypes bindings of the CNN kernels (csrc/kernels/conv.hip, cnn_aux.hip).
+
+Thin, shape-checked wrappers: every function takes torch tensors (NHWC bf16
+activations, fp32 statistics/gradients) and launches on the current stream,
+so the CNN engine's whole step can be captured in a hipGraph.  No fallback:
+on a GPU box a missing or failing kernel raises.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as N
+
+P, I, L, F = N.P, N.I, N.L, N.F
+
+N.register("sl_conv_fwd", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, I, P, P, P, P])
+N.register("sl_conv_dgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, P, P])
+N.register("sl_conv_wgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, I, P])
+N.register("sl_conv_wt", [P, I, L, P])
+N.register("sl_conv_wt_desc_size", [])
+N.register("sl_input_norm", [P, P, P, I, I, L, P, P, F, F, F, F, F, F, P])
+N.register("sl_cursor_bump", [P, P])
+N.register("sl_bn_finalize", [P, P, P, P, P, P, I, F, F, F, P])
+N.register("sl_bn_apply", [P, P, P, P, P, L, I, I, I, P])
+N.register("sl_bn_bwd_reduce", [P, P, P, P, P, L, I, P])
+N.register("sl_bn_bwd_finalize", [P, P, P, P, P, I, F, P])
+N.register("sl_bn_bwd_apply", [P, P, P, P, P, L, I, P])
+N.register("sl_maxpool_fwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
+N.register("sl_maxpool_bwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
+N.register("sl_avgpool_fwd", [P, P, I, I, I, P])
+N.register("sl_avgpool_bwd", [P, P, I, I, I, P])
+N.register("sl_softmax_ce", [P, P, P, P, P, I, P, I, I, F, P])
+
+p = N.ptr
+
+
+def _bf16(t):
+    assert t.dtype == torch.bfloat16 and t.is_contiguous(), (t.dtype, t.shape)
+    return p(t)
+
+
+def _f32(t):
+    if t is None:
+        return None
+    assert t.dtype == torch.float32 and t.is_contiguous()
+    return p(t)
+
+
+def out_size(h: int, k: int, s: int, pad: int) -> int:
+    return (h + 2 * pad - k) // s + 1
+
+
+def conv_fwd(x, w, cout: int, k: int, stride: int, pad: int, y=None, yf=None, bias=None, stats=None, ldy=None):
+    """x [N,H,W,C] bf16, w [cout, k*k*C] bf16 -> y [N,OH,OW,ldy] bf16 and/or yf [N*OH*OW, cout] fp32."""
+    n, h, wd, c = x.shape
+    oh, ow = out_size(h, k, stride, pad), out_size(wd, k, stride, pad)
+    assert w.numel() >= cout * k * k * c
+    if y is not None:
+        assert y.shape[:3] == (n, oh, ow), (y.shape, n, oh, ow)
+        ldy = y.shape[3]
+    N.call("sl_conv_fwd", _bf16(x), n, h, wd, c, _bf16(w), cout, k, k, stride, pad, oh, ow,
+           _bf16(y) if y is not None else None, int(ldy or cout), _f32(yf), _f32(bias), _f32(stats), N.stream_ptr())
+    return oh, ow
+
+
+def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None):
+    """dy [N,OH,OW,Cd] bf16 (Cd channels, zero beyond cout), wt [cin, k*k*Cd] -> dx [N,H,W,cin] (+ add)."""
+    n, oh, ow, cd = dy.shape
+    _, h, wd, ci = dx.shape
+    assert ci == cin
+    if add is not None:
+        assert add.shape == dx.shape and add.dtype == torch.bfloat16
+    N.call("sl_conv_dgrad", _bf16(dy), n, oh, ow, cd, _bf16(wt), cin, k, k, stride, pad, h, wd, _bf16(dx),
+           _bf16(add) if add is not None else None, N.stream_ptr())
+
+
+def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: int = 1024):
+    """dw [cout, k*k*C] fp32 += sum over pixels dy^T im2col(x)."""
+    n, h, wd, c = x.shape
+    _, oh, ow, ldy = dy.shape
+    assert dw.dtype == torch.float32 and dw.numel() >= cout * k * k * c
+    N.call("sl_conv_wgrad", _bf16(x), n, h, wd, c, _bf16(dy), ldy, cout, k, k, stride, pad, oh, ow, p(dw),
+           int(target_wgs), N.stream_ptr())
+
+
+class WtDesc(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("wt", ctypes.c_void_p), ("cout", ctypes.c_int), ("taps", ctypes.c_int),
+                ("cin", ctypes.c_int), ("ldt", ctypes.c_int), ("begin", ctypes.c_long)]
+
+
+class WeightTransposer:
+    """Multi-tensor Wt[ci][tap][co] = W[co][tap][ci] for every conv (one launch)."""
+
+    def __init__(self, items, device):
+        """items: [(w_bf16_view, wt_bf16_view, cout, taps, cin, ldt)]"""
+        assert ctypes.sizeof(WtDesc) == N.lib().sl_conv_wt_desc_size()
+        arr = (WtDesc * len(items))()
+        total = 0
+        for i, (w, wt, cout, taps, cin, ldt) in enumerate(items):
+            assert wt.numel() == cin * taps * ldt and w.numel() >= cout * taps * cin
+            arr[i] = WtDesc(p(w), p(wt), cout, taps, cin, ldt, total)
+            total += wt.numel()
+        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self.desc = host.to(device)
+        self.n = len(items)
+        self.total = total
+
+    def __call__(self):
+        N.call("sl_conv_wt", p(self.desc), self.n, self.total, N.stream_ptr())
+
+
+def input_norm(x_u8, labels, cursor, batch: int, y, lab_out, mean, std):
+    """Batch ``cursor % n_batches`` of the shard x_u8 [n,H,W,3] -> y [batch,H,W,8] bf16 (+ labels)."""
+    assert x_u8.dtype == torch.uint8 and x_u8.shape[-1] == 3 and y.shape[-1] == 8
+    img = x_u8.shape[1] * x_u8.shape[2]
+    n_batches = x_u8.shape[0] // batch
+    assert n_batches >= 1 and y.shape[0] == batch
+    N.call("sl_input_norm", p(x_u8), p(labels), p(cursor), n_batches, batch, img, _bf16(y), p(lab_out),
+           *[float(v) for v in mean], *[float(v) for v in std], N.stream_ptr())
+
+
+def cursor_bump(cursor):
+    N.call("sl_cursor_bump", p(cursor), N.stream_ptr())
+
+
+def bn_finalize(stats, gamma, beta, coef, run_mean, run_var, count, eps=1e-5, momentum=0.1):
+    c = gamma.numel()
+    N.call("sl_bn_finalize", _f32(stats), _f32(gamma), _f32(beta), _f32(coef), _f32(run_mean), _f32(run_var), c,
+           float(count), float(eps), float(momentum), N.stream_ptr())
+
+
+def bn_apply(x, coef, y, relu=True, res=None, rcoef=None):
+    c = x.shape[-1]
+    rows = x.numel() // c
+    mode = 0 if res is None else (2 if rcoef is not None else 1)
+    N.call("sl_bn_apply", _bf16(x), _f32(coef), _bf16(res) if res is not None else None, _f32(rcoef), _bf16(y),
+           rows, c, 1 if relu else 0, mode, N.stream_ptr())
+
+
+def bn_bwd_reduce(dy, y, x, sums, dz_out=None):
+    c = x.shape[-1]
+    rows = x.numel() // c
+    N.call("sl_bn_bwd_reduce", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x),
+           _bf16(dz_out) if dz_out is not None else None, _f32(sums), rows, c, N.stream_ptr())
+
+
+def bn_bwd_finalize(sums, coef, dcoef, grad_gamma, grad_beta, count):
+    c = grad_gamma.numel()
+    N.call("sl_bn_bwd_finalize", _f32(sums), _f32(coef), _f32(dcoef), _f32(grad_gamma), _f32(grad_beta), c,
+           float(count), N.stream_ptr())
+
+
+def bn_bwd_apply(dy, y, x, dcoef, dx):
+    c = x.shape[-1]
+    rows = x.numel() // c
+    N.call("sl_bn_bwd_apply", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x), _f32(dcoef), _bf16(dx),
+           rows, c, N.stream_ptr())
+
+
+def maxpool_fwd(x, y, arg, k=3, s=2, pad=1):
+    n, h, w, c = x.shape
+    _, oh, ow, _ = y.shape
+    N.call("sl_maxpool_fwd", _bf16(x), _bf16(y), p(arg), n, h, w, c, oh, ow, k, s, pad, N.stream_ptr())
+
+
+def maxpool_bwd(dy, arg, dx, k=3, s=2, pad=1):
+    n, h, w, c = dx.shape
+    _, oh, ow, _ = dy.shape
+    N.call("sl_maxpool_bwd", _bf16(dy), p(arg), _bf16(dx), n, h, w, c, oh, ow, k, s, pad, N.stream_ptr())
+
+
+def avgpool_fwd(x, y):
+    n, h, w, c = x.shape
+    N.call("sl_avgpool_fwd", _bf16(x), _bf16(y), n, h * w, c, N.stream_ptr())
+
+
+def avgpool_bwd(dy, dx):
+    n, h, w, c = dx.shape
+    N.call("sl_avgpool_bwd", _bf16(dy), _bf16(dx), n, h * w, c, N.stream_ptr())
+
+
+def softmax_ce(logits, labels, loss, correct, dlogits, dbias, grad_scale):
+    n, ncls = logits.shape
+    N.call("sl_softmax_ce", _f32(logits), p(labels), _f32(loss), _f32(correct), _bf16(dlogits), dlogits.shape[-1],
+           _f32(dbias), n, ncls, float(grad_scale), N.stream_ptr())

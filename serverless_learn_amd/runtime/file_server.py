@@ -98,7 +98,7 @@ class FileServer:
                 data = core().reference_dummy_file(self.cfg.dummy_file_length)
             else:
                 data = make_shard(self.cfg.shard_records, shard_index=file_num,
-                                  num_shards=self.cfg.num_shards, seed=self.cfg.seed)
+                                  num_shards=self.cfg.num_shards, seed=self.cfg.seed, dataset=self.cfg.dataset)
             with self._lock:
                 self._files[file_num] = data
             self.log.info("file_ready", file_num=file_num, bytes=len(data), gen_s=round(time.perf_counter() - t0, 3))

@@ -95,10 +95,11 @@ class _Sink:
         return pb.ReceiveFileAck(ok=True).SerializeToString()
 
 
-def fetch_shard_via_grpc(n_records: int, shard_index: int = 0, num_shards: int = 1, seed: int = 0) -> bytes:
+def fetch_shard_via_grpc(n_records: int, shard_index: int = 0, num_shards: int = 1, seed: int = 0,
+                         dataset: str = "synthetic-mnist") -> bytes:
     """Serve shard ``shard_index`` from an in-process file server and receive it over gRPC."""
     cfg = Config.from_env(file_server_addr="127.0.0.1:0", shard_records=n_records, num_shards=num_shards,
-                          seed=seed)
+                          seed=seed, dataset=dataset)
     fs = FileServer(cfg, addr="127.0.0.1:0").start()
     sink = _Sink()
     try:
