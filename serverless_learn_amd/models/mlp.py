@@ -174,6 +174,18 @@ class CPUTrainer:
         self.allreduce = None  # callable(tensor) -> None (sum in place)
         self._last = None
 
+    n_params = N_PARAMS
+    model_name = "mlp-784-256-256-10"
+
+    def layout(self):
+        return [[n, list(s), o] for n, s, o, _ in param_layout()]
+
+    def set_world(self, world: int) -> None:
+        self.world_size = world
+
+    def refresh_shadows(self) -> None:
+        pass
+
     def load_shard(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> None:
         assert x_u8.shape[0] >= self.batch
         self.x, self.y = x_u8.reshape(-1, D_IN), y_u8.reshape(-1)
@@ -260,6 +272,18 @@ class FusedMLPTrainer:
         self.n_batches = 1
         self.graph = None
         self.refresh_shadows()
+
+    n_params = N_PARAMS
+    model_name = "mlp-784-256-256-10"
+
+    def layout(self):
+        return [[n, list(s), o] for n, s, o, _ in param_layout()]
+
+    def set_world(self, world: int) -> None:
+        """Gradient scale follows the group size (mean over the global batch)."""
+        self.world_size = world
+        self.grad_scale = 1.0 / (self.batch * world)
+        self.graph = None
 
     # ---- data ----
     def load_shard(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> None:

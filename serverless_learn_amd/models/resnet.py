@@ -159,6 +159,19 @@ def resnet18_spec(stem: str = "cifar", classes: int = 10, in_hw: int | None = No
     return spec
 
 
+def spec_layout(spec: ResNetSpec) -> list:
+    """[name, shape, offset] of every tensor in the flat vector (checkpoint metadata)."""
+    out = []
+    for c in spec.convs():
+        out.append([c.name + ".weight", [c.cout, c.k, c.k, c.cin], c.off])
+    for b in spec.bns():
+        out.append([b.name + ".weight", [b.c], b.g_off])
+        out.append([b.name + ".bias", [b.c], b.b_off])
+    out.append(["fc.weight", [spec.classes, 512], spec.fc_w])
+    out.append(["fc.bias", [spec.classes], spec.fc_b])
+    return sorted(out, key=lambda e: e[2])
+
+
 def init_params(spec: ResNetSpec, seed: int = 0) -> torch.Tensor:
     """Kaiming-normal (fan_out, relu) convs, BN gamma=1/beta=0, nn.Linear-style FC."""
     g = torch.Generator().manual_seed(seed)
@@ -244,9 +257,27 @@ class CPUResNetTrainer:
         self.params = (flat if flat is not None else init_params(self.spec, seed)).clone().float()
         self.mom = torch.zeros_like(self.params) if momentum > 0 else None
         self.running = running_stats(self.spec)
+        self.x = self.y = None
         self.cursor = 0
         self.allreduce = None
         self._last = None
+
+    @property
+    def n_params(self) -> int:
+        return self.spec.n_flat
+
+    @property
+    def model_name(self) -> str:
+        return f"resnet18-{self.spec.stem}"
+
+    def layout(self):
+        return spec_layout(self.spec)
+
+    def set_world(self, world: int) -> None:
+        self.world_size = world
+
+    def refresh_shadows(self) -> None:
+        pass
 
     def load_shard(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> None:
         hw = self.spec.in_hw

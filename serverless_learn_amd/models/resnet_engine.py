@@ -151,6 +151,24 @@ class FusedResNetTrainer:
         self.wt = K.WeightTransposer(items, dev)
         self.refresh_shadows()
 
+    @property
+    def n_params(self) -> int:
+        return self.spec.n_flat
+
+    @property
+    def model_name(self) -> str:
+        return f"resnet18-{self.spec.stem}"
+
+    def layout(self):
+        from .resnet import spec_layout
+
+        return spec_layout(self.spec)
+
+    def set_world(self, world: int) -> None:
+        self.world_size = world
+        self.grad_scale = 1.0 / (self.batch * world)
+        self.graph = None
+
     # ------------------------------------------------------------------
     def refresh_shadows(self) -> None:
         self.O.to_bf16(self.params, self.shadow)

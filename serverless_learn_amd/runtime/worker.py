@@ -13,7 +13,8 @@ Here a worker:
 * lands ``ReceiveFile`` chunks through the native pinned ring straight into
   HBM (data shards) or host memory (checkpoints), then swaps the resident
   shard into the trainer at a step boundary;
-* trains the real model: the fused HIP MLP on MI355X (FusedMLPTrainer) or the
+* trains the real model (``Config.model``: the MLP or the ResNet-18-shaped CNN):
+  the hand-written HIP engines on MI355X (FusedMLPTrainer / FusedResNetTrainer) or the
   torch reference on CPU, or -- ``model="simulate"`` -- the reference's
   vector += 1 every ``simulated_train_interval_ms``;
 * synchronizes per ``sync``: ``allreduce`` (RCCL/gloo group re-formed from the
@@ -38,7 +39,7 @@ from .._core import core
 from ..ckpt import format as ckfmt
 from ..config import Config
 from ..data.synthetic import HEADER_SIZE, MAGIC as SHARD_MAGIC, decode_header
-from ..models import mlp as M
+from ..models import make_trainer
 from ..parallel.dp import ElasticGroup, GroupBroken
 from ..parallel.gossip import GossipState
 from ..proto import messages as pb
@@ -106,29 +107,20 @@ class Worker:
         world = max(1, self.view["world"]) if self.cfg.sync == "allreduce" else 1
         kw = dict(batch=self.cfg.batch, lr=self.cfg.lr, momentum=self.cfg.momentum,
                   weight_decay=self.cfg.weight_decay, seed=self.cfg.seed, world_size=world)
-        if self.device.type == "cuda":
-            self.trainer = M.FusedMLPTrainer(device=self.device, **kw)
-        else:
-            self.trainer = M.CPUTrainer(**kw)
+        self.trainer = make_trainer(self.cfg.model, self.device, **kw)
         if self.cfg.sync in ("gossip", "ps"):
             self.gossip = GossipState(self._flat_view(), self.cfg.learn_rate, self.cfg.gossip_compat)
 
     def _flat_view(self) -> torch.Tensor:
-        return self.trainer.params[:M.N_PARAMS]
+        return self.trainer.params[:self.trainer.n_params]
 
     def _after_external_update(self):
-        if isinstance(self.trainer, M.FusedMLPTrainer):
-            self.trainer.refresh_shadows()
+        self.trainer.refresh_shadows()
 
     def _set_world(self, world: int):
         """Gradient scale follows the group size (mean over the global batch)."""
-        t = self.trainer
-        if t is None:
-            return
-        t.world_size = world
-        if isinstance(t, M.FusedMLPTrainer):
-            t.grad_scale = 1.0 / (t.batch * world)
-            t.graph = None
+        if self.trainer is not None:
+            self.trainer.set_world(world)
 
     # ---- RPC handlers --------------------------------------------------------
     def _receive_file(self, requests, context) -> bytes:
@@ -172,7 +164,7 @@ class Worker:
         kind = "data"
         if is_shard:
             hdr = decode_header(head)
-            n, d = hdr["n"], hdr["height"] * hdr["width"]
+            n, d = hdr["n"], hdr["height"] * hdr["width"] * hdr["channels"]
             if isinstance(buf, np.ndarray):
                 buf = torch.from_numpy(buf)
             x = buf[HEADER_SIZE:HEADER_SIZE + n * d].view(n, d)
@@ -219,12 +211,15 @@ class Worker:
             self._ensure_trainer()
             if self.trainer is None:
                 return
+            if meta.get("model", self.trainer.model_name) != self.trainer.model_name:
+                self.log.warn("checkpoint_model_mismatch", ckpt=meta.get("model"), running=self.trainer.model_name)
+                return
             if meta.get("step", 0) < self.step:
                 self.log.info("checkpoint_skipped", ckpt_step=meta.get("step"), step=self.step)
                 return
             self.trainer.set_flat(torch.from_numpy(params))
             if mom is not None and self.trainer.mom is not None:
-                self.trainer.mom[:M.N_PARAMS].copy_(torch.from_numpy(mom))
+                self.trainer.mom[:self.trainer.n_params].copy_(torch.from_numpy(mom))
             self.step = int(meta.get("step", 0))
             if self.gossip is not None:
                 self.gossip.old.copy_(self._flat_view())
@@ -233,9 +228,10 @@ class Worker:
     def save_checkpoint(self) -> int:
         with self.train_lock:
             flat = self.trainer.get_flat().cpu().numpy()
-            mom = self.trainer.mom[:M.N_PARAMS].cpu().numpy() if self.trainer.mom is not None else None
-            meta = {"model": "mlp-784-256-256-10", "step": self.step, "epoch": self.group.epoch,
-                    "layout": [[n, list(s), o] for n, s, o, _ in M.param_layout()],
+            n = self.trainer.n_params
+            mom = self.trainer.mom[:n].cpu().numpy() if self.trainer.mom is not None else None
+            meta = {"model": self.trainer.model_name, "step": self.step, "epoch": self.group.epoch,
+                    "layout": self.trainer.layout(),
                     "optimizer": {"lr": self.cfg.lr, "momentum": self.cfg.momentum}}
         data = ckfmt.encode(flat, meta, mom)
         file_num = ckfmt.CKPT_BASE + self.ckpt_slot

@@ -71,3 +71,21 @@ def test_checkpoint_then_new_worker_resumes(cluster):
     from serverless_learn_amd.ckpt.format import CKPT_BASE
 
     assert any(f >= CKPT_BASE for f in b.files_received)
+
+
+def test_resnet_worker_trains_on_cifar_shards():
+    """BASELINE config 4 plumbing on CPU: the CNN trains from pushed CIFAR-shaped shards."""
+    c = LocalCluster(fast_config(dataset="synthetic-cifar", shard_records=64))
+    try:
+        w = c.add_worker(sync="none", model="resnet18", batch=8, max_steps=3, lr=0.01)
+        assert c.wait_for(lambda: w.state == "done", 120), (w.state, w.step)
+        assert w.trainer.model_name == "resnet18-cifar"
+        assert w.trainer.x.shape[1:] == (32, 32, 3)
+        assert np.isfinite(w.trainer.stats().loss)
+        fn = w.save_checkpoint()
+        from serverless_learn_amd.ckpt.format import decode
+
+        meta, params, _ = decode(c.file_server.get_file(fn))
+        assert meta["model"] == "resnet18-cifar" and params.size == w.trainer.n_params
+    finally:
+        c.stop()

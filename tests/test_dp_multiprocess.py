@@ -62,3 +62,43 @@ def test_gloo_dp_matches_single_process(tmp_path):
     for _ in range(STEPS):
         ref.step()
     assert torch.allclose(p0, ref.params, atol=3e-4, rtol=1e-3), (p0 - ref.params).abs().max()
+
+
+def _resnet_rank_main(rank, world, port, out_path):
+    import torch.distributed as dist
+
+    from serverless_learn_amd.data.synthetic import make_cifar_like
+    from serverless_learn_amd.models.resnet import CPUResNetTrainer
+
+    torch.set_num_threads(2)
+    if rank == 0:
+        store = dist.TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False)  # noqa: F841
+    g = ElasticGroup(device=torch.device("cpu"), timeout_s=60)
+    assert g.reform(1, rank, world, f"127.0.0.1:{port}")
+    x, y = make_cifar_like(8, seed=10 + rank)
+    tr = CPUResNetTrainer(batch=4, lr=0.05, world_size=world, seed=5)
+    tr.load_shard(torch.from_numpy(x), torch.from_numpy(y))
+    tr.allreduce = g.allreduce_
+    for _ in range(2):
+        tr.step()
+    torch.save(tr.params, out_path)
+    g.teardown()
+
+
+def test_gloo_dp_resnet_ranks_stay_identical(tmp_path):
+    """Different data per rank, one all-reduced gradient: replicas must not drift."""
+    world = 2
+    port = _free_port()
+    outs = [str(tmp_path / f"r{r}.pt") for r in range(world)]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_resnet_rank_main, args=(r, world, port, outs[r])) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    p0, p1 = (torch.load(o, weights_only=True) for o in outs)
+    assert torch.equal(p0, p1)
+    from serverless_learn_amd.models.resnet import init_params, resnet18_spec
+
+    assert not torch.equal(p0, init_params(resnet18_spec(), 5))
