@@ -4,16 +4,23 @@
 // /root/reference/src/worker.cc:221-231, `model[i] += 1` every 2 s) with
 // a real bf16 MFMA forward/backward + SGD.  The step is three launches:
 //
-//   K_rows  (mlp_rows_kernel)  one workgroup per 64 batch rows: u8 pixels are
-//           normalised into LDS, then L1 -> ReLU -> L2 -> ReLU -> L3 ->
-//           softmax-CE -> dZ -> dH2 -> dH1, all row-local, activations kept
-//           in LDS; ReLU masks kept as bits in registers.  It writes the
-//           operands of the weight gradients TRANSPOSED ([feature][batch])
-//           so that the batch (= reduction) index is contiguous for MFMA.
-//   K_wgrad (mlp_wgrad_kernel) grouped split-K TN GEMM for dW1|db1, dW2|db2,
-//           dW3|db3 (bias = virtual all-ones column); the u8 input is
-//           re-read, normalised and transposed on the fly through LDS with
-//           ds_read_b64_tr_b16.  Deterministic fp32 slabs, no atomics.
+//   K_rows  (mlp_rows_kernel)  one workgroup per 64 batch rows, 2 workgroups
+//           per CU (67.5 KB LDS): L1 -> ReLU -> L2 -> ReLU -> L3 -> softmax-CE
+//           -> dZ -> dH2 -> dH1, all row-local.  The u8 input streams through
+//           a 2-slot LDS ring in 64-wide K chunks (normalised to bf16 on the
+//           way in, two chunks of register prefetch); weights are stored in
+//           MFMA-fragment order (each wave-load is one contiguous 1 KB block)
+//           and stream from L2 through a 4-deep per-wave register ring; ReLU
+//           masks stay as bits in registers.  Every operand the weight
+//           gradient needs (normalised X, H1, H2, dZ, dH2, dH1) is written
+//           row-major with coalesced 16-B stores.
+//   K_wgrad (mlp_wgrad_kernel) grouped split-K GEMM dW = dH^T . A over the
+//           batch: 128x128 tiles; both operands stream global -> LDS by
+//           LDS-DMA (global_load_lds_dwordx4, no VGPR staging) into a 4-slot
+//           ring of XOR-swizzled [64 batch rows][128] images (three stages in
+//           flight, counted vmcnt + raw s_barrier), read transposed with
+//           ds_read_b64_tr_b16; bias gradients come from an extra MFMA
+//           against a ones fragment.  Deterministic fp32 slabs.
 //   K_sgd   (mlp_sgd_kernel)   slab reduction (+ optional all-reduce
 //           hand-off) + momentum SGD on fp32 master weights, refreshing the
 //           bf16 shadow weights (and the transposed copies the backward
@@ -25,20 +32,19 @@ using namespace sl;
 
 namespace {
 constexpr int D_IN = 784;   // input features (28x28)
-constexpr int D_INP = 800;  // K padded to a multiple of 32
+constexpr int D_INP = 832;  // layer-1 K padded to 13 chunks of 64 (w1h row stride)
+constexpr int NCHUNK = D_INP / 64;
 constexpr int HID = 256;
 constexpr int NC = 10;
-constexpr int BM = 64;      // batch rows per workgroup
-constexpr int XS_LD = 808;  // LDS row strides (elements), chosen conflict-free for ds_read_b128
-constexpr int HS_LD = 264;
+constexpr int DZ_COLS = 16;  // dZ row stride in global memory
+constexpr int BM = 64;       // batch rows per workgroup
+constexpr int HS_LD = 264;   // [64][256] bf16 LDS images: 528-B rows
+constexpr int XC_LD = 72;    // X chunk image rows: 64 k + 8 pad = 144 B (ds_read_b128 conflict-free)
 constexpr int DZ_LD = 40;
-constexpr int OFF_XS = 0;
-constexpr int OFF_H1S = BM * XS_LD;             // elements
-constexpr int OFF_H2S = 0;                      // reuses the X image after layer 1
-constexpr int OFF_DZS = BM * HS_LD;
-constexpr int OFF_DHS = OFF_DZS + BM * DZ_LD;
-constexpr int SMEM_ELEMS = OFF_H1S + BM * HS_LD;  // 68608 elements = 137216 B
-static_assert(OFF_DHS + BM * HS_LD <= OFF_H1S, "LDS overlay overflow");
+constexpr int REG = BM * HS_LD;  // one LDS region (elements) = 33,792 B
+static_assert(2 * BM * XC_LD <= REG, "X ring must fit region 0");
+constexpr int XN_LD = 896;       // normalised-X row stride (7 column tiles of 128 for K_wgrad)
+constexpr int KS1 = D_INP / 32, KS2 = HID / 32;  // 32-deep k-steps of layer 1 / of 256-wide layers
 
 // Flat parameter layout (torch nn.Linear order): W1 b1 W2 b2 W3 b3.
 constexpr long P_W1 = 0;
@@ -50,6 +56,16 @@ constexpr long P_B3 = P_W3 + (long)NC * HID;
 constexpr long P_N = P_B3 + NC;  // 269322
 }  // namespace
 
+// Weights are kept in MFMA B-fragment order: for a [N][K] matrix (K
+// contiguous), block (nt, ks) holds W[16 nt + r][32 ks + 8 g + j] at lane
+// l = 16 g + r, element j -- one wave's fragment is 1 KB of contiguous memory.
+__host__ __device__ constexpr long frag_off(int n, int k, int ks_per_row) {
+  return ((long)(n >> 4) * ks_per_row + (k >> 5)) * 512 + ((((k & 31) >> 3) << 4) | (n & 15)) * 8 + (k & 7);
+}
+__device__ __forceinline__ short8_t ld_frag(const uint16_t* w, int nt, int ks, int ks_per_row, int lane) {
+  return ld8(w + ((long)nt * ks_per_row + ks) * 512 + lane * 8);
+}
+
 struct MlpRowArgs {
   const uint8_t* x;
   const uint8_t* y;
@@ -58,16 +74,16 @@ struct MlpRowArgs {
   const uint16_t *w1h, *w2h, *w3h, *w2th, *w3th;
   const float *b1, *b2, *b3;
   float xa, xb, grad_scale;
-  uint16_t *h1t, *h2t, *dzt, *dh2t, *dh1t;
+  uint16_t *h1, *h2, *dz, *dh2, *dh1;  // row-major [batch][256] ([batch][16] for dz)
+  uint16_t* xn;                         // normalised X, row-major [batch][XN_LD]
   float *loss, *correct, *logits;
 };
 
 // Fully unrolled K loop with a 4-deep register ring for the per-wave B
-// operand (weights, streamed from L2): the load for step s+4 is issued right
-// after step s's MFMAs, so ~4 x 16 MFMAs (~1000 cycles) cover the L2 latency
-// even at one wave per SIMD (the row kernel is LDS-limited to 1 WG per CU).
-template <int NSTEPS, class LoadB, class Step>
-__device__ __forceinline__ void kloop_ring4(LoadB&& loadb, Step&& step) {
+// operand (weights, streamed from L2).  `after(s)` runs after step s's MFMAs
+// and its ring refill (chunk hand-offs / barriers of the A operand ring).
+template <int NSTEPS, class LoadB, class Step, class After>
+__device__ __forceinline__ void kloop_ring4(LoadB&& loadb, Step&& step, After&& after) {
   short8_t r0[4], r1[4], r2[4], r3[4];
   loadb(r0, 0);
   if (NSTEPS > 1) loadb(r1, 1);
@@ -77,17 +93,21 @@ __device__ __forceinline__ void kloop_ring4(LoadB&& loadb, Step&& step) {
   for (int s = 0; s < NSTEPS; s += 4) {
     step(s, r0);
     if (s + 4 < NSTEPS) loadb(r0, s + 4);
+    after(s);
     if (s + 1 < NSTEPS) {
       step(s + 1, r1);
       if (s + 5 < NSTEPS) loadb(r1, s + 5);
+      after(s + 1);
     }
     if (s + 2 < NSTEPS) {
       step(s + 2, r2);
       if (s + 6 < NSTEPS) loadb(r2, s + 6);
+      after(s + 2);
     }
     if (s + 3 < NSTEPS) {
       step(s + 3, r3);
       if (s + 7 < NSTEPS) loadb(r3, s + 7);
+      after(s + 3);
     }
   }
 }
@@ -97,71 +117,85 @@ __device__ __forceinline__ long batch_base(const int* cursor, int n_batches, int
   return b * batch;
 }
 
-// Store the 4 consecutive-row values a lane holds for one column into a
-// [feature][batch] transposed activation (8 bytes, rows 4g..4g+3).
-__device__ __forceinline__ void st_t4(uint16_t* t, int col, int ldb, int row, float v0, float v1, float v2, float v3) {
-  uint2 pk;
-  pk.x = pack2(v0, v1);
-  pk.y = pack2(v2, v3);
-  *reinterpret_cast<uint2*>(t + (long)col * ldb + row) = pk;
+// Copy a [64][ncols] bf16 LDS image (row stride ld) to global rows (stride gld): 16-B stores.
+template <int NCOLS>
+__device__ __forceinline__ void copy_out(const uint16_t* src, int ld, uint16_t* dst, int gld, int tid) {
+  constexpr int CPR = NCOLS / 8;
+#pragma unroll
+  for (int q = tid; q < BM * CPR; q += 256) {
+    const int r = q / CPR, c = (q - r * CPR) * 8;
+    *reinterpret_cast<short8_t*>(dst + (long)r * gld + c) = *reinterpret_cast<const short8_t*>(src + r * ld + c);
+  }
 }
 
 template <bool TRAIN>
-__global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_ELEMS];
-  uint16_t* XS = smem + OFF_XS;
-  uint16_t* H1S = smem + OFF_H1S;
-  uint16_t* H2S = smem + OFF_H2S;
-  uint16_t* DZS = smem + OFF_DZS;
-  uint16_t* DHS = smem + OFF_DHS;
+__global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * REG];
+  uint16_t* R0 = smem;        // X ring -> H2 image -> dH2 image
+  uint16_t* R1 = smem + REG;  // H1 image -> dZ image -> dH1 image
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int row0 = blockIdx.x * BM;
   const long srow0 = batch_base(a.cursor, a.n_batches, a.batch) + row0;
-  const int B = a.batch;
-
-  // ---- stage + normalise the 64x784 u8 tile into LDS as bf16 (16-B loads) ----
-  {
-    const uint8_t* xg = a.x + srow0 * D_IN;
-    for (int e = tid; e < BM * 49; e += 256) {
-      const int r = e / 49, c = e - r * 49;
-      const uint4 v = *reinterpret_cast<const uint4*>(xg + (long)r * D_IN + c * 16);
-      uint16_t* d = XS + r * XS_LD + c * 16;
-      *reinterpret_cast<short8_t*>(d) = u8x8_to_bf16(make_uint2(v.x, v.y), a.xa, a.xb);
-      *reinterpret_cast<short8_t*>(d + 8) = u8x8_to_bf16(make_uint2(v.z, v.w), a.xa, a.xb);
-    }
-    if (tid < BM) {
-      *reinterpret_cast<short8_t*>(XS + tid * XS_LD + D_IN) = zero8();
-      *reinterpret_cast<short8_t*>(XS + tid * XS_LD + D_IN + 8) = zero8();
-    }
-  }
-  __syncthreads();
-
   const int cw = wave * 64;  // this wave's 64 output columns
   floatx4_t acc[4][4];
 
-  // ---- layer 1: H1 = relu(X W1^T + b1), K = 800 ----
+  // ---- layer 1: H1 = relu(X W1^T + b1), K = 832 streamed in 13 chunks of 64 ----
+  const int xrow = tid >> 2, xcol = (tid & 3) * 16;
+  const uint8_t* xg = a.x + (srow0 + xrow) * D_IN + xcol;
+  // Normalisation coefficients as lane values (VGPRs): with both in SGPRs,
+  // ROCm 7.2 emits a packed FMA that breaks the gfx950 constant-bus limit.
+  const float nxa = a.xa + 0.f * (float)lane, nxb = a.xb + 0.f * (float)lane;
+  auto xload = [&](int c) -> uint4 {
+    return (c * 64 + xcol < D_IN) ? *reinterpret_cast<const uint4*>(xg + c * 64) : make_uint4(0, 0, 0, 0);
+  };
+  auto xstore = [&](int c, uint4 v) {
+    uint16_t* d = R0 + (c & 1) * BM * XC_LD + xrow * XC_LD + xcol;
+    short8_t lo = zero8(), hi = zero8();
+    if (c * 64 + xcol < D_IN) {
+      lo = u8x8_to_bf16(make_uint2(v.x, v.y), nxa, nxb);
+      hi = u8x8_to_bf16(make_uint2(v.z, v.w), nxa, nxb);
+    }
+    *reinterpret_cast<short8_t*>(d) = lo;
+    *reinterpret_cast<short8_t*>(d + 8) = hi;
+    if (TRAIN) {  // the weight gradient's B operand for dW1
+      uint16_t* g = a.xn + (long)(row0 + xrow) * XN_LD + c * 64 + xcol;
+      *reinterpret_cast<short8_t*>(g) = lo;
+      *reinterpret_cast<short8_t*>(g + 8) = hi;
+    }
+  };
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
   {
-    const uint16_t* wb = a.w1h + (long)(cw + lr) * D_INP + 8 * lg;
-    const uint16_t* xa_ = XS + lr * XS_LD + 8 * lg;
-    kloop_ring4<D_INP / 32>(
+    uint4 xn1 = xload(1), xn2 = xload(2);
+    xstore(0, xload(0));
+    __syncthreads();
+    kloop_ring4<KS1>(
         [&](short8_t (&r)[4], int st) {
 #pragma unroll
-          for (int n = 0; n < 4; ++n) r[n] = ld8(wb + n * 16 * D_INP + st * 32);
+          for (int n = 0; n < 4; ++n) r[n] = ld_frag(a.w1h, 4 * wave + n, st, KS1, lane);
         },
         [&](int st, short8_t (&b)[4]) {
+          const uint16_t* xa_ = R0 + ((st >> 1) & 1) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg;
           short8_t af[4];
 #pragma unroll
-          for (int m = 0; m < 4; ++m) af[m] = lds8(xa_ + m * 16 * XS_LD + st * 32);
+          for (int m = 0; m < 4; ++m) af[m] = lds8(xa_ + m * 16 * XC_LD);
 #pragma unroll
           for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
+        },
+        [&](int st) {
+          if (st & 1) {  // end of chunk c: publish chunk c+1, prefetch chunk c+3
+            const int c = st >> 1;
+            if (c + 1 < NCHUNK) xstore(c + 1, xn1);
+            xn1 = xn2;
+            if (c + 3 < NCHUNK) xn2 = xload(c + 3);
+            __syncthreads();
+          }
         });
   }
   uint64_t mask1 = 0;
@@ -170,33 +204,29 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
     const int col = cw + n * 16 + lr;
     const float bias = a.b1[col];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float v[4];
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float h = acc[m][n][r] + bias;
         const bool pos = h > 0.f;
-        v[r] = pos ? h : 0.f;
         mask1 |= (uint64_t)pos << (m * 16 + n * 4 + r);
-        H1S[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(v[r]);
+        R1[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(pos ? h : 0.f);
       }
-      if (TRAIN) st_t4(a.h1t, col, B, row0 + m * 16 + 4 * lg, v[0], v[1], v[2], v[3]);
-    }
   }
   __syncthreads();
+  if (TRAIN) copy_out<HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid);
 
-  // ---- layer 2: H2 = relu(H1 W2^T + b2), K = 256 ----
+  // ---- layer 2: H2 = relu(H1 W2^T + b2), K = 256; A = R1, out -> R0 ----
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
   {
-    const uint16_t* wb = a.w2h + (long)(cw + lr) * HID + 8 * lg;
-    const uint16_t* ha = H1S + lr * HS_LD + 8 * lg;
-    kloop_ring4<HID / 32>(
+    const uint16_t* ha = R1 + lr * HS_LD + 8 * lg;
+    kloop_ring4<KS2>(
         [&](short8_t (&r)[4], int st) {
 #pragma unroll
-          for (int n = 0; n < 4; ++n) r[n] = ld8(wb + n * 16 * HID + st * 32);
+          for (int n = 0; n < 4; ++n) r[n] = ld_frag(a.w2h, 4 * wave + n, st, KS2, lane);
         },
         [&](int st, short8_t (&b)[4]) {
           short8_t af[4];
@@ -206,7 +236,8 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
           for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
-        });
+        },
+        [](int) {});
   }
   uint64_t mask2 = 0;
 #pragma unroll
@@ -214,31 +245,26 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
     const int col = cw + n * 16 + lr;
     const float bias = a.b2[col];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float v[4];
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float h = acc[m][n][r] + bias;
         const bool pos = h > 0.f;
-        v[r] = pos ? h : 0.f;
         mask2 |= (uint64_t)pos << (m * 16 + n * 4 + r);
-        H2S[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(v[r]);
+        R0[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(pos ? h : 0.f);
       }
-      if (TRAIN) st_t4(a.h2t, col, B, row0 + m * 16 + 4 * lg, v[0], v[1], v[2], v[3]);
-    }
   }
   __syncthreads();
+  if (TRAIN) copy_out<HID>(R0, HS_LD, a.h2 + (long)row0 * HID, HID, tid);
 
-  // ---- layer 3 + softmax cross-entropy: wave w owns rows 16w..16w+15 ----
+  // ---- layer 3 + softmax cross-entropy: wave w owns rows 16w..16w+15; dZ -> R1 ----
   {
     floatx4_t z = zero4();
-    const uint16_t* w3b = a.w3h + lr * HID + 8 * lg;
-    const uint16_t* ha = H2S + (wave * 16 + lr) * HS_LD + 8 * lg;
+    const uint16_t* ha = R0 + (wave * 16 + lr) * HS_LD + 8 * lg;
 #pragma unroll
-    for (int k0 = 0; k0 < HID; k0 += 32) z = mfma16(lds8(ha + k0), ld8(w3b + k0), z);
+    for (int ks = 0; ks < KS2; ++ks) z = mfma16(lds8(ha + ks * 32), ld_frag(a.w3h, 0, ks, KS2, lane), z);
     const int c = lr;
     const float bias3 = c < NC ? a.b3[c] : 0.f;
-    float dzv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = wave * 16 + 4 * lg + r;
@@ -268,18 +294,18 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
         if (a.correct) a.correct[row0 + row] = (idx == lab) ? 1.f : 0.f;
       }
       if (a.logits && c < NC) a.logits[(long)(row0 + row) * NC + c] = zz;
-      dzv[r] = c < NC ? (e / s - (c == lab ? 1.f : 0.f)) * a.grad_scale : 0.f;
       if (TRAIN) {
-        DZS[row * DZ_LD + c] = f2bf(dzv[r]);
-        DZS[row * DZ_LD + 16 + c] = 0;
+        const float dzv = c < NC ? (e / s - (c == lab ? 1.f : 0.f)) * a.grad_scale : 0.f;
+        R1[row * DZ_LD + c] = f2bf(dzv);
+        R1[row * DZ_LD + 16 + c] = 0;
       }
     }
-    if (TRAIN) st_t4(a.dzt, c, B, row0 + wave * 16 + 4 * lg, dzv[0], dzv[1], dzv[2], dzv[3]);
   }
   if (!TRAIN) return;
   __syncthreads();
+  copy_out<DZ_COLS>(R1, DZ_LD, a.dz + (long)row0 * DZ_COLS, DZ_COLS, tid);
 
-  // ---- dH2 = (dZ W3) * 1[H2 > 0], K = 32 (10 classes, zero padded) ----
+  // ---- dH2 = (dZ W3) * 1[H2 > 0], K = 32 (10 classes, zero padded); out -> R0 ----
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -287,9 +313,9 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
   {
     short8_t bf[4], af[4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) bf[n] = ld8(a.w3th + (cw + n * 16 + lr) * 32 + 8 * lg);
+    for (int n = 0; n < 4; ++n) bf[n] = ld_frag(a.w3th, 4 * wave + n, 0, 1, lane);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) af[m] = lds8(DZS + (m * 16 + lr) * DZ_LD + 8 * lg);
+    for (int m = 0; m < 4; ++m) af[m] = lds8(R1 + (m * 16 + lr) * DZ_LD + 8 * lg);
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -299,30 +325,26 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
   for (int n = 0; n < 4; ++n) {
     const int col = cw + n * 16 + lr;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float v[4];
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = ((mask2 >> (m * 16 + n * 4 + r)) & 1) ? acc[m][n][r] : 0.f;
-        DHS[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(v[r]);
-      }
-      st_t4(a.dh2t, col, B, row0 + m * 16 + 4 * lg, v[0], v[1], v[2], v[3]);
-    }
+      for (int r = 0; r < 4; ++r)
+        R0[(m * 16 + 4 * lg + r) * HS_LD + col] =
+            f2bf(((mask2 >> (m * 16 + n * 4 + r)) & 1) ? acc[m][n][r] : 0.f);
   }
   __syncthreads();
+  copy_out<HID>(R0, HS_LD, a.dh2 + (long)row0 * HID, HID, tid);
 
-  // ---- dH1 = (dH2 W2) * 1[H1 > 0], K = 256 ----
+  // ---- dH1 = (dH2 W2) * 1[H1 > 0], K = 256; A = R0, out -> R1 ----
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
   {
-    const uint16_t* wb = a.w2th + (long)(cw + lr) * HID + 8 * lg;
-    const uint16_t* ha = DHS + lr * HS_LD + 8 * lg;
-    kloop_ring4<HID / 32>(
+    const uint16_t* ha = R0 + lr * HS_LD + 8 * lg;
+    kloop_ring4<KS2>(
         [&](short8_t (&r)[4], int st) {
 #pragma unroll
-          for (int n = 0; n < 4; ++n) r[n] = ld8(wb + n * 16 * HID + st * 32);
+          for (int n = 0; n < 4; ++n) r[n] = ld_frag(a.w2th, 4 * wave + n, st, KS2, lane);
         },
         [&](int st, short8_t (&b)[4]) {
           short8_t af[4];
@@ -332,195 +354,205 @@ __global__ __launch_bounds__(256) void mlp_rows_kernel(MlpRowArgs a) {
           for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
-        });
+        },
+        [](int) {});
   }
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
     const int col = cw + n * 16 + lr;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float v[4];
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = ((mask1 >> (m * 16 + n * 4 + r)) & 1) ? acc[m][n][r] : 0.f;
-      st_t4(a.dh1t, col, B, row0 + m * 16 + 4 * lg, v[0], v[1], v[2], v[3]);
-    }
+      for (int r = 0; r < 4; ++r)
+        R1[(m * 16 + 4 * lg + r) * HS_LD + col] =
+            f2bf(((mask1 >> (m * 16 + n * 4 + r)) & 1) ? acc[m][n][r] : 0.f);
   }
+  __syncthreads();
+  copy_out<HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid);
 }
 
 // ---------------------------------------------------------------------------
-// Weight-gradient grouped split-K GEMM:  G[m][n] = sum_b At[m][b] * Bop[b][n]
+// Weight-gradient grouped split-K GEMM:  G[m][n] = sum_b A[b][m] * Bop[b][n]
+// (+ db[m] = sum_b A[b][m]), A and Bop row-major over the batch index b.
 //
-// Workgroup tile 64 (m) x 128 (n), 4 waves of 32 x 64 (2 x 4 MFMA tiles), one
-// K slice of the batch per workgroup.  Grid order is slice-major after the
-// XCD remap, so every tile of one slice -- which all read the same batch
-// columns of dH1/dH2/dZ and the same input rows -- runs on one XCD and shares
-// its L2.  Operands stream through a 2-deep register ring (global) and, for
-// the u8 input, a double-buffered LDS tile read back transposed with
-// ds_read_b64_tr_b16.
+// Workgroup tile 128 (m) x 128 (n), 4 waves of 64 x 64.  One K slice of the
+// batch per workgroup; grid order is slice-major after the XCD remap, so all
+// tiles of one slice -- which read the same batch rows -- share an L2.
 // ---------------------------------------------------------------------------
 struct WgProblem {
-  const uint16_t* at;  // [m_real][ldk] bf16, batch-contiguous
-  const uint16_t* bt;  // mode 0: [n_real][ldk] bf16, batch-contiguous
-  int mode;            // 0: bf16 operand, 1: u8 input rows normalised on the fly
-  int m_real, n_real;  // column n_real is the virtual all-ones column (bias grad)
+  const uint16_t* a;  // [batch][lda] bf16: dH1 / dH2 / dZ
+  int lda;
+  const uint16_t* b;  // [batch][ldb] bf16: normalised X / H1 / H2
+  int ldb;
+  int m_real, n_real;
   int tiles_m, tiles_n, tile_base;
-  long w_off, b_off;   // flat destinations of dW and db
+  long w_off, b_off;  // flat destinations of dW ([m_real][n_real]) and db
 };
 struct WgArgs {
   WgProblem p[3];
   int total_tiles;
-  int slices, k_slice, ldk;
-  const uint8_t* x;
-  const int* cursor;
-  int n_batches;
-  float xa, xb;
+  int steps_per_slice, total_steps;  // 64-row stages
   float* slab;
   long slab_stride;
 };
 
-constexpr int WG_TN = 128;
-constexpr int XT_LD = WG_TN + 8;  // [32 k][128 n] bf16 X tile; 272-B rows (8-B aligned tr reads)
+constexpr int WG_NSLOT = 4;               // LDS ring slots; three stages in flight
+constexpr int WG_IMG = 64 * 128;          // one [64 k][128] bf16 image, unpadded (swizzled)
+constexpr int WG_SLOT = 2 * WG_IMG;       // A image + B image = 32 KB
+constexpr int WG_OUT_LD = 128 + 4;        // fp32 epilogue tile
+static_assert(128 * WG_OUT_LD * 2 <= WG_NSLOT * WG_SLOT, "epilogue tile must fit the ring");
 
-__global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t xs[2][32 * XT_LD];
+// 16-B chunk position inside a 256-B image row.  XOR on chunk-pair bits with
+// f(r) = (r & 3) | ((r >> 3) & 1) << 2 makes every ds_read_b64_tr_b16 of the
+// transposed fragment read (rows k..k+3 and k+8..k+11 per 32-lane half)
+// conflict-free; LDS-DMA writes the image linearly, so the same involution is
+// applied to the per-lane SOURCE address (cdna_hip_programming.md rule 21).
+__device__ __forceinline__ int wg_swz(int c, int r) { return c ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
+
+// Transposed B-style fragment (8 consecutive k rows of one column) from a
+// swizzled image.  Issued as inline asm on purpose: hipcc treats a visible
+// ds_read as possibly aliasing the in-flight LDS-DMA and drains vmcnt to 0 in
+// front of it, which would serialise the ring; the caller waits lgkmcnt
+// itself and fences the MFMAs with sched_barrier (cdna_hip_programming.md
+// rules 18 and "Three .s-level traps" (b)).
+__device__ __forceinline__ short4_t ds_tr16_asm(const uint16_t* p) {
+  short4_t r;
+  const uint32_t a = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+__device__ __forceinline__ short8_t wg_tr8(const uint16_t* img, int k0, int n0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int c = (n0 >> 3) + (p >> 1), w = (p & 1) * 4;
+  const int ra = k0 + 8 * g + q, rb = ra + 4;
+  const short4_t lo = ds_tr16_asm(img + ra * 128 + wg_swz(c, ra) * 8 + w);
+  const short4_t hi = ds_tr16_asm(img + rb * 128 + wg_swz(c, rb) * 8 + w);
+  short8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__device__ __forceinline__ void wg_vmcnt(int n) {
+  // vmcnt needs an immediate; LDS-DMA pieces per wave per stage = 8
+  if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WG_NSLOT * WG_SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int s = logical / a.total_tiles;
-  const int t = logical - s * a.total_tiles;
-  const int pi = t >= a.p[2].tile_base ? 2 : (t >= a.p[1].tile_base ? 1 : 0);
-  const WgProblem& P = a.p[pi];
+  const int s = logical / A.total_tiles;
+  const int t = logical - s * A.total_tiles;
+  const int pi = t >= A.p[2].tile_base ? 2 : (t >= A.p[1].tile_base ? 1 : 0);
+  const WgProblem& P = A.p[pi];
   const int lt = t - P.tile_base;
   const int tm = lt / P.tiles_n, tn = lt - tm * P.tiles_n;
+  const int m0 = tm * 128, n0 = tn * 128;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = tm * 64 + wm * 32, n0 = tn * WG_TN + wn * 64;
-  const int kb = s * a.k_slice;
-  const int nsteps = a.k_slice / 32;  // even (host guarantees k_slice % 64 == 0)
+  const int st0 = s * A.steps_per_slice;
+  const int nst = min(A.steps_per_slice, A.total_steps - st0);
+  const bool do_bias = tn == 0 && wn == 0;
+  const bool m_live = m0 + wm * 64 < P.m_real;  // wave-uniform: skip MFMAs on all-padding rows
 
-  floatx4_t acc[2][4];
+  // LDS-DMA map: wave w, piece j (0..3) covers image rows 4 (4w + j) .. +3;
+  // lane -> row 4 (4w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row).
+  const int prow = lane >> 4;
+  const uint16_t* asrc[4];
+  const uint16_t* bsrc[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < 4; ++j) {
+    const int row = 4 * (4 * wave + j) + prow;
+    const int c = wg_swz(lane & 15, row);
+    const int acol = min(m0 + c * 8, P.lda - 8);  // columns past dZ's 16 are don't-care rows of dW3
+    asrc[j] = P.a + (long)(st0 * 64 + row) * P.lda + acol;
+    bsrc[j] = P.b + (long)(st0 * 64 + row) * P.ldb + n0 + c * 8;
+  }
+  auto issue = [&](int st) {  // stage st (relative to the slice) -> ring slot st % 4
+    uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
+    uint16_t* Bi = Ai + WG_IMG;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int rbase = 4 * (4 * wave + j) * 128;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(asrc[j] + (long)st * 64 * P.lda),
+                                       (SL_LDS void*)(Ai + rbase), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[j] + (long)st * 64 * P.ldb),
+                                       (SL_LDS void*)(Bi + rbase), 16, 0, 0);
+    }
+  };
+
+  floatx4_t acc[4][4], accb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    accb[i] = zero4();
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
-
-  const uint16_t* ap[2];
-  bool av[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = m0 + i * 16 + lr;
-    av[i] = row < P.m_real;
-    ap[i] = P.at + (long)(av[i] ? row : 0) * a.ldk + kb + 8 * lg;
   }
-  auto load_a = [&](short8_t (&r)[2], int ks) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) r[i] = av[i] ? ld8(ap[i] + ks * 32) : zero8();
-  };
-  auto mma = [&](const short8_t (&af)[2], const short8_t (&bf)[4]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-  };
-
   short8_t ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
 
-  if (P.mode == 0) {
-    const uint16_t* bp[4];
-    int bk[4];  // 0 = load, 1 = ones, 2 = zero
+  for (int st = 0; st < 3 && st < nst; ++st) issue(st);
+  for (int st = 0; st < nst; ++st) {
+    wg_vmcnt(8 * min(2, nst - 1 - st));  // this wave's pieces of stage st have landed
+    __builtin_amdgcn_s_barrier();        // ... everyone's have; slot (st+3)%4 is free
+    if (st + 3 < nst) issue(st + 3);
+    if (m_live) {
+      const uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
+      const uint16_t* Bi = Ai + WG_IMG;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + j * 16 + lr;
-      bk[j] = n < P.n_real ? 0 : (n == P.n_real ? 1 : 2);
-      bp[j] = P.bt + (long)(n < P.n_real ? n : 0) * a.ldk + kb + 8 * lg;
-    }
-    auto load_b = [&](short8_t (&r)[4], int ks) {
+      for (int ks = 0; ks < 64; ks += 32) {
+        short8_t af[4], bf[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = bk[j] == 0 ? ld8(bp[j] + ks * 32) : (bk[j] == 1 ? ones : zero8());
-    };
-    short8_t a0[2], a1[2], b0[4], b1[4];
-    load_a(a0, 0);
-    load_b(b0, 0);
-    load_a(a1, 1);
-    load_b(b1, 1);
-    for (int ks = 0; ks < nsteps; ks += 2) {
-      mma(a0, b0);
-      if (ks + 2 < nsteps) { load_a(a0, ks + 2); load_b(b0, ks + 2); }
-      mma(a1, b1);
-      if (ks + 3 < nsteps) { load_a(a1, ks + 3); load_b(b1, ks + 3); }
-    }
-  } else {
-    // u8 input rows: 32 batch rows x 128 features per stage (16 B per thread)
-    const long xrow0 = batch_base(a.cursor, a.n_batches, a.ldk) + kb;
-    const int sr = tid >> 3, sc = (tid & 7) * 16;
-    const int col = tn * WG_TN + sc;
-    auto load_x = [&](int ks) -> uint4 {
-      if (col < D_IN) return *reinterpret_cast<const uint4*>(a.x + (xrow0 + ks * 32 + sr) * D_IN + col);
-      return make_uint4(0, 0, 0, 0);
-    };
-    auto store_x = [&](uint16_t* dst, uint4 v) {
-      short8_t lo, hi;
-      if (col < D_IN) {
-        lo = u8x8_to_bf16(make_uint2(v.x, v.y), a.xa, a.xb);
-        hi = u8x8_to_bf16(make_uint2(v.z, v.w), a.xa, a.xb);
-      } else {
+        for (int i = 0; i < 4; ++i) af[i] = wg_tr8(Ai, ks, wm * 64 + i * 16, lane);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          lo[j] = (col + j == D_IN) ? (short)0x3f80 : (short)0;
-          hi[j] = (col + 8 + j == D_IN) ? (short)0x3f80 : (short)0;
+        for (int j = 0; j < 4; ++j) bf[j] = wg_tr8(Bi, ks, wn * 64 + j * 16, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+        if (do_bias) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) accb[i] = mfma16(af[i], ones, accb[i]);
         }
       }
-      *reinterpret_cast<short8_t*>(dst + sr * XT_LD + sc) = lo;
-      *reinterpret_cast<short8_t*>(dst + sr * XT_LD + sc + 8) = hi;
-    };
-    uint4 x0 = load_x(0);
-    uint4 x1 = nsteps > 1 ? load_x(1) : x0;
-    store_x(xs[0], x0);
-    short8_t a0[2], a1[2];
-    load_a(a0, 0);
-    load_a(a1, 1);
-    __syncthreads();
-    for (int ks = 0; ks < nsteps; ks += 2) {
-      // even step: compute from xs[0] while x1 (step ks+1) waits in registers
-      if (ks + 2 < nsteps) x0 = load_x(ks + 2);
-      {
-        short8_t bf[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = lds_tr8(xs[0] + wn * 64 + j * 16, XT_LD, lane);
-        mma(a0, bf);
-      }
-      if (ks + 2 < nsteps) load_a(a0, ks + 2);
-      store_x(xs[1], x1);
-      __syncthreads();
-      // odd step: compute from xs[1]
-      if (ks + 3 < nsteps) x1 = load_x(ks + 3);
-      {
-        short8_t bf[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = lds_tr8(xs[1] + wn * 64 + j * 16, XT_LD, lane);
-        mma(a1, bf);
-      }
-      if (ks + 3 < nsteps) load_a(a1, ks + 3);
-      if (ks + 2 < nsteps) store_x(xs[0], x0);
-      __syncthreads();
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-  float* out = a.slab + (long)s * a.slab_stride;
+  // ---- epilogue: fp32 tile through LDS -> 16-B row stores into the slab ----
+  float* Os = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + j * 16 + lr;
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Os[(wm * 64 + i * 16 + 4 * lg + r) * WG_OUT_LD + wn * 64 + j * 16 + lr] = acc[i][j][r];
+  float* out = A.slab + (long)s * A.slab_stride;
+  if (do_bias && lr == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + i * 16 + 4 * lg + r;
-        if (m >= P.m_real) continue;
-        if (n < P.n_real) out[P.w_off + (long)m * P.n_real + n] = acc[i][j][r];
-        else if (n == P.n_real) out[P.b_off + m] = acc[i][j][r];
+        const int m = m0 + wm * 64 + i * 16 + 4 * lg + r;
+        if (m < P.m_real) out[P.b_off + m] = accb[i][r];
       }
-    }
+  }
+  __syncthreads();
+  for (int q = tid; q < 128 * 32; q += 256) {
+    const int rl = q >> 5, c4 = (q & 31) * 4;
+    const int m = m0 + rl, n = n0 + c4;
+    if (m < P.m_real && n < P.n_real)
+      *reinterpret_cast<float4*>(out + P.w_off + (long)m * P.n_real + n) =
+          *reinterpret_cast<const float4*>(Os + rl * WG_OUT_LD + c4);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -544,16 +576,16 @@ struct SgdArgs {
 __device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) {
   const uint16_t h = f2bf(w);
   if (p < P_B1) {
-    const long o = p / D_IN, i = p - o * D_IN;
-    a.w1h[o * D_INP + i] = h;
+    const int o = (int)(p / D_IN), i = (int)(p - (long)o * D_IN);
+    a.w1h[frag_off(o, i, KS1)] = h;                     // layer 1: B[k=i][n=o]
   } else if (p >= P_W2 && p < P_B2) {
-    const long q = p - P_W2, o = q >> 8, i = q & 255;
-    a.w2h[q] = h;
-    a.w2th[i * HID + o] = h;
+    const int q = (int)(p - P_W2), o = q >> 8, i = q & 255;
+    a.w2h[frag_off(o, i, KS2)] = h;                     // layer 2: B[k=i][n=o]
+    a.w2th[frag_off(i, o, KS2)] = h;                    // dH1 = dH2 W2: B[k=o][n=i]
   } else if (p >= P_W3 && p < P_B3) {
-    const long q = p - P_W3, c = q >> 8, i = q & 255;
-    a.w3h[q] = h;
-    a.w3th[i * 32 + c] = h;
+    const int q = (int)(p - P_W3), c = q >> 8, i = q & 255;
+    a.w3h[frag_off(c, i, KS2)] = h;                     // layer 3: B[k=i][n=c]
+    a.w3th[frag_off(i, c, 1)] = h;                      // dH2 = dZ W3: B[k=c][n=i]
   }
 }
 
@@ -569,14 +601,23 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
   const bool full = p0 + 4 <= a.n;
   float g[4] = {0.f, 0.f, 0.f, 0.f};
   if (a.slab) {
-    for (int s = 0; s < a.slices; ++s) {
-      const float* src = a.slab + (long)s * a.slab_stride + p0;
-      if (full) {
-        const float4 v = *reinterpret_cast<const float4*>(src);
-        g[0] += v.x; g[1] += v.y; g[2] += v.z; g[3] += v.w;
-      } else {
-        for (int j = 0; p0 + j < a.n; ++j) g[j] += src[j];
+    if (full) {
+      const float* src = a.slab + p0;
+      int sidx = 0;
+      for (; sidx + 4 <= a.slices; sidx += 4) {  // 4 independent 16-B loads in flight per thread
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(src + (long)(sidx + u) * a.slab_stride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { g[0] += v[u].x; g[1] += v[u].y; g[2] += v[u].z; g[3] += v[u].w; }
       }
+      for (; sidx < a.slices; ++sidx) {
+        const float4 v = *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride);
+        g[0] += v.x; g[1] += v.y; g[2] += v.z; g[3] += v.w;
+      }
+    } else {
+      for (int sidx = 0; sidx < a.slices; ++sidx)
+        for (int j = 0; p0 + j < a.n; ++j) g[j] += a.slab[(long)sidx * a.slab_stride + p0 + j];
     }
   } else {
     for (int j = 0; j < 4 && p0 + j < a.n; ++j) g[j] = a.grad_in[p0 + j];
@@ -605,22 +646,23 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
 extern "C" {
 
 long sl_mlp_param_count() { return P_N; }
+int sl_mlp_xn_stride() { return XN_LD; }
 
 int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_batches, int batch,
                 const uint16_t* w1h, const uint16_t* w2h, const uint16_t* w3h, const uint16_t* w2th,
                 const uint16_t* w3th, const float* params, float xa, float xb, float grad_scale,
-                uint16_t* h1t, uint16_t* h2t, uint16_t* dzt, uint16_t* dh2t, uint16_t* dh1t, float* loss,
-                float* correct, float* logits, int train, hipStream_t stream) {
+                uint16_t* h1, uint16_t* h2, uint16_t* dz, uint16_t* dh2, uint16_t* dh1, uint16_t* xn,
+                float* loss, float* correct, float* logits, int train, hipStream_t stream) {
   if (batch <= 0 || batch % BM != 0) return -1;
   MlpRowArgs a;
   a.x = x; a.y = y; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
   a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th;
   a.b1 = params + P_B1; a.b2 = params + P_B2; a.b3 = params + P_B3;
   a.xa = xa; a.xb = xb; a.grad_scale = grad_scale;
-  a.h1t = h1t; a.h2t = h2t; a.dzt = dzt; a.dh2t = dh2t; a.dh1t = dh1t;
+  a.h1 = h1; a.h2 = h2; a.dz = dz; a.dh2 = dh2; a.dh1 = dh1; a.xn = xn;
   a.loss = loss; a.correct = correct; a.logits = logits;
   if (train) {
-    if (!h1t || !h2t || !dzt || !dh2t || !dh1t) return -2;
+    if (!h1 || !h2 || !dz || !dh2 || !dh1 || !xn) return -2;
     hipLaunchKernelGGL(mlp_rows_kernel<true>, dim3(batch / BM), dim3(256), 0, stream, a);
   } else {
     hipLaunchKernelGGL(mlp_rows_kernel<false>, dim3(batch / BM), dim3(256), 0, stream, a);
@@ -629,26 +671,37 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   return 0;
 }
 
-int sl_mlp_wgrad(const uint8_t* x, const int* cursor, int n_batches, int batch, float xa, float xb,
-                 const uint16_t* h1t, const uint16_t* h2t, const uint16_t* dzt, const uint16_t* dh2t,
-                 const uint16_t* dh1t, float* slab, int slices, long slab_stride, hipStream_t stream) {
-  if (batch <= 0 || slices <= 0 || batch % (64 * slices) != 0) return -1;
+// Effective slice count for a batch: whole 64-row stages, equal-length
+// slices except the last (the slab array holds this many partial gradients).
+int sl_mlp_wgrad_slices(int batch, int requested) {
+  if (batch <= 0 || batch % 64 != 0) return -1;
+  const int total = batch / 64;
+  int req = requested > 0 ? requested : 12;  // 20 tiles x 12 slices = 240 WGs: one per CU (128 KB LDS each)
+  if (req > total) req = total;
+  const int spp = (total + req - 1) / req;
+  return (total + spp - 1) / spp;
+}
+
+int sl_mlp_wgrad(int batch, const uint16_t* xn, const uint16_t* h1, const uint16_t* h2, const uint16_t* dz,
+                 const uint16_t* dh2, const uint16_t* dh1, float* slab, int slices, long slab_stride,
+                 hipStream_t stream) {
+  const int s_eff = sl_mlp_wgrad_slices(batch, slices);
+  if (s_eff <= 0 || s_eff != slices) return -1;
   WgArgs a;
-  const int tn_in = (D_IN + 1 + WG_TN - 1) / WG_TN, tn_h = (HID + 1 + WG_TN - 1) / WG_TN;
-  // dW1|db1 = dH1^T [256 x B] . [X | 1]  (u8 operand)
-  a.p[0] = WgProblem{dh1t, nullptr, 1, HID, D_IN, HID / 64, tn_in, 0, P_W1, P_B1};
-  // dW2|db2 = dH2^T . [H1 | 1]
-  a.p[1] = WgProblem{dh2t, h1t, 0, HID, HID, HID / 64, tn_h, 0, P_W2, P_B2};
-  // dW3|db3 = dZ^T . [H2 | 1]
-  a.p[2] = WgProblem{dzt, h2t, 0, NC, HID, 1, tn_h, 0, P_W3, P_B3};
+  // dW1, db1 = dH1^T [256 x B] . Xn
+  a.p[0] = WgProblem{dh1, HID, xn, XN_LD, HID, D_IN, HID / 128, (D_IN + 127) / 128, 0, P_W1, P_B1};
+  // dW2, db2 = dH2^T . H1
+  a.p[1] = WgProblem{dh2, HID, h1, HID, HID, HID, HID / 128, HID / 128, 0, P_W2, P_B2};
+  // dW3, db3 = dZ^T . H2
+  a.p[2] = WgProblem{dz, DZ_COLS, h2, HID, NC, HID, 1, HID / 128, 0, P_W3, P_B3};
   int base = 0;
   for (int i = 0; i < 3; ++i) {
     a.p[i].tile_base = base;
     base += a.p[i].tiles_m * a.p[i].tiles_n;
   }
   a.total_tiles = base;
-  a.slices = slices; a.k_slice = batch / slices; a.ldk = batch;
-  a.x = x; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.xa = xa; a.xb = xb;
+  a.total_steps = batch / 64;
+  a.steps_per_slice = (a.total_steps + slices - 1) / slices;
   a.slab = slab; a.slab_stride = slab_stride;
   hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();
@@ -664,6 +717,7 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
   if (mode != 0 && !slab && !grad_in) return -1;
   if (mode == 1 && !grad_out) return -1;
+  if (slab && (slab_stride & 3)) return -1;
   const long groups = (P_N + 3) / 4;
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups + 255) / 256), dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();

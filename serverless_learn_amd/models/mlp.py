@@ -27,7 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 D_IN = 784
-D_IN_PAD = 800
+D_IN_PAD = 832  # w1h row stride: layer-1 K in 13 chunks of 64 (mlp_fused.hip)
 HIDDEN = 256
 CLASSES = 10
 MNIST_MEAN = 0.1307
@@ -214,10 +214,10 @@ class CPUTrainer:
 
 
 def default_slices(batch: int) -> int:
-    s = max(1, min(16, batch // 1024))
-    while s > 1 and batch % (64 * s) != 0:
-        s -= 1
-    return s
+    """Split-K slices of the weight-gradient GEMM (the kernel's own choice: one workgroup per CU)."""
+    from ..ops import _native
+
+    return int(_native.lib().sl_mlp_wgrad_slices(batch, 0))
 
 
 class FusedMLPTrainer:
@@ -243,7 +243,9 @@ class FusedMLPTrainer:
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
         self.world_size = world_size
         self.grad_scale = 1.0 / (batch * world_size)
-        self.slices = slices or default_slices(batch)
+        self.slices = int(_native.lib().sl_mlp_wgrad_slices(batch, slices or 0))
+        if self.slices <= 0:
+            raise ValueError(f"batch {batch} not supported by the weight-gradient kernel")
         self.xa, self.xb = norm_coeffs()
         n = N_PARAMS
         self.n_pad = (n + 3) // 4 * 4
@@ -257,11 +259,14 @@ class FusedMLPTrainer:
         self.w2th = torch.zeros(HIDDEN, HIDDEN, dtype=bf, device=dev)
         self.w3h = torch.zeros(16, HIDDEN, dtype=bf, device=dev)
         self.w3th = torch.zeros(HIDDEN, 32, dtype=bf, device=dev)
-        self.h1t = torch.empty(HIDDEN, batch, dtype=bf, device=dev)
-        self.h2t = torch.empty(HIDDEN, batch, dtype=bf, device=dev)
-        self.dh1t = torch.empty(HIDDEN, batch, dtype=bf, device=dev)
-        self.dh2t = torch.empty(HIDDEN, batch, dtype=bf, device=dev)
-        self.dzt = torch.empty(16, batch, dtype=bf, device=dev)
+        # row-major activations for the weight-gradient kernel ([batch][256], dZ [batch][16])
+        self.h1t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
+        self.h2t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
+        self.dh1t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
+        self.dh2t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
+        self.dzt = torch.empty(batch, 16, dtype=bf, device=dev)
+        # normalised input (bf16) written by the row kernel for dW1; columns >= 784 stay zero
+        self.xn = torch.zeros(batch, int(_native.lib().sl_mlp_xn_stride()), dtype=bf, device=dev)
         self.loss = torch.zeros(batch, dtype=torch.float32, device=dev)
         self.correct = torch.zeros(batch, dtype=torch.float32, device=dev)
         self.slab = torch.empty(self.slices, self.n_pad, dtype=torch.float32, device=dev)
@@ -308,14 +313,13 @@ class FusedMLPTrainer:
         n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, self.grad_scale,
-               n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t),
+               n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t), n.ptr(self.xn),
                n.ptr(self.loss), n.ptr(self.correct), None, 1 if train else 0, n.stream_ptr())
 
     def _wgrad(self):
         n = self._n
-        n.call("sl_mlp_wgrad", n.ptr(self.x), n.ptr(self.cursor), self.n_batches, self.batch, self.xa, self.xb,
-               n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t),
-               n.ptr(self.slab), self.slices, self.n_pad, n.stream_ptr())
+        n.call("sl_mlp_wgrad", self.batch, n.ptr(self.xn), n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt),
+               n.ptr(self.dh2t), n.ptr(self.dh1t), n.ptr(self.slab), self.slices, self.n_pad, n.stream_ptr())
 
     def _sgd(self, mode: int, from_grad: bool, grad_out: bool, bump: bool = True):
         n = self._n
@@ -377,7 +381,7 @@ class FusedMLPTrainer:
         corr = torch.zeros(rows, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None, None,
                n.ptr(loss), n.ptr(corr), None, 0, n.stream_ptr())
         return StepStats(float(loss.mean()), float(corr.mean()), rows)
 
@@ -390,7 +394,7 @@ class FusedMLPTrainer:
         out = torch.empty(rows, CLASSES, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None, None,
                None, None, n.ptr(out), 0, n.stream_ptr())
         return out
 

@@ -30,8 +30,10 @@ F = ctypes.c_float
 # name -> argtypes (restype is always c_int unless listed in _RESTYPE)
 _SIGS: dict[str, list] = {
     "sl_mlp_param_count": [],
-    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, P, P, P, P, P, P, P, P, I, P],
-    "sl_mlp_wgrad": [P, P, I, I, F, F, P, P, P, P, P, P, I, L, P],
+    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, P, P, P, P, P, P, P, P, P, I, P],
+    "sl_mlp_wgrad": [I, P, P, P, P, P, P, P, I, L, P],
+    "sl_mlp_wgrad_slices": [I, I],
+    "sl_mlp_xn_stride": [],
     "sl_mlp_sgd": [P, P, P, I, L, P, P, F, F, F, I, P, P, P, P, P, P, P],
 }
 _RESTYPE = {"sl_mlp_param_count": ctypes.c_long}

@@ -115,7 +115,8 @@ class Worker:
         return self.trainer.params[:self.trainer.n_params]
 
     def _after_external_update(self):
-        self.trainer.refresh_shadows()
+        if self.trainer is not None:
+            self.trainer.refresh_shadows()
 
     def _set_world(self, world: int):
         """Gradient scale follows the group size (mean over the global batch)."""
