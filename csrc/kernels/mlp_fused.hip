@@ -28,6 +28,8 @@
 //           the whole step replays from a hipGraph without host work.
 #include "common.h"
 
+#include <type_traits>
+
 using namespace sl;
 
 namespace {
@@ -421,12 +423,26 @@ __device__ __forceinline__ short4_t ds_tr16_asm(const uint16_t* p) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
   return r;
 }
-__device__ __forceinline__ short8_t wg_tr8(const uint16_t* img, int k0, int n0, int lane) {
+// LDS byte address (within one image) of this lane's first tr read for the
+// fragment at column n0, rows k0.. (k0 % 32 == 0).  The other reads of the
+// fragment family are fixed byte offsets: +1024 (rows +4), +8192 (k0 + 32),
+// because f(r) is equal on those rows.
+__device__ __forceinline__ uint32_t wg_tr_addr(int n0, int lane) {
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   const int c = (n0 >> 3) + (p >> 1), w = (p & 1) * 4;
-  const int ra = k0 + 8 * g + q, rb = ra + 4;
-  const short4_t lo = ds_tr16_asm(img + ra * 128 + wg_swz(c, ra) * 8 + w);
-  const short4_t hi = ds_tr16_asm(img + rb * 128 + wg_swz(c, rb) * 8 + w);
+  const int ra = 8 * g + q;
+  return (uint32_t)((ra * 128 + wg_swz(c, ra) * 8 + w) * 2);
+}
+template <int OFF>
+__device__ __forceinline__ short4_t ds_tr16_off(uint32_t a) {
+  short4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+template <int KOFF>
+__device__ __forceinline__ short8_t wg_tr8(uint32_t a) {
+  const short4_t lo = ds_tr16_off<KOFF>(a);
+  const short4_t hi = ds_tr16_off<KOFF + 1024>(a);
   short8_t r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
@@ -495,21 +511,28 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
 
+  // per-lane tr-read addresses, computed once (slot base and k offsets are immediates/one add)
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
+  uint32_t a_addr[4], b_addr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a_addr[i] = wg_tr_addr(wm * 64 + i * 16, lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b_addr[j] = wg_tr_addr(wn * 64 + j * 16, lane);
+
   for (int st = 0; st < 3 && st < nst; ++st) issue(st);
   for (int st = 0; st < nst; ++st) {
     wg_vmcnt(8 * min(2, nst - 1 - st));  // this wave's pieces of stage st have landed
     __builtin_amdgcn_s_barrier();        // ... everyone's have; slot (st+3)%4 is free
     if (st + 3 < nst) issue(st + 3);
     if (m_live) {
-      const uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
-      const uint16_t* Bi = Ai + WG_IMG;
-#pragma unroll
-      for (int ks = 0; ks < 64; ks += 32) {
+      const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
+      auto kstep = [&](auto koff) {
+        constexpr int KO = decltype(koff)::value;
         short8_t af[4], bf[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = wg_tr8(Ai, ks, wm * 64 + i * 16, lane);
+        for (int i = 0; i < 4; ++i) af[i] = wg_tr8<KO>(sb + a_addr[i]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = wg_tr8(Bi, ks, wn * 64 + j * 16, lane);
+        for (int j = 0; j < 4; ++j) bf[j] = wg_tr8<KO + WG_IMG * 2>(sb + b_addr[j]);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -520,7 +543,9 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) accb[i] = mfma16(af[i], ones, accb[i]);
         }
-      }
+      };
+      kstep(std::integral_constant<int, 0>{});
+      kstep(std::integral_constant<int, 32 * 128 * 2>{});
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
