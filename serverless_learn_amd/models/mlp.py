@@ -308,27 +308,51 @@ class FusedMLPTrainer:
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
                None, n.stream_ptr())
 
+    def _launches(self):
+        """Cached launches for the current buffers/hyper-parameters (rebuilt on change)."""
+        key = (self.x.data_ptr() if self.x is not None else 0, self.n_batches, self.grad_scale, self.lr,
+               self.momentum, self.weight_decay)
+        if getattr(self, "_lkey", None) == key:
+            return self._lc
+        n, p = self._n, self._n.ptr
+        ws = (p(self.w1h), p(self.w2h), p(self.w2th), p(self.w3h), p(self.w3th))
+        lc = {
+            "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
+                             p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
+                             p(self.params), self.xa, self.xb, self.grad_scale,
+                             p(self.h1t), p(self.h2t), p(self.dzt), p(self.dh2t), p(self.dh1t), p(self.xn),
+                             p(self.loss), p(self.correct), None, 1),
+            "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.xn), p(self.h1t), p(self.h2t), p(self.dzt),
+                              p(self.dh2t), p(self.dh1t), p(self.slab), self.slices, self.n_pad),
+        }
+        for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
+                                                        "reduce": (1, False, True, False),
+                                                        "update": (2, True, False, True)}.items():
+            lc[name] = n.Launch("sl_mlp_sgd", p(self.params), p(self.mom),
+                                None if from_grad else p(self.slab), self.slices, self.n_pad,
+                                p(self.grad) if from_grad else None, p(self.grad) if grad_out else None,
+                                self.lr, self.momentum, self.weight_decay, mode, *ws,
+                                p(self.cursor) if bump else None)
+        self._lc, self._lkey = lc, key
+        return lc
+
     def _rows(self, train: bool = True):
+        if train:
+            return self._launches()["rows"]()
         n = self._n
         n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, self.grad_scale,
                n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t), n.ptr(self.xn),
-               n.ptr(self.loss), n.ptr(self.correct), None, 1 if train else 0, n.stream_ptr())
+               n.ptr(self.loss), n.ptr(self.correct), None, 0, n.stream_ptr())
 
     def _wgrad(self):
-        n = self._n
-        n.call("sl_mlp_wgrad", self.batch, n.ptr(self.xn), n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt),
-               n.ptr(self.dh2t), n.ptr(self.dh1t), n.ptr(self.slab), self.slices, self.n_pad, n.stream_ptr())
+        self._launches()["wgrad"]()
 
     def _sgd(self, mode: int, from_grad: bool, grad_out: bool, bump: bool = True):
-        n = self._n
-        n.call("sl_mlp_sgd", n.ptr(self.params), n.ptr(self.mom),
-               None if from_grad else n.ptr(self.slab), self.slices, self.n_pad,
-               n.ptr(self.grad) if from_grad else None, n.ptr(self.grad) if grad_out else None,
-               self.lr, self.momentum, self.weight_decay, mode,
-               n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
-               n.ptr(self.cursor) if bump else None, n.stream_ptr())
+        name = {(2, False, False, True): "sgd", (1, False, True, False): "reduce",
+                (2, True, False, True): "update"}[(mode, from_grad, grad_out, bump)]
+        self._launches()[name]()
 
     def compute_grads(self) -> torch.Tensor:
         """Forward + backward only; returns the reduced (local) gradient."""

@@ -25,6 +25,7 @@ from __future__ import annotations
 import datetime
 import os
 import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -57,6 +58,7 @@ class ElasticGroup:
         self.lock = threading.Lock()
         self.log = Logger("dp")
         self._stores = {}
+        self._rounds: dict[int, int] = {}
 
     @property
     def active(self) -> bool:
@@ -78,6 +80,29 @@ class ElasticGroup:
             except Exception as e:
                 self.log.warn("abort_failed", error=repr(e))
 
+    def _open_round(self, ep_store, epoch: int, rank: int) -> int:
+        """Agree on a fresh rendezvous round for this epoch.
+
+        Rank 0 opens round r+1 on every attempt; the other ranks join the first
+        round newer than the last one they tried.  A failed or half-formed
+        attempt therefore never leaves stale keys under the next attempt's
+        prefix (which would make gloo/RCCL connect to dead endpoints).
+        """
+        need = self._rounds.get(epoch, 0) + 1
+        if rank == 0:
+            rnd = int(ep_store.add("round", 1))
+        else:
+            deadline = time.monotonic() + self.timeout.total_seconds()
+            while True:
+                rnd = int(ep_store.add("round", 0))
+                if rnd >= need:
+                    break
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"rank 0 opened no round >= {need} for epoch {epoch}")
+                time.sleep(0.05)
+        self._rounds[epoch] = rnd
+        return rnd
+
     def reform(self, epoch: int, rank: int, world: int, rendezvous: str) -> bool:
         """Join the group for ``epoch``. Returns True when the group is usable."""
         with self.lock:
@@ -87,7 +112,9 @@ class ElasticGroup:
             if world <= 1 or rank < 0 or not rendezvous:
                 return True  # single worker: nothing to reduce
             try:
-                store = dist.PrefixStore(f"sl/epoch{epoch}", self._store(rendezvous))
+                base = self._store(rendezvous)
+                rnd = self._open_round(dist.PrefixStore(f"sl/e{epoch}", base), epoch, rank)
+                store = dist.PrefixStore(f"sl/e{epoch}/r{rnd}", base)
                 if self.backend == "nccl":
                     opts = dist.ProcessGroupNCCL.Options()
                     opts._timeout = self.timeout
@@ -96,7 +123,7 @@ class ElasticGroup:
                 else:
                     pg = dist.ProcessGroupGloo(store, rank, world, self.timeout)
                 self.pg = pg
-                self.log.info("group_formed", epoch=epoch, rank=rank, world=world, backend=self.backend)
+                self.log.info("group_formed", epoch=epoch, round=rnd, rank=rank, world=world, backend=self.backend)
                 return True
             except Exception as e:
                 self.broken = True

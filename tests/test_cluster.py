@@ -89,3 +89,46 @@ def test_resnet_worker_trains_on_cifar_shards():
         assert meta["model"] == "resnet18-cifar" and params.size == w.trainer.n_params
     finally:
         c.stop()
+
+
+def test_elastic_kill_two_respawn_two_resume_from_checkpoint():
+    """BASELINE config 5 (in-process, CPU): 4 all-reduce workers; 2 crash mid-run
+    (no Deregister); the survivors regroup; 2 fresh workers join, receive the
+    file server's checkpoint, get rank 0's state on regroup and train in lock-step."""
+    from serverless_learn_amd.ckpt.format import CKPT_BASE
+
+    c = LocalCluster(fast_config(checkpoint_every=15))
+    try:
+        ws = [c.add_worker(sync="allreduce", batch=128) for _ in range(4)]
+        assert c.wait_for(lambda: all(w.group.world == 4 and w.step > 30 for w in ws), 90), \
+            [(w.group.world, w.step) for w in ws]
+        assert c.wait_for(lambda: c.master.latest_ckpt >= CKPT_BASE, 30)
+        epoch0 = c.master.registry.epoch()
+        for v in ws[2:]:  # crash: stop training and serving, never deregister
+            v._stop.set()
+            v.server.stop(grace=0)
+        survivors = ws[:2]
+        assert c.wait_for(lambda: c.master.registry.epoch() > epoch0 and
+                          all(w.group.world == 2 for w in survivors), 60), \
+            [(w.group.world, w.group.epoch) for w in survivors]
+        s0 = [w.step for w in survivors]
+        assert c.wait_for(lambda: all(w.step > s + 10 for w, s in zip(survivors, s0)), 60)
+        fresh = [c.add_worker(sync="allreduce", batch=128) for _ in range(2)]
+        group = survivors + fresh
+        assert c.wait_for(lambda: all(w.group.world == 4 for w in group) and
+                          all(w.step > 10 for w in fresh), 90), \
+            [(w.group.world, w.step, w.state) for w in group]
+        assert all(any(f >= CKPT_BASE for f in w.files_received) for w in fresh), \
+            [w.files_received for w in fresh]
+        # lock-step replicas: stop all four at the same step and compare
+        target = max(w.step for w in group) + 15
+        for w in group:
+            w.cfg.max_steps = target
+        assert c.wait_for(lambda: all(w.state == "done" for w in group), 90), [(w.step, w.state) for w in group]
+        steps = {w.step for w in group}
+        assert steps == {target}, steps
+        params = [w.trainer.params for w in group]
+        assert all(torch.equal(params[0], p) for p in params[1:])
+        assert min(steps) > max(s0), (steps, s0)  # resumed, not restarted from 0
+    finally:
+        c.stop()
