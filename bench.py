@@ -50,7 +50,9 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
-    ap.add_argument("--ingest", choices=["grpc", "local"], default="grpc")
+    ap.add_argument("--ingest", choices=["grpc", "local", "device"], default="grpc",
+                    help="grpc: file server -> ReceiveFile -> pinned ring -> HBM; local: host-generated shard; "
+                         "device: shard synthesised in HBM by the Philox kernel (K8)")
     ap.add_argument("--bucket-mb", type=float, default=16.0, help="CNN all-reduce bucket size")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
@@ -88,16 +90,21 @@ def main(argv=None) -> int:
 
     # ---- 1. shard delivery -------------------------------------------------
     t_ingest = time.perf_counter()
-    if args.ingest == "grpc":
-        from serverless_learn_amd.runtime.local_cluster import fetch_shard_via_grpc
+    if args.ingest == "device":
+        from serverless_learn_amd.data.device_synth import synth_on_device
 
-        host_buf = fetch_shard_via_grpc(n_records=n_records, shard_index=rank, num_shards=world, seed=0,
-                                        dataset=dataset)
+        x, y = synth_on_device("mnist" if mlp else "cifar", n_records, seed=rank, device=dev)
     else:
-        host_buf = make_shard(n_records, shard_index=rank, num_shards=world, seed=0, dataset=dataset)
-    hdr, images, labels = decode_shard(bytearray(host_buf))
-    x = torch.from_numpy(images).pin_memory().to(dev, non_blocking=True)
-    y = torch.from_numpy(labels.copy()).pin_memory().to(dev, non_blocking=True)
+        if args.ingest == "grpc":
+            from serverless_learn_amd.runtime.local_cluster import fetch_shard_via_grpc
+
+            host_buf = fetch_shard_via_grpc(n_records=n_records, shard_index=rank, num_shards=world, seed=0,
+                                            dataset=dataset)
+        else:
+            host_buf = make_shard(n_records, shard_index=rank, num_shards=world, seed=0, dataset=dataset)
+        hdr, images, labels = decode_shard(bytearray(host_buf))
+        x = torch.from_numpy(images).pin_memory().to(dev, non_blocking=True)
+        y = torch.from_numpy(labels.copy()).pin_memory().to(dev, non_blocking=True)
     torch.cuda.synchronize()
     t_ingest = time.perf_counter() - t_ingest
 

@@ -87,3 +87,18 @@ def test_gpu_worker_trains_from_pushed_shard():
         assert st.accuracy > 0.8, st
     finally:
         c.stop()
+
+
+def test_device_synth_matches_numpy_reference():
+    """K8: the on-device Philox generator reproduces the numpy reference (u8 +-1 at fp32 rounding ties)."""
+    import numpy as np
+
+    from serverless_learn_amd.data.device_synth import synth_on_device, synth_reference
+
+    for kind, first in (("mnist", 0), ("cifar", 1234567)):
+        img, lab = synth_on_device(kind, 96, seed=0xABCDEF0123, first=first)
+        ref_img, ref_lab = synth_reference(kind, 96, seed=0xABCDEF0123, first=first)
+        torch.cuda.synchronize()
+        assert np.array_equal(lab.cpu().numpy(), ref_lab)
+        diff = np.abs(img.cpu().numpy().astype(int) - ref_img.astype(int))
+        assert diff.max() <= 1 and (diff > 0).mean() < 0.01, (kind, diff.max(), (diff > 0).mean())
