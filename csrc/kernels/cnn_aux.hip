@@ -194,6 +194,134 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
 }
 
 // ---------------------------------------------------------------------------
+// Fused forms used by the engine: the per-channel finalize folds into the
+// element-wise pass (each thread owns 8 fixed channels, so it derives their
+// coefficients once from the raw sums), and workgroup 0 publishes the
+// coefficients / running statistics / dgamma, dbeta.  Two fewer launches per
+// BatchNorm per direction (a 1-WG kernel costs ~4.5 us of serialised time).
+struct BnStats {
+  const float* stats;  // [2][C] sum, sum of squares (conv epilogue)
+  const float* gamma;
+  const float* beta;
+  float* coef;         // [4][C] out: scale, shift, mean, rstd (for backward)
+  float* run_mean;
+  float* run_var;
+};
+
+__device__ __forceinline__ void bn_coef8(const BnStats& b, int C, int c0, float count, float eps, float (&sc)[8],
+                                         float (&sh)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float mean = b.stats[c0 + j] / count;
+    const float var = fmaxf(b.stats[C + c0 + j] / count - mean * mean, 0.f);
+    sc[j] = b.gamma[c0 + j] * rsqrtf(var + eps);
+    sh[j] = b.beta[c0 + j] - mean * sc[j];
+  }
+}
+
+__device__ __forceinline__ void bn_publish(const BnStats& b, int C, float count, float eps, float momentum) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float mean = b.stats[c] / count;
+    const float var = fmaxf(b.stats[C + c] / count - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + eps);
+    const float sc = b.gamma[c] * rstd;
+    b.coef[c] = sc;
+    b.coef[C + c] = b.beta[c] - mean * sc;
+    b.coef[2 * C + c] = mean;
+    b.coef[3 * C + c] = rstd;
+    if (b.run_mean) {
+      b.run_mean[c] = (1.f - momentum) * b.run_mean[c] + momentum * mean;
+      b.run_var[c] = (1.f - momentum) * b.run_var[c] + momentum * var * (count / fmaxf(count - 1.f, 1.f));
+    }
+  }
+}
+
+// y = relu?(bn(x) + r), r = 0 | res | bn_r(res); grid stride is a multiple of C/8.
+__global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __restrict__ x, BnStats b,
+                                                             const uint16_t* __restrict__ res, BnStats rb,
+                                                             uint16_t* __restrict__ y, long rows, int C, int relu,
+                                                             int mode, float count, float eps, float momentum) {
+  const int cpr = C >> 3;
+  const long total = rows * cpr;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(t0 % cpr) * 8;
+  float sc[8], sh[8], rsc[8], rsh[8];
+  bn_coef8(b, C, c0, count, eps, sc, sh);
+  if (mode == 2) bn_coef8(rb, C, c0, count, eps, rsc, rsh);
+  for (long q = t0; q < total; q += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(ld8(x + q * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+    if (mode) {
+      float r[8];
+      unpack8(ld8(res + q * 8), r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += mode == 2 ? r[j] * rsc[j] + rsh[j] : r[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    *reinterpret_cast<short8_t*>(y + q * 8) = pack8(f);
+  }
+  if (blockIdx.x == 0) {
+    bn_publish(b, C, count, eps, momentum);
+    if (mode == 2) bn_publish(rb, C, count, eps, momentum);
+  }
+}
+
+// dx = a*dz + b*x + c with (a, b, c) derived per channel from the reduce
+// kernel's sums and the forward coefficients; workgroup 0 adds dgamma, dbeta.
+__global__ __launch_bounds__(256) void bn_bwd_apply_sums_kernel(const uint16_t* __restrict__ dy,
+                                                                const uint16_t* __restrict__ y,
+                                                                const uint16_t* __restrict__ x,
+                                                                const float* __restrict__ sums,
+                                                                const float* __restrict__ coef,
+                                                                float* __restrict__ grad_gamma,
+                                                                float* __restrict__ grad_beta,
+                                                                uint16_t* __restrict__ dx, long rows, int C,
+                                                                float count) {
+  const int cpr = C >> 3;
+  const long total = rows * cpr;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(t0 % cpr) * 8;
+  float ca[8], cb[8], cc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const float s0 = sums[c], s1 = sums[C + c];
+    const float sc = coef[c], mean = coef[2 * C + c], rstd = coef[3 * C + c];
+    const float sdxh = rstd * (s1 - mean * s0);
+    ca[j] = sc;
+    cb[j] = -sc * rstd * sdxh / count;
+    cc[j] = -sc * s0 / count - cb[j] * mean;
+  }
+  for (long q = t0; q < total; q += (long)gridDim.x * blockDim.x) {
+    float g[8], xv[8];
+    unpack8(ld8(dy + q * 8), g);
+    if (y) {
+      float yv[8];
+      unpack8(ld8(y + q * 8), yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    }
+    unpack8(ld8(x + q * 8), xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = ca[j] * g[j] + cb[j] * xv[j] + cc[j];
+    *reinterpret_cast<short8_t*>(dx + q * 8) = pack8(g);
+  }
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float s0 = sums[c], s1 = sums[C + c];
+      const float mean = coef[2 * C + c], rstd = coef[3 * C + c];
+      if (grad_gamma) grad_gamma[c] += rstd * (s1 - mean * s0);
+      if (grad_beta) grad_beta[c] += s0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Max pool (KxK, stride s, pad p) with a per-output argmax tap (u8) for backward.
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C,
@@ -417,6 +545,31 @@ int sl_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, co
   if (C & 7) return -1;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, dy, y, x, dcoef,
                      dx, rows, C);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_bn_apply_stats(const uint16_t* x, const float* stats, const float* gamma, const float* beta, float* coef,
+                      float* run_mean, float* run_var, const uint16_t* res, const float* rstats, const float* rgamma,
+                      const float* rbeta, float* rcoef, float* rrun_mean, float* rrun_var, uint16_t* y, long rows,
+                      int C, int relu, int mode, float count, float eps, float momentum, hipStream_t stream) {
+  if ((C & 7) || 256 % (C / 8) != 0) return -1;
+  if (mode && !res) return -2;
+  if (mode == 2 && !rstats) return -2;
+  BnStats b{stats, gamma, beta, coef, run_mean, run_var};
+  BnStats rb{rstats, rgamma, rbeta, rcoef, rrun_mean, rrun_var};
+  hipLaunchKernelGGL(bn_apply_stats_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, x, b, res, rb, y,
+                     rows, C, relu, mode, count, eps, momentum);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_bn_bwd_apply_sums(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* sums,
+                         const float* coef, float* grad_gamma, float* grad_beta, uint16_t* dx, long rows, int C,
+                         float count, hipStream_t stream) {
+  if ((C & 7) || 256 % (C / 8) != 0) return -1;
+  hipLaunchKernelGGL(bn_bwd_apply_sums_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, dy, y, x, sums,
+                     coef, grad_gamma, grad_beta, dx, rows, C, count);
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -390,22 +390,38 @@ struct WtDesc {
   const uint16_t* w;
   uint16_t* wt;
   int cout, taps, cin, ldt;  // wt row stride = taps*ldt
-  long begin;                // first flat work item of this conv
+  long begin;                // first 64x64 tile of this conv (tile-granular work list)
 };
 
+// One workgroup per 64 (co) x 64 (ci) tile of one tap of one conv, through
+// LDS: coalesced 16-B reads along ci, coalesced writes along co.
 __global__ __launch_bounds__(256) void conv_wt_kernel(const WtDesc* __restrict__ d, int nd, long total) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int lo = 0, hi = nd - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (d[mid].begin <= i) lo = mid; else hi = mid - 1;
-    }
-    const WtDesc& D = d[lo];
-    const long j = i - D.begin;  // destination index in [cin][taps][ldt]
-    const int co = (int)(j % D.ldt);
-    const long r = j / D.ldt;
-    const int tap = (int)(r % D.taps), ci = (int)(r / D.taps);
-    D.wt[j] = co < D.cout ? D.w[((long)co * D.taps + tap) * D.cin + ci] : (uint16_t)0;
+  __shared__ uint16_t tile[64][66];
+  const long b = blockIdx.x;
+  if (b >= total) return;
+  int lo = 0, hi = nd - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const WtDesc& D = d[lo];
+  const int tco = (D.ldt + 63) / 64, tci = (D.cin + 63) / 64;
+  long j = b - D.begin;
+  const int tap = (int)(j / ((long)tco * tci));
+  j -= (long)tap * tco * tci;
+  const int ti = (int)(j / tco), to = (int)(j - (long)ti * tco);
+  const int co0 = to * 64, ci0 = ti * 64;
+  const int t = threadIdx.x;
+  for (int e = t; e < 64 * 64; e += 256) {  // read W[co][tap][ci] rows (ci contiguous)
+    const int r = e >> 6, c = e & 63;
+    const int co = co0 + r, ci = ci0 + c;
+    tile[r][c] = (co < D.cout && ci < D.cin) ? D.w[((long)co * D.taps + tap) * D.cin + ci] : (uint16_t)0;
+  }
+  __syncthreads();
+  for (int e = t; e < 64 * 64; e += 256) {  // write Wt[ci][tap][co] rows (co contiguous)
+    const int r = e >> 6, c = e & 63;
+    const int ci = ci0 + r, co = co0 + c;
+    if (ci < D.cin && co < D.ldt) D.wt[((long)ci * D.taps + tap) * D.ldt + co] = tile[c][r];
   }
 }
 
@@ -495,11 +511,10 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
 }
 
 // Multi-tensor weight re-layout; `descs` is a device array of WtDesc.
+// `total` = number of 64x64 tiles over all descriptors (WtDesc.begin is tile-granular).
 int sl_conv_wt(const void* descs, int nd, long total, hipStream_t stream) {
   if (nd <= 0 || total <= 0) return 0;
-  long blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(conv_wt_kernel, dim3(blocks), dim3(256), 0, stream, (const WtDesc*)descs, nd, total);
+  hipLaunchKernelGGL(conv_wt_kernel, dim3(total), dim3(256), 0, stream, (const WtDesc*)descs, nd, total);
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -8,10 +8,10 @@ and replayed with zero host work (the data batch is chosen by a device-side
 cursor, like the MLP engine).
 
 Per step:
-  forward   input_norm -> [conv (+BN stats in the epilogue) -> bn_finalize ->
-            bn_apply(+residual, ReLU)] x 20 -> avgpool -> fc (fp32 logits) ->
+  forward   input_norm -> [conv (+BN stats in the epilogue) -> bn_apply with
+            the finalize folded in (+residual, ReLU)] x 20 -> avgpool -> fc -> 
             softmax-CE (loss, dlogits, dbias)
-  backward  per block, in reverse: bn_bwd_reduce/finalize/apply (ReLU mask
+  backward  per block, in reverse: bn_bwd_reduce + bn_bwd_apply (ReLU mask
             fused), conv wgrad (split-K, fp32 atomics straight into the flat
             gradient) and dgrad (residual gradient fused into its epilogue)
   comms     optional: the flat gradient is laid out in forward order, so
@@ -188,8 +188,6 @@ class FusedResNetTrainer:
         K = self.K
         c = conv.spec
         K.conv_fwd(x, conv.w, c.cout, c.k, c.stride, c.pad, y=out, stats=bn.stats)
-        K.bn_finalize(bn.stats, bn.gamma, bn.beta, bn.coef, bn.run_mean, bn.run_var,
-                      out.numel() // c.cout, momentum=self.bn_momentum)
 
     def forward(self, train: bool = True):
         K, spec = self.K, self.spec
@@ -197,21 +195,22 @@ class FusedResNetTrainer:
         K.input_norm(self.x, self.y, self.cursor, self.batch, self.x0, self.labels, CIFAR_MEAN, CIFAR_STD)
         sbn = self.bn[spec.stem_bn.name]
         self._conv_bn(self.x0, self.conv["stem"], sbn, self.c0)
-        K.bn_apply(self.c0, sbn.coef, self.a0, relu=True)
+        K.bn_apply_stats(self.c0, sbn, self.a0, self.c0.numel() // 64, momentum=self.bn_momentum)
         if spec.stem == "imagenet":
             K.maxpool_fwd(self.a0, self.p0, self.p0_arg)
         for st in self.blocks:
             blk: BlockSpec = st["spec"]
             b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
             self._conv_bn(st["x"], self.conv[blk.conv1.name], b1, st["c1"])
-            K.bn_apply(st["c1"], b1.coef, st["a1"], relu=True)
+            cnt = st["c1"].numel() // blk.conv1.cout
+            K.bn_apply_stats(st["c1"], b1, st["a1"], cnt, momentum=self.bn_momentum)
             self._conv_bn(st["a1"], self.conv[blk.conv2.name], b2, st["c2"])
             if blk.down is not None:
                 bd = self.bn[blk.dbn.name]
                 self._conv_bn(st["x"], self.conv[blk.down.name], bd, st["cs"])
-                K.bn_apply(st["c2"], b2.coef, st["y"], relu=True, res=st["cs"], rcoef=bd.coef)
+                K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=st["cs"], rbn=bd, momentum=self.bn_momentum)
             else:
-                K.bn_apply(st["c2"], b2.coef, st["y"], relu=True, res=st["x"])
+                K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=st["x"], momentum=self.bn_momentum)
         K.avgpool_fwd(self.feat_in, self.feat)
         K.conv_fwd(self.feat, self.fc_w, spec.classes, 1, 1, 0, yf=self.logits, bias=self.fc_b)
         K.softmax_ce(self.logits, self.labels, self.loss, self.correct, self.dlogits.view(self.batch, LOGIT_LD),
@@ -239,25 +238,21 @@ class FusedResNetTrainer:
             blk: BlockSpec = st["spec"]
             c1, c2 = self.conv[blk.conv1.name], self.conv[blk.conv2.name]
             b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
-            n1 = st["c1"].numel() // blk.conv1.cout
             # y = relu(bn2(c2) + sc): dz = dy * 1[y > 0] feeds bn2 and the shortcut
             K.bn_bwd_reduce(dy, st["y"], st["c2"], b2.sums, dz_out=st["dz"])
-            K.bn_bwd_finalize(b2.sums, b2.coef, b2.dcoef, b2.ggamma, b2.gbeta, n1)
             add = st["dz"]
             if blk.down is not None:
                 cd, bd = self.conv[blk.down.name], self.bn[blk.dbn.name]
                 K.bn_bwd_reduce(st["dz"], None, st["cs"], bd.sums)
-                K.bn_bwd_finalize(bd.sums, bd.coef, bd.dcoef, bd.ggamma, bd.gbeta, n1)
-                K.bn_bwd_apply(st["dz"], None, st["cs"], bd.dcoef, st["dcs"])
+                K.bn_bwd_apply_sums(st["dz"], None, st["cs"], bd.sums, bd.coef, bd.ggamma, bd.gbeta, st["dcs"])
                 K.conv_wgrad(st["x"], st["dcs"], blk.down.cout, 1, blk.down.stride, 0, cd.g)
                 K.conv_dgrad(st["dcs"], cd.wt, blk.down.cin, 1, blk.down.stride, 0, st["dxs"])
                 add = st["dxs"]
-            K.bn_bwd_apply(st["dz"], None, st["c2"], b2.dcoef, st["dc2"])
+            K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
             K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g)
             K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"])
             K.bn_bwd_reduce(st["da1"], st["a1"], st["c1"], b1.sums)
-            K.bn_bwd_finalize(b1.sums, b1.coef, b1.dcoef, b1.ggamma, b1.gbeta, n1)
-            K.bn_bwd_apply(st["da1"], st["a1"], st["c1"], b1.dcoef, st["dc1"])
+            K.bn_bwd_apply_sums(st["da1"], st["a1"], st["c1"], b1.sums, b1.coef, b1.ggamma, b1.gbeta, st["dc1"])
             K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g)
             K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, st["dx"], add=add)
             dy = st["dx"]
@@ -267,10 +262,8 @@ class FusedResNetTrainer:
         if spec.stem == "imagenet":
             K.maxpool_bwd(dy, self.p0_arg, self.da0)
             dy = self.da0
-        n0 = self.c0.numel() // 64
         K.bn_bwd_reduce(dy, self.a0, self.c0, sbn.sums)
-        K.bn_bwd_finalize(sbn.sums, sbn.coef, sbn.dcoef, sbn.ggamma, sbn.gbeta, n0)
-        K.bn_bwd_apply(dy, self.a0, self.c0, sbn.dcoef, self.dc0)
+        K.bn_bwd_apply_sums(dy, self.a0, self.c0, sbn.sums, sbn.coef, sbn.ggamma, sbn.gbeta, self.dc0)
         sc = spec.stem_conv
         K.conv_wgrad(self.x0, self.dc0, 64, sc.k, sc.stride, sc.pad, self.conv["stem"].g)
         maybe_bucket(0, force=True)

@@ -27,6 +27,8 @@ N.register("sl_bn_apply", [P, P, P, P, P, L, I, I, I, P])
 N.register("sl_bn_bwd_reduce", [P, P, P, P, P, L, I, P])
 N.register("sl_bn_bwd_finalize", [P, P, P, P, P, I, F, P])
 N.register("sl_bn_bwd_apply", [P, P, P, P, P, L, I, P])
+N.register("sl_bn_apply_stats", [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, F, F, F, P])
+N.register("sl_bn_bwd_apply_sums", [P, P, P, P, P, P, P, P, L, I, F, P])
 N.register("sl_maxpool_fwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_maxpool_bwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_avgpool_fwd", [P, P, I, I, I, P])
@@ -101,7 +103,7 @@ class WeightTransposer:
         for i, (w, wt, cout, taps, cin, ldt) in enumerate(items):
             assert wt.numel() == cin * taps * ldt and w.numel() >= cout * taps * cin
             arr[i] = WtDesc(p(w), p(wt), cout, taps, cin, ldt, total)
-            total += wt.numel()
+            total += taps * ((ldt + 63) // 64) * ((cin + 63) // 64)  # 64x64 tiles
         host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         self.desc = host.to(device)
         self.n = len(items)
@@ -157,6 +159,27 @@ def bn_bwd_apply(dy, y, x, dcoef, dx):
     rows = x.numel() // c
     N.call("sl_bn_bwd_apply", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x), _f32(dcoef), _bf16(dx),
            rows, c, N.stream_ptr())
+
+
+def bn_apply_stats(x, bn, y, count, relu=True, res=None, rbn=None, eps=1e-5, momentum=0.1):
+    """Fused finalize + apply; ``bn``/``rbn`` expose stats, gamma, beta, coef, run_mean, run_var."""
+    c = x.shape[-1]
+    rows = x.numel() // c
+    mode = 0 if res is None else (2 if rbn is not None else 1)
+    r = rbn
+    N.call("sl_bn_apply_stats", _bf16(x), _f32(bn.stats), _f32(bn.gamma), _f32(bn.beta), _f32(bn.coef),
+           _f32(bn.run_mean), _f32(bn.run_var), _bf16(res) if res is not None else None,
+           _f32(r.stats) if r else None, _f32(r.gamma) if r else None, _f32(r.beta) if r else None,
+           _f32(r.coef) if r else None, _f32(r.run_mean) if r else None, _f32(r.run_var) if r else None,
+           _bf16(y), rows, c, 1 if relu else 0, mode, float(count), float(eps), float(momentum), N.stream_ptr())
+
+
+def bn_bwd_apply_sums(dy, y, x, sums, coef, grad_gamma, grad_beta, dx):
+    """Fused backward finalize + apply: dx, and dgamma/dbeta accumulated into the flat gradient."""
+    c = x.shape[-1]
+    rows = x.numel() // c
+    N.call("sl_bn_bwd_apply_sums", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x), _f32(sums),
+           _f32(coef), _f32(grad_gamma), _f32(grad_beta), _bf16(dx), rows, c, float(rows), N.stream_ptr())
 
 
 def maxpool_fwd(x, y, arg, k=3, s=2, pad=1):

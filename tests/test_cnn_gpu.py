@@ -83,13 +83,13 @@ def test_conv_fwd_dgrad_wgrad(case):
 def test_weight_transposer_matches_permute():
     from serverless_learn_amd.ops import cnn as K
 
-    w1 = bf(torch.randn(64, 3, 3, 32, device=DEV))
+    w1 = bf(torch.randn(64, 3, 3, 96, device=DEV))
     w2 = bf(torch.randn(10, 1, 1, 512, device=DEV))
-    t1 = torch.empty(32 * 9 * 64, dtype=torch.bfloat16, device=DEV)
+    t1 = torch.empty(96 * 9 * 64, dtype=torch.bfloat16, device=DEV)
     t2 = torch.empty(512 * 16, dtype=torch.bfloat16, device=DEV)
-    K.WeightTransposer([(w1.reshape(-1), t1, 64, 9, 32, 64), (w2.reshape(-1), t2, 10, 1, 512, 16)], DEV)()
+    K.WeightTransposer([(w1.reshape(-1), t1, 64, 9, 96, 64), (w2.reshape(-1), t2, 10, 1, 512, 16)], DEV)()
     torch.cuda.synchronize()
-    assert torch.equal(t1.view(32, 9, 64), w1.reshape(64, 9, 32).permute(2, 1, 0))
+    assert torch.equal(t1.view(96, 9, 64), w1.reshape(64, 9, 96).permute(2, 1, 0))
     e2 = torch.zeros(512, 16, dtype=torch.bfloat16, device=DEV)
     e2[:, :10] = w2.reshape(10, 512).t()
     assert torch.equal(t2.view(512, 16), e2)
@@ -135,6 +135,32 @@ def test_bn_forward_backward_matches_torch():
     assert rel(dx.float().permute(0, 3, 1, 2), xr.grad) < 2e-2
     assert rel(gg, g_.grad) < 1e-2 and rel(gb, b_.grad) < 1e-2
     assert torch.equal(dz.float(), dy.float() * (y.float() > 0))
+
+    # fused engine forms: finalize folded into apply (fwd) and into bwd-apply
+    class _B:
+        pass
+    b = _B()
+    b.stats, b.gamma, b.beta = stats, gamma, beta
+    b.coef, b.run_mean, b.run_var = torch.zeros(4 * c, device=DEV), torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+    rbn = _B()
+    rf = res.float().reshape(-1, c)
+    rbn.stats = torch.stack([rf.sum(0), (rf * rf).sum(0)]).reshape(-1).contiguous()
+    rbn.gamma, rbn.beta = torch.rand(c, device=DEV) + 0.5, torch.randn(c, device=DEV)
+    rbn.coef, rbn.run_mean, rbn.run_var = torch.zeros(4 * c, device=DEV), torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+    y2 = torch.empty_like(x)
+    K.bn_apply_stats(x, b, y2, xf.shape[0], res=res)
+    y3 = torch.empty_like(x)
+    K.bn_apply_stats(x, b, y3, xf.shape[0], res=res, rbn=rbn)
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y) and torch.allclose(b.coef, coef)
+    ref3 = F.relu(F.batch_norm(x.float().permute(0, 3, 1, 2), None, None, gamma, beta, training=True) +
+                  F.batch_norm(res.float().permute(0, 3, 1, 2), None, None, rbn.gamma, rbn.beta, training=True))
+    assert rel(y3.float().permute(0, 3, 1, 2), ref3) < 1e-2
+    gg2, gb2 = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
+    dx2 = torch.empty_like(x)
+    K.bn_bwd_apply_sums(dy, y, x, sums, coef, gg2, gb2, dx2)
+    torch.cuda.synchronize()
+    assert rel(dx2, dx) < 1e-3 and rel(gg2, gg) < 1e-5 and rel(gb2, gb) < 1e-5
 
 
 def test_pools_and_softmax_ce():
