@@ -18,7 +18,8 @@ RANK/LOCAL_RANK/WORLD_SIZE); each rank is one worker that
 synthetic CIFAR-shaped 32x32x3 data, implicit-GEMM convolutions), with the
 gradient all-reduce bucketed and overlapped with backward.
 
-Weak scaling: the per-GPU batch is fixed as N grows.  The reference publishes
+Weak scaling: the per-GPU batch is fixed as N grows (MLP default 65,536 rows
+per GPU; ``--batch 16384`` reproduces the smaller configuration).  The reference publishes
 no number; ``vs_baseline`` is against the reference's derived
 data-delivery ceiling of 25,478 samples/s per worker (BASELINE.md row
 "Derived: data-delivery ceiling"), i.e. 25,478 * N.
@@ -59,8 +60,10 @@ def parse(argv=None):
     mlp = a.model == "mlp"
     a.steps = a.steps if a.steps is not None else (200 if mlp else 30)
     a.warmup = a.warmup if a.warmup is not None else (20 if mlp else 5)
-    a.batch = a.batch or (16384 if mlp else 256)
-    a.shard_batches = a.shard_batches or (8 if mlp else 4)
+    # MLP: 65,536 rows per GPU -- 1,024 row blocks, i.e. 4 per CU (16,384 leaves one per CU and the
+    # step latency-bound); the shard (4 batches, 205 MB u8) is a sliver of the 288 GB of HBM.
+    a.batch = a.batch or (65536 if mlp else 256)
+    a.shard_batches = a.shard_batches or (4 if mlp else 4)
     a.lr = a.lr if a.lr is not None else (0.05 if mlp else 0.1)
     return a
 

@@ -104,7 +104,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 }
 
 // Per-channel sums of dz = dy*1[y>0] and dz*x.  Thread layout: TPR = C/8
-// threads per row, 256/TPR rows per pass; partials folded through LDS.
+// threads per row, 256/TPR rows per pass; partials folded through LDS, then
+// across workgroups through an rsum buffer (result at rsum_result(sums, 2C)).
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
                                                             const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ x,
@@ -142,13 +143,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   }
   __syncthreads();
   // fold the rpp row-groups: thread t < 2*C handles one (quantity, channel)
+  float* rep = rsum_replica(sums, 2 * C);
   for (int t = tid; t < 2 * C; t += 256) {
     const int qsel = t / C, c = t - qsel * C;
     const int g = c >> 3, j = c & 7;
     float acc = 0.f;
     for (int r = 0; r < rpp; ++r) acc += part[r * tpr + g][qsel * 8 + j];
-    atomicAdd(sums + qsel * C + c, acc);
+    atomicAdd(rep + qsel * C + c, acc);
   }
+  rsum_finish(sums, 2 * C, reinterpret_cast<int*>(&part[0][16]));
 }
 
 // dcoef layout [3][C]: a, b, c with dx = a*dz + b*x + c.  grad_gamma/beta += (flat gradient).
@@ -478,6 +481,9 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict
 
 // ---------------------------------------------------------------------------
 extern "C" {
+
+long sl_rsum_floats(int n) { return rsum_floats(n); }
+long sl_rsum_result_offset(int n) { return (long)SL_REP * n; }
 
 int sl_input_norm(const uint8_t* x, const uint8_t* lab, const int* cursor, int n_batches, int batch,
                   long img_pixels, uint16_t* y, uint8_t* lab_out, float m0, float m1, float m2, float s0, float s1,

@@ -4,8 +4,14 @@
 // part of the compute layer that replaces it.
 //
 // Layout is channels-last everywhere (activations NHWC bf16, weights
-// [Cout][KH][KW][Cin] bf16), so the im2col matrix is never materialised: the
-// GEMM's LDS staging pass gathers it on the fly, 8 channels (16 B) per load.
+// [Cout][KH][KW][Cin] bf16), so the im2col matrix is never materialised: each
+// lane's 16-B piece of an operand tile is GATHERED straight from the NHWC
+// tensor (8 channels of one tap) by LDS-DMA (global_load_lds_dwordx4 with a
+// per-lane source address; padded taps point at a zero block), into a 4-slot
+// LDS ring with three 64-deep stages in flight -- no VGPR staging, counted
+// vmcnt + raw s_barrier, fragment reads as inline asm so hipcc does not drain
+// the DMA queue in front of them (cdna_hip_programming.md §5, "Three .s-level
+// traps").  The LDS images are XOR-swizzled on the SOURCE side (rule 21).
 //
 //   conv_gemm_kernel<BM,BN,false>  forward   Y[m][co] = sum_k im2col(X)[m][k] W[co][k]
 //   conv_gemm_kernel<BM,BN,true>   dgrad     dX[m][ci] = sum_k col(dY)[m][k] Wt[ci][k]
@@ -14,29 +20,35 @@
 //                                  the division is exact and in range)
 //   conv_wgrad_kernel<BMO>         wgrad     dW[co][k] += sum_m dY[m][co] im2col(X)[m][k]
 //                                  (reduction over the batch*pixels index, split
-//                                  over workgroups, fp32 atomics into the flat
-//                                  gradient; both operands are read transposed
-//                                  out of LDS with ds_read_b64_tr_b16)
+//                                  over workgroups; both operands land as
+//                                  row-major [64 m][.] images and are read
+//                                  transposed with ds_read_b64_tr_b16)
 //
 // Forward epilogue options, all fused: per-channel BatchNorm statistics
 // (sum, sum of squares of the fp32 accumulator -> fp32 atomics), bias, fp32
 // output (logits), residual add (dgrad of a tensor that also feeds a skip).
 #include "common.h"
 
+#include <type_traits>
+
 using namespace sl;
 
 namespace {
-constexpr int BK = 64;        // reduction depth per LDS stage
-constexpr int LDK = BK + 8;   // 144-B LDS rows: 16 consecutive rows hit 16 distinct 16-B slots (ds_read_b128)
-constexpr int WG_M = 64;      // wgrad: batch*pixel rows per LDS stage
-constexpr int LDT = 128 + 8;  // wgrad LDS image row stride (elements), as the MLP wgrad kernel
+constexpr int BK = 64;     // reduction depth per stage
+constexpr int WG_M = 64;   // wgrad: batch*pixel rows per stage
 }  // namespace
+
+// 16-B source for padded taps, rows past M and columns past the operand.
+__device__ __attribute__((aligned(16))) uint16_t g_conv_zero[64];
 
 struct ConvGeom {
   const uint16_t* src;  // gather source, NHWC [N][SH][SW][SC]
   int N, SH, SW, SC, c_shift;
   int OH, OW;           // GEMM rows = pixels (n, oh, ow) of the produced tensor
+  int hw_shift, w_shift;  // log2(OH*OW), log2(OW) when powers of two, else -1
   int KH, KW, stride, pad;
+  int kw_magic;         // tap / KW == (tap * kw_magic) >> 16 for the tap counts used here
+  int s_shift;          // log2(stride) (strides are powers of two)
   int K;                // KH*KW*SC
   int M;                // N*OH*OW
 };
@@ -49,10 +61,9 @@ struct ConvEpi {
   float* yf;            // [M][ncols] fp32 output (nullable)
   const float* bias;    // [ncols] (nullable)
   const uint16_t* add;  // [M][ldy] bf16 added to the result (nullable)
-  float* stats;         // [2][ncols] fp32: sum, sum of squares (nullable)
+  float* stats;         // rsum buffer of 2*ncols (sum, sum of squares), zeroed (nullable)
 };
 
-// Pixel decode for one GEMM row.
 struct Pix {
   int n, oh, ow;
   bool ok;
@@ -62,55 +73,133 @@ __device__ __forceinline__ Pix decode_pix(const ConvGeom& g, int m) {
   Pix p;
   p.ok = m < g.M;
   const int mm = p.ok ? m : 0;
-  const int hw = g.OH * g.OW;
-  p.n = mm / hw;
-  const int r = mm - p.n * hw;
-  p.oh = r / g.OW;
-  p.ow = r - p.oh * g.OW;
+  int r;
+  if (g.hw_shift >= 0) {
+    p.n = mm >> g.hw_shift;
+    r = mm & ((1 << g.hw_shift) - 1);
+  } else {
+    const int hw = g.OH * g.OW;
+    p.n = mm / hw;
+    r = mm - p.n * hw;
+  }
+  if (g.w_shift >= 0) {
+    p.oh = r >> g.w_shift;
+    p.ow = r & ((1 << g.w_shift) - 1);
+  } else {
+    p.oh = r / g.OW;
+    p.ow = r - p.oh * g.OW;
+  }
   return p;
 }
 
-// 8 consecutive reduction elements (one tap, 8 channels) of row `p` at k0.
+// Source of the 8 consecutive reduction elements (one tap, 8 channels) of row p at k0
+// (general path: any channel count; used by the stem and the weight gradient).
 template <bool TRANSPOSED>
-__device__ __forceinline__ short8_t gather8(const ConvGeom& g, const Pix& p, int k0) {
-  if (!p.ok || k0 >= g.K) return zero8();
+__device__ __forceinline__ const uint16_t* gather_src(const ConvGeom& g, const Pix& p, int k0) {
+  if (!p.ok || k0 >= g.K) return g_conv_zero;
   const int c = k0 & (g.SC - 1);
   const int tap = k0 >> g.c_shift;
-  const int kh = tap / g.KW, kw = tap - kh * g.KW;
+  const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
   int ih, iw;
   if (!TRANSPOSED) {
     ih = p.oh * g.stride - g.pad + kh;
     iw = p.ow * g.stride - g.pad + kw;
   } else {
     const int th = p.oh + g.pad - kh, tw = p.ow + g.pad - kw;
-    if (th < 0 || tw < 0) return zero8();
-    if (g.stride == 1) {
-      ih = th; iw = tw;
-    } else {
-      ih = th / g.stride; iw = tw / g.stride;
-      if (ih * g.stride != th || iw * g.stride != tw) return zero8();
-    }
+    const int msk = (1 << g.s_shift) - 1;
+    if ((th | tw) < 0 || ((th | tw) & msk)) return g_conv_zero;
+    ih = th >> g.s_shift;
+    iw = tw >> g.s_shift;
   }
-  if ((unsigned)ih >= (unsigned)g.SH || (unsigned)iw >= (unsigned)g.SW) return zero8();
-  return ld8(g.src + (((long)p.n * g.SH + ih) * g.SW + iw) * g.SC + c);
+  if ((unsigned)ih >= (unsigned)g.SH || (unsigned)iw >= (unsigned)g.SW) return g_conv_zero;
+  return g.src + (((long)p.n * g.SH + ih) * g.SW + iw) * g.SC + c;
+}
+
+// Fast path when SC % 64 == 0: a 64-deep stage is 64 channels of ONE tap, so
+// (kh, kw, channel offset) are workgroup-uniform scalars and each lane only
+// offsets its row's precomputed pixel base.
+struct RowG {
+  long base;  // element offset of (n, ih0, iw0) [+ lane chunk], may be "negative" (padding)
+  int ih0, iw0;
+  bool ok;
+};
+
+template <bool TRANSPOSED>
+__device__ __forceinline__ RowG row_gather(const ConvGeom& g, const Pix& p, int chunk8) {
+  RowG r;
+  r.ok = p.ok;
+  if (!TRANSPOSED) {
+    r.ih0 = p.oh * g.stride - g.pad;
+    r.iw0 = p.ow * g.stride - g.pad;
+  } else {
+    r.ih0 = p.oh + g.pad;
+    r.iw0 = p.ow + g.pad;
+  }
+  r.base = (long)p.n * g.SH * g.SW * g.SC + chunk8;
+  return r;
+}
+
+template <bool TRANSPOSED>
+__device__ __forceinline__ const uint16_t* gather_tap(const ConvGeom& g, const RowG& r, int kh, int kw, int ch0) {
+  int ih, iw;
+  if (!TRANSPOSED) {
+    ih = r.ih0 + kh;
+    iw = r.iw0 + kw;
+  } else {
+    const int th = r.ih0 - kh, tw = r.iw0 - kw;
+    const int msk = (1 << g.s_shift) - 1;
+    if ((th | tw) < 0 || ((th | tw) & msk)) return g_conv_zero;
+    ih = th >> g.s_shift;
+    iw = tw >> g.s_shift;
+  }
+  if (!r.ok || (unsigned)ih >= (unsigned)g.SH || (unsigned)iw >= (unsigned)g.SW) return g_conv_zero;
+  return g.src + r.base + ((long)ih * g.SW + iw) * g.SC + ch0;
+}
+
+__device__ __forceinline__ void glds16(const void* src, SL_LDS void* dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, dst, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vmcnt_stages(int stages_after) {
+  // this wave's DMA pieces of the stage about to be read have landed once at
+  // most `stages_after` younger stages (N pieces each) remain outstanding
+  if (stages_after >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * N) : "memory");
+  else if (stages_after == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * N) : "memory");
+  else if (stages_after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ short8_t ds_b128(uint32_t a) {
+  short8_t r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ short4_t ds_tr16(uint32_t a) {
+  short4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
 }
 
 // ---------------------------------------------------------------------------
 // Forward / dgrad implicit GEMM.  256 threads = 2x2 waves; each wave owns a
-// (BM/2) x (BN/2) sub-tile = (BM/32) x (BN/32) MFMA 16x16 tiles.  LDS is
-// double buffered with register prefetch of the next stage (one barrier per
-// 64-deep stage).  Grid is XCD-remapped so the column tiles of one row panel
-// (which re-read the same gathered rows) share an L2.
+// (BM/2) x (BN/2) sub-tile = (BM/32) x (BN/32) MFMA 16x16 tiles.  Operand
+// images are [rows][64 k] bf16 (128-B rows); 16-B chunk c of row r sits at
+// position c ^ ((r >> 1) & 7), which makes the 16 rows of a fragment read hit
+// 16 distinct bank groups.  One DMA piece = 8 rows = 1 KB.
 // ---------------------------------------------------------------------------
-template <int BM, int BN, bool TRANSPOSED>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
+__device__ __forceinline__ int swz64(int c, int r) { return c ^ ((r >> 1) & 7); }
+
+template <int BM, int BN, bool TRANSPOSED, int NSLOT>
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
   constexpr int MT = BM / 32, NT = BN / 32;
-  constexpr int A_PER = BM * (BK / 8) / 256;  // 16-B chunks per thread per stage
-  constexpr int B_PER = BN * (BK / 8) / 256;
-  constexpr int STAGE = (BM + BN) * LDK;
+  constexpr int PA = BM / 32, PB = BN / 32;  // DMA pieces per wave per stage
+  constexpr int PS = PA + PB;
+  constexpr int SLOT = (BM + BN) * BK;       // elements
   constexpr int CS_LD = BN + 8;
-  constexpr int SMEM = 2 * STAGE > BM * CS_LD ? 2 * STAGE : BM * CS_LD;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
+  static_assert(BM * CS_LD <= NSLOT * SLOT, "epilogue tile must fit the ring");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSLOT * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
@@ -119,36 +208,65 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, ConvEpi e, i
   const int m0 = tm * BM, n0 = tn * BN;
   const int wm = wave >> 1, wn = wave & 1;
 
-  // staging assignment: chunk q = tid + i*256 -> row q>>3, k-chunk q&7
-  const int kc = (tid & 7) * 8;
-  Pix pa[A_PER];
+  // DMA map: piece j of this wave covers rows 8 (wave * P + j) .. +7; lane -> row + lane / 8,
+  // LDS position lane % 8 <- source chunk swz64(lane % 8, row).
+  Pix pa[PA];
+  int ca[PA];
+  RowG ra[PA];
 #pragma unroll
-  for (int i = 0; i < A_PER; ++i) pa[i] = decode_pix(g, m0 + (tid >> 3) + 32 * i);
-  const uint16_t* pb[B_PER];
-  bool bok[B_PER];
-#pragma unroll
-  for (int i = 0; i < B_PER; ++i) {
-    const int col = n0 + (tid >> 3) + 32 * i;
-    bok[i] = col < e.ncols;
-    pb[i] = e.w + (long)(bok[i] ? col : 0) * g.K;
+  for (int j = 0; j < PA; ++j) {
+    const int row = 8 * (wave * PA + j) + (lane >> 3);
+    pa[j] = decode_pix(g, m0 + row);
+    ca[j] = swz64(lane & 7, row);
+    ra[j] = row_gather<TRANSPOSED>(g, pa[j], ca[j] * 8);
   }
+  const bool uniform_tap = (g.SC & 63) == 0;
+  const int cps_shift = g.c_shift - 6;  // log2(stages per tap) on the fast path
+  const uint16_t* pb[PB];
+  int cb[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    const int row = 8 * (wave * PB + j) + (lane >> 3);
+    const int col = n0 + row;
+    pb[j] = col < e.ncols ? e.w + (long)col * g.K : nullptr;
+    cb[j] = swz64(lane & 7, row);
+  }
+  auto issue = [&](int kt) {
+    uint16_t* As = smem + (kt % NSLOT) * SLOT;
+    uint16_t* Bs = As + BM * BK;
+    if (uniform_tap) {
+      const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
+      const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
+#pragma unroll
+      for (int j = 0; j < PA; ++j)
+        glds16(gather_tap<TRANSPOSED>(g, ra[j], kh, kw, ch0), (SL_LDS void*)(As + (wave * PA + j) * 8 * BK));
+    } else {
+#pragma unroll
+      for (int j = 0; j < PA; ++j)
+        glds16(gather_src<TRANSPOSED>(g, pa[j], kt * BK + ca[j] * 8), (SL_LDS void*)(As + (wave * PA + j) * 8 * BK));
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int k0 = kt * BK + cb[j] * 8;
+      glds16((pb[j] && k0 < g.K) ? pb[j] + k0 : g_conv_zero, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK));
+    }
+  };
 
-  short8_t ra[A_PER], rb[B_PER];
-  auto load = [&](int kt) {
-    const int k0 = kt * BK + kc;
+  // per-lane fragment byte offsets (within a slot) for the two 32-deep halves
+  uint32_t aoff[MT][2], boff[NT][2];
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) ra[i] = gather8<TRANSPOSED>(g, pa[i], k0);
+  for (int i = 0; i < MT; ++i) {
+    const int r = wm * (BM / 2) + i * 16 + lr;
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) rb[i] = (bok[i] && k0 < g.K) ? ld8(pb[i] + k0) : zero8();
-  };
-  auto store = [&](int buf) {
-    uint16_t* As = smem + buf * STAGE;
-    uint16_t* Bs = As + BM * LDK;
+    for (int h = 0; h < 2; ++h) aoff[i][h] = (uint32_t)((r * BK + swz64(h * 4 + lg, r) * 8) * 2);
+  }
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) *reinterpret_cast<short8_t*>(As + ((tid >> 3) + 32 * i) * LDK + kc) = ra[i];
+  for (int j = 0; j < NT; ++j) {
+    const int r = wn * (BN / 2) + j * 16 + lr;
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) *reinterpret_cast<short8_t*>(Bs + ((tid >> 3) + 32 * i) * LDK + kc) = rb[i];
-  };
+    for (int h = 0; h < 2; ++h) boff[j][h] = (uint32_t)(((BM + r) * BK + swz64(h * 4 + lg, r) * 8) * 2);
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
 
   floatx4_t acc[MT][NT];
 #pragma unroll
@@ -157,31 +275,33 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, ConvEpi e, i
     for (int j = 0; j < NT; ++j) acc[i][j] = zero4();
 
   const int nk = (g.K + BK - 1) / BK;
-  load(0);
-  store(0);
-  __syncthreads();
+  for (int kt = 0; kt < NSLOT - 1 && kt < nk; ++kt) issue(kt);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load(kt + 1);
-    const uint16_t* As = smem + (kt & 1) * STAGE + (wm * (BM / 2) + lr) * LDK + 8 * lg;
-    const uint16_t* Bs = smem + (kt & 1) * STAGE + BM * LDK + (wn * (BN / 2) + lr) * LDK + 8 * lg;
+    vmcnt_stages<PS>(min(NSLOT - 2, nk - 1 - kt));
+    __builtin_amdgcn_s_barrier();  // stage kt visible; slot (kt - 1) % NSLOT free
+    if (kt + NSLOT - 1 < nk) issue(kt + NSLOT - 1);
+    const uint32_t sb = lds0 + (uint32_t)((kt % NSLOT) * SLOT * 2);
 #pragma unroll
-    for (int ks = 0; ks < BK; ks += 32) {
+    for (int h = 0; h < 2; ++h) {
       short8_t af[MT], bf[NT];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) af[i] = lds8(As + i * 16 * LDK + ks);
+      for (int i = 0; i < MT; ++i) af[i] = ds_b128(sb + aoff[i][h]);
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bf[j] = lds8(Bs + j * 16 * LDK + ks);
+      for (int j = 0; j < NT; ++j) bf[j] = ds_b128(sb + boff[j][h]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
     }
-    if (kt + 1 < nk) store((kt + 1) & 1);
-    __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   // ---- epilogue ----
   if (e.stats) {
+    float* rep = rsum_replica(e.stats, 2 * e.ncols);
     // per-column partial sums over this wave's rows (rows >= M are exact zeros)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -200,10 +320,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, ConvEpi e, i
       q += __shfl_xor(q, 32);
       const int col = n0 + wn * (BN / 2) + j * 16 + lr;
       if (lg == 0 && col < e.ncols) {
-        atomicAdd(e.stats + col, s);
-        atomicAdd(e.stats + e.ncols + col, q);
+        atomicAdd(rep + col, s);
+        atomicAdd(rep + e.ncols + col, q);
       }
     }
+    int* flag = reinterpret_cast<int*>(smem);  // ring is drained; reused as the last-arriver flag
+    rsum_finish(e.stats, 2 * e.ncols, flag);
+    __syncthreads();
   }
   if (e.yf) {
 #pragma unroll
@@ -259,29 +382,59 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, ConvEpi e, i
 
 // ---------------------------------------------------------------------------
 // Weight gradient.  Output tile BMO (co) x 128 (k); the batch*pixel index m is
-// the reduction, split into `slices` contiguous ranges (one per workgroup
-// row of the grid).  Per stage, 64 m-rows of dY [m][co] and of im2col(X)
-// [m][k] are staged as row-major LDS images and read transposed
-// (ds_read_b64_tr_b16) into A = dY^T and B = im2col(X) fragments.
+// the reduction, split into `slices` contiguous ranges.  Per stage, 64 m-rows
+// of dY [m][co] (BMO wide) and of im2col(X) [m][k] (128 wide) land as
+// row-major LDS images and are read transposed (ds_read_b64_tr_b16) into
+// A = dY^T and B = im2col(X) fragments.  Swizzle for a W-chunk row (W = 8 or
+// 16 chunks of 16 B): c ^ (f(r) << 1) with f mixing rows {k..k+3, k+8..k+11}
+// of each 32-lane tr-read group onto distinct bank groups.
 // ---------------------------------------------------------------------------
+template <int W>
+__device__ __forceinline__ int swz_tr(int c, int r) {
+  if (W == 16) return c ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1);
+  return c ^ ((((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1);
+}
+
+// byte offset (within an image of W-chunk rows) of this lane's first tr read
+// for the fragment at column n0 (elements); rows +4 -> +4*W*16 bytes, k0+32 -> +32*W*16
+template <int W>
+__device__ __forceinline__ uint32_t tr_off(int n0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int c = (n0 >> 3) + (p >> 1), w = (p & 1) * 4;
+  const int ra = 8 * g + q;
+  return (uint32_t)((ra * W * 8 + swz_tr<W>(c, ra) * 8 + w) * 2);
+}
+template <int W, int KOFF>
+__device__ __forceinline__ short8_t tr8(uint32_t a) {
+  const short4_t lo = ds_tr16<KOFF>(a);
+  const short4_t hi = ds_tr16<KOFF + 4 * W * 16>(a);
+  short8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
 struct WgradArgs {
   ConvGeom g;           // forward geometry: src = X, OH/OW = dY dims
   const uint16_t* dy;   // [M][ldy]
   int ldy, cout;
-  float* dw;            // [cout][K] fp32, accumulated atomically
+  float* dw;            // [cout][K] fp32, accumulated
   int tiles_k, tiles_co, slices, steps_per_slice;
 };
 
-template <int BMO>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+template <int BMO, int NSLOT>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   constexpr int BNO = 128;
-  constexpr int MT = BMO / 32, NT = BNO / 32;  // per-wave MFMA tiles (2x2 waves)
-  constexpr int DY_PER = WG_M * (BMO / 8) / 256;
-  constexpr int X_PER = WG_M * (BNO / 8) / 256;
-  constexpr int STAGE = WG_M * LDT * 2;  // dY image + X image
+  constexpr int WA = BMO / 8, WB = BNO / 8;       // 16-B chunks per image row
+  constexpr int MT = BMO / 32, NT = BNO / 32;     // per-wave MFMA tiles (2x2 waves)
+  constexpr int RA = 64 / WA, RB = 64 / WB;       // rows per 1-KB DMA piece
+  constexpr int PA = (WG_M / RA) / 4, PB = (WG_M / RB) / 4;  // pieces per wave per stage
+  constexpr int PS = PA + PB;
+  constexpr int IMG_A = WG_M * BMO, IMG_B = WG_M * BNO;      // elements
+  constexpr int SLOT = IMG_A + IMG_B;
   constexpr int OUT_LD = BNO + 4;
-  constexpr int SMEM_B = (2 * STAGE * 2 > BMO * OUT_LD * 4) ? 2 * STAGE * 2 : BMO * OUT_LD * 4;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_B / 2];
+  constexpr int SMEM = NSLOT * SLOT > BMO * OUT_LD * 2 ? NSLOT * SLOT : BMO * OUT_LD * 2;  // ring / fp32 epilogue
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
   const ConvGeom& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -294,40 +447,54 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   const int co0 = tco * BMO, k0 = tk * BNO;
   const int wm = wave >> 1, wn = wave & 1;
   const int mbeg = s * a.steps_per_slice * WG_M;
-  const int nsteps = min(a.steps_per_slice, (g.M - mbeg + WG_M - 1) / WG_M);
+  const int nst = min(a.steps_per_slice, (g.M - mbeg + WG_M - 1) / WG_M);
 
-  // staging: dY chunk q -> row q / (BMO/8), col chunk q % (BMO/8); X chunk q -> row q>>4, col chunk q&15
-  constexpr int DY_CPR = BMO / 8;
-  short8_t rdy[DY_PER], rx[X_PER];
-  auto load = [&](int st) {
+  // A (dY) pieces: row = RA * (wave * PA + j) + lane / WA, LDS chunk lane % WA
+  int arow[PA];
+  const uint16_t* acol[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    arow[j] = RA * (wave * PA + j) + lane / WA;
+    const int co = co0 + swz_tr<WA>(lane % WA, arow[j]) * 8;
+    acol[j] = co < a.ldy ? a.dy + co : nullptr;
+  }
+  // B (im2col) pieces: the k chunk (tap, channels) of each lane is fixed for the workgroup
+  int brow[PB], bkh[PB], bkw[PB], bch[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    brow[j] = RB * (wave * PB + j) + lane / WB;
+    const int kk = k0 + swz_tr<WB>(lane % WB, brow[j]) * 8;
+    const int tap = kk >> g.c_shift;
+    bkh[j] = kk < g.K ? (tap * g.kw_magic) >> 16 : -(1 << 20);  // k past K -> never in range
+    bkw[j] = tap - ((tap * g.kw_magic) >> 16) * g.KW;
+    bch[j] = kk & (g.SC - 1);
+  }
+  auto issue = [&](int st) {
+    uint16_t* Ai = smem + (st % NSLOT) * SLOT;
+    uint16_t* Bi = Ai + IMG_A;
     const int mb = mbeg + st * WG_M;
 #pragma unroll
-    for (int i = 0; i < DY_PER; ++i) {
-      const int q = tid + 256 * i;
-      const int row = mb + q / DY_CPR, co = co0 + (q % DY_CPR) * 8;
-      rdy[i] = (row < g.M && co < a.cout) ? ld8(a.dy + (long)row * a.ldy + co) : zero8();
+    for (int j = 0; j < PA; ++j) {
+      const int m = mb + arow[j];
+      glds16((acol[j] && m < g.M) ? acol[j] + (long)m * a.ldy : g_conv_zero,
+             (SL_LDS void*)(Ai + (wave * PA + j) * RA * BMO));
     }
 #pragma unroll
-    for (int i = 0; i < X_PER; ++i) {
-      const int q = tid + 256 * i;
-      const Pix p = decode_pix(g, mb + (q >> 4));
-      rx[i] = gather8<false>(g, p, k0 + (q & 15) * 8);
+    for (int j = 0; j < PB; ++j) {
+      const Pix p = decode_pix(g, mb + brow[j]);
+      const int ih = p.oh * g.stride - g.pad + bkh[j], iw = p.ow * g.stride - g.pad + bkw[j];
+      const bool ok = p.ok && (unsigned)ih < (unsigned)g.SH && (unsigned)iw < (unsigned)g.SW;
+      glds16(ok ? g.src + (((long)p.n * g.SH + ih) * g.SW + iw) * g.SC + bch[j] : g_conv_zero,
+             (SL_LDS void*)(Bi + (wave * PB + j) * RB * BNO));
     }
   };
-  auto store = [&](int buf) {
-    uint16_t* Ds = smem + buf * STAGE;
-    uint16_t* Xs = Ds + WG_M * LDT;
+
+  uint32_t aoff[MT], boff[NT];
 #pragma unroll
-    for (int i = 0; i < DY_PER; ++i) {
-      const int q = tid + 256 * i;
-      *reinterpret_cast<short8_t*>(Ds + (q / DY_CPR) * LDT + (q % DY_CPR) * 8) = rdy[i];
-    }
+  for (int i = 0; i < MT; ++i) aoff[i] = tr_off<WA>(wm * (BMO / 2) + i * 16, lane);
 #pragma unroll
-    for (int i = 0; i < X_PER; ++i) {
-      const int q = tid + 256 * i;
-      *reinterpret_cast<short8_t*>(Xs + (q >> 4) * LDT + (q & 15) * 8) = rx[i];
-    }
-  };
+  for (int j = 0; j < NT; ++j) boff[j] = (uint32_t)(IMG_A * 2) + tr_off<WB>(wn * (BNO / 2) + j * 16, lane);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
 
   floatx4_t acc[MT][NT];
 #pragma unroll
@@ -335,30 +502,31 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = zero4();
 
-  if (nsteps > 0) {
-    load(0);
-    store(0);
-    __syncthreads();
-    for (int st = 0; st < nsteps; ++st) {
-      if (st + 1 < nsteps) load(st + 1);
-      const uint16_t* Ds = smem + (st & 1) * STAGE;
-      const uint16_t* Xs = Ds + WG_M * LDT;
+  for (int st = 0; st < NSLOT - 1 && st < nst; ++st) issue(st);
+  for (int st = 0; st < nst; ++st) {
+    vmcnt_stages<PS>(min(NSLOT - 2, nst - 1 - st));
+    __builtin_amdgcn_s_barrier();
+    if (st + NSLOT - 1 < nst) issue(st + NSLOT - 1);
+    const uint32_t sb = lds0 + (uint32_t)((st % NSLOT) * SLOT * 2);
+    auto half = [&](auto kk) {
+      constexpr int H = decltype(kk)::value;
+      short8_t af[MT], bf[NT];
 #pragma unroll
-      for (int ks = 0; ks < WG_M; ks += 32) {
-        short8_t af[MT], bf[NT];
+      for (int i = 0; i < MT; ++i) af[i] = tr8<WA, H * 32 * WA * 16>(sb + aoff[i]);
 #pragma unroll
-        for (int i = 0; i < MT; ++i) af[i] = lds_tr8(Ds + ks * LDT + wm * (BMO / 2) + i * 16, LDT, lane);
+      for (int j = 0; j < NT; ++j) bf[j] = tr8<WB, H * 32 * WB * 16>(sb + boff[j]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < NT; ++j) bf[j] = lds_tr8(Xs + ks * LDT + wn * (BNO / 2) + j * 16, LDT, lane);
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-      }
-      if (st + 1 < nsteps) store((st + 1) & 1);
-      __syncthreads();
-    }
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+    };
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   // fp32 tile through LDS so each wave's atomics cover 256 contiguous bytes
   float* Os = reinterpret_cast<float*>(smem);
@@ -394,7 +562,7 @@ struct WtDesc {
 };
 
 // One workgroup per 64 (co) x 64 (ci) tile of one tap of one conv, through
-// LDS: coalesced 16-B reads along ci, coalesced writes along co.
+// LDS: coalesced reads along ci, coalesced writes along co.
 __global__ __launch_bounds__(256) void conv_wt_kernel(const WtDesc* __restrict__ d, int nd, long total) {
   __shared__ uint16_t tile[64][66];
   const long b = blockIdx.x;
@@ -438,9 +606,12 @@ static int fill_geom(ConvGeom& g, const uint16_t* src, int N, int SH, int SW, in
                      int stride, int pad) {
   g.src = src; g.N = N; g.SH = SH; g.SW = SW; g.SC = SC; g.c_shift = ilog2(SC);
   g.OH = OH; g.OW = OW; g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  g.hw_shift = ilog2(OH * OW); g.w_shift = ilog2(OW);
+  g.kw_magic = (65536 + KW - 1) / KW;  // exact for tap < 65536 / KW^2 (taps here <= 49)
+  g.s_shift = ilog2(stride);
   g.K = KH * KW * SC;
   const long M = (long)N * OH * OW;
-  if (g.c_shift < 3 || M <= 0 || M > (1L << 30) || stride < 1) return -1;
+  if (g.c_shift < 3 || M <= 0 || M > (1L << 30) || g.s_shift < 0 || OH <= 0 || OW <= 0 || KH * KW > 64) return -1;
   g.M = (int)M;
   return 0;
 }
@@ -448,14 +619,18 @@ static int fill_geom(ConvGeom& g, const uint16_t* src, int N, int SH, int SW, in
 template <bool T>
 static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) {
   const bool small_n = e.ncols <= 64;
-  const bool small_m = g.M <= 16384;
+  // two workgroups per CU: prefer 128-row tiles while they still give >= 2
+  // rounds of workgroups over the 512 slots
+  const int tn128 = (e.ncols + (small_n ? 63 : 127)) / (small_n ? 64 : 128);
+  const bool small_m = (long)((g.M + 127) / 128) * tn128 < 1024;
   const int BMv = small_m ? 64 : 128, BNv = small_n ? 64 : 128;
   const int tiles_m = (g.M + BMv - 1) / BMv, tiles_n = (e.ncols + BNv - 1) / BNv;
   dim3 grid(tiles_m * tiles_n), block(256);
-  if (BMv == 128 && BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 128, T>), grid, block, 0, stream, g, e, tiles_n);
-  else if (BMv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 64, T>), grid, block, 0, stream, g, e, tiles_n);
-  else if (BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<64, 128, T>), grid, block, 0, stream, g, e, tiles_n);
-  else hipLaunchKernelGGL((conv_gemm_kernel<64, 64, T>), grid, block, 0, stream, g, e, tiles_n);
+  // LDS ring sized for two workgroups per CU (<= 72 KB each)
+  if (BMv == 128 && BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 128, T, 2>), grid, block, 0, stream, g, e, tiles_n);
+  else if (BMv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 64, T, 3>), grid, block, 0, stream, g, e, tiles_n);
+  else if (BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<64, 128, T, 3>), grid, block, 0, stream, g, e, tiles_n);
+  else hipLaunchKernelGGL((conv_gemm_kernel<64, 64, T, 4>), grid, block, 0, stream, g, e, tiles_n);
   SL_CHECK_LAUNCH();
   return 0;
 }
@@ -469,6 +644,7 @@ int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w
   ConvGeom g;
   if (fill_geom(g, x, N, H, W, C, OH, OW, KH, KW, stride, pad)) return -1;
   if (y && (ldy < cout || (ldy & 7))) return -2;
+  if ((g.K & 7) || (((uintptr_t)x | (uintptr_t)w) & 15)) return -3;
   ConvEpi e{w, cout, y, ldy, yf, bias, nullptr, stats};
   return launch_gemm<false>(g, e, stream);
 }
@@ -480,6 +656,7 @@ int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint
   ConvGeom g;
   if (fill_geom(g, dy, N, OH, OW, ldd, H, W, KH, KW, stride, pad)) return -1;
   if (cin & 7) return -2;
+  if (((uintptr_t)dy | (uintptr_t)wt) & 15) return -3;
   ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr};
   return launch_gemm<true>(g, e, stream);
 }
@@ -491,21 +668,22 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   WgradArgs a;
   if (fill_geom(a.g, x, N, H, W, C, OH, OW, KH, KW, stride, pad)) return -1;
   if ((ldy & 7) || ldy < cout) return -2;
+  if (((uintptr_t)x | (uintptr_t)dy) & 15) return -3;
   a.dy = dy; a.ldy = ldy; a.cout = cout; a.dw = dw;
   const int BMO = cout <= 64 ? 64 : 128;
   a.tiles_co = (cout + BMO - 1) / BMO;
   a.tiles_k = (a.g.K + 127) / 128;
   const int tiles = a.tiles_co * a.tiles_k;
   const int total_steps = (a.g.M + WG_M - 1) / WG_M;
-  if (target_wgs <= 0) target_wgs = 1024;
-  int slices = (target_wgs + tiles - 1) / tiles;
+  if (target_wgs <= 0) target_wgs = 512;  // two workgroups per CU (64-72 KB LDS ring each)
+  int slices = tiles >= target_wgs / 2 ? 1 : (target_wgs + tiles - 1) / tiles;
   if (slices > total_steps) slices = total_steps;
   if (slices < 1) slices = 1;
   a.steps_per_slice = (total_steps + slices - 1) / slices;
   a.slices = (total_steps + a.steps_per_slice - 1) / a.steps_per_slice;
   dim3 grid(tiles * a.slices), block(256);
-  if (BMO == 64) hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, block, 0, stream, a);
-  else hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, block, 0, stream, a);
+  if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3>), grid, block, 0, stream, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<128, 2>), grid, block, 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }

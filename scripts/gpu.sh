@@ -4,11 +4,11 @@
 # usage: scripts/gpu.sh <timeout_s> <command...>
 t=$1; shift
 rm -f gpurun_out/*.log
-for attempt in 1 2 3 4; do
+for attempt in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun --timeout "$t" -- "$@"
   rc=$?
   st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('status',''))" 2>/dev/null)
-  if [ "$rc" = "3" ] || [ "$st" = "transient" ]; then echo "[gpu.sh] transient ($st rc=$rc), retry in 30s"; sleep 30; continue; fi
+  if [ "$rc" = "3" ] || [ "$st" = "transient" ]; then echo "[gpu.sh] transient ($st rc=$rc), retry in 60s"; sleep 60; continue; fi
   exit $rc
 done
 exit $rc

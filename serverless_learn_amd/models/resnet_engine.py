@@ -33,15 +33,23 @@ LOGIT_LD = 16  # dlogits row stride (classes padded for 16-B gathers)
 
 
 class _BN:
-    def __init__(self, spec: BNSpec, params, grad, arena, off, dev):
+    """Per-BatchNorm buffers.  ``stats_buf``/``sums_buf`` are cross-workgroup sum
+    buffers (replicas | result | ticket, csrc/kernels/common.h rsum_*) living in
+    the per-step zeroed arena; ``stats``/``sums`` are their folded results."""
+
+    def __init__(self, spec: BNSpec, params, grad, arena, off, dev, rs):
+        from ..ops import cnn as K
+
         c = spec.c
         self.spec = spec
         self.gamma = params[spec.g_off:spec.g_off + c]
         self.beta = params[spec.b_off:spec.b_off + c]
         self.ggamma = grad[spec.g_off:spec.g_off + c]
         self.gbeta = grad[spec.b_off:spec.b_off + c]
-        self.stats = arena[off:off + 2 * c]
-        self.sums = arena[off + 2 * c:off + 4 * c]
+        self.stats_buf = arena[off:off + rs]
+        self.sums_buf = arena[off + rs:off + 2 * rs]
+        self.stats = K.rsum_result(self.stats_buf, 2 * c)
+        self.sums = K.rsum_result(self.sums_buf, 2 * c)
         self.coef = torch.zeros(4 * c, device=dev)
         self.dcoef = torch.zeros(3 * c, device=dev)
         self.run_mean = torch.zeros(c, device=dev)
@@ -82,12 +90,13 @@ class FusedResNetTrainer:
         self.grad = torch.zeros_like(self.params)
         self.shadow = torch.zeros(n, dtype=torch.bfloat16, device=dev)
         bns = list(spec.bns())
-        self.arena = torch.zeros(sum(4 * b.c for b in bns), device=dev)
+        rsz = {b.name: (K.rsum_floats(2 * b.c) + 3) // 4 * 4 for b in bns}  # 16-B aligned regions
+        self.arena = torch.zeros(sum(2 * rsz[b.name] for b in bns), device=dev)
         off = 0
         self.bn = {}
         for b in bns:
-            self.bn[b.name] = _BN(b, self.params, self.grad, self.arena, off, dev)
-            off += 4 * b.c
+            self.bn[b.name] = _BN(b, self.params, self.grad, self.arena, off, dev, rsz[b.name])
+            off += 2 * rsz[b.name]
         self.conv = {c.name: _Conv(c, self.params, self.shadow, self.grad, dev) for c in spec.convs()}
         self.fc_w = self.shadow[spec.fc_w:spec.fc_w + classes * 512]
         self.fc_b = self.params[spec.fc_b:spec.fc_b + classes]
@@ -187,7 +196,7 @@ class FusedResNetTrainer:
     def _conv_bn(self, x, conv: _Conv, bn: _BN, out):
         K = self.K
         c = conv.spec
-        K.conv_fwd(x, conv.w, c.cout, c.k, c.stride, c.pad, y=out, stats=bn.stats)
+        K.conv_fwd(x, conv.w, c.cout, c.k, c.stride, c.pad, y=out, stats=bn.stats_buf)
 
     def forward(self, train: bool = True):
         K, spec = self.K, self.spec
@@ -239,11 +248,11 @@ class FusedResNetTrainer:
             c1, c2 = self.conv[blk.conv1.name], self.conv[blk.conv2.name]
             b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
             # y = relu(bn2(c2) + sc): dz = dy * 1[y > 0] feeds bn2 and the shortcut
-            K.bn_bwd_reduce(dy, st["y"], st["c2"], b2.sums, dz_out=st["dz"])
+            K.bn_bwd_reduce(dy, st["y"], st["c2"], b2.sums_buf, dz_out=st["dz"])
             add = st["dz"]
             if blk.down is not None:
                 cd, bd = self.conv[blk.down.name], self.bn[blk.dbn.name]
-                K.bn_bwd_reduce(st["dz"], None, st["cs"], bd.sums)
+                K.bn_bwd_reduce(st["dz"], None, st["cs"], bd.sums_buf)
                 K.bn_bwd_apply_sums(st["dz"], None, st["cs"], bd.sums, bd.coef, bd.ggamma, bd.gbeta, st["dcs"])
                 K.conv_wgrad(st["x"], st["dcs"], blk.down.cout, 1, blk.down.stride, 0, cd.g)
                 K.conv_dgrad(st["dcs"], cd.wt, blk.down.cin, 1, blk.down.stride, 0, st["dxs"])
@@ -251,7 +260,7 @@ class FusedResNetTrainer:
             K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
             K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g)
             K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"])
-            K.bn_bwd_reduce(st["da1"], st["a1"], st["c1"], b1.sums)
+            K.bn_bwd_reduce(st["da1"], st["a1"], st["c1"], b1.sums_buf)
             K.bn_bwd_apply_sums(st["da1"], st["a1"], st["c1"], b1.sums, b1.coef, b1.ggamma, b1.gbeta, st["dc1"])
             K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g)
             K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, st["dx"], add=add)
@@ -262,7 +271,7 @@ class FusedResNetTrainer:
         if spec.stem == "imagenet":
             K.maxpool_bwd(dy, self.p0_arg, self.da0)
             dy = self.da0
-        K.bn_bwd_reduce(dy, self.a0, self.c0, sbn.sums)
+        K.bn_bwd_reduce(dy, self.a0, self.c0, sbn.sums_buf)
         K.bn_bwd_apply_sums(dy, self.a0, self.c0, sbn.sums, sbn.coef, sbn.ggamma, sbn.gbeta, self.dc0)
         sc = spec.stem_conv
         K.conv_wgrad(self.x0, self.dc0, 64, sc.k, sc.stride, sc.pad, self.conv["stem"].g)

@@ -27,6 +27,8 @@ N.register("sl_bn_apply", [P, P, P, P, P, L, I, I, I, P])
 N.register("sl_bn_bwd_reduce", [P, P, P, P, P, L, I, P])
 N.register("sl_bn_bwd_finalize", [P, P, P, P, P, I, F, P])
 N.register("sl_bn_bwd_apply", [P, P, P, P, P, L, I, P])
+N.register("sl_rsum_floats", [I], ctypes.c_long)
+N.register("sl_rsum_result_offset", [I], ctypes.c_long)
 N.register("sl_bn_apply_stats", [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, F, F, F, P])
 N.register("sl_bn_bwd_apply_sums", [P, P, P, P, P, P, P, P, L, I, F, P])
 N.register("sl_maxpool_fwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
@@ -48,6 +50,17 @@ def _f32(t):
         return None
     assert t.dtype == torch.float32 and t.is_contiguous()
     return p(t)
+
+
+def rsum_floats(n: int) -> int:
+    """Size of a cross-workgroup sum buffer for n values (replicas | result | ticket)."""
+    return int(N.lib().sl_rsum_floats(n))
+
+
+def rsum_result(buf: torch.Tensor, n: int) -> torch.Tensor:
+    """The folded result (n floats) inside an rsum buffer."""
+    off = int(N.lib().sl_rsum_result_offset(n))
+    return buf[off:off + n]
 
 
 def out_size(h: int, k: int, s: int, pad: int) -> int:

@@ -48,8 +48,9 @@ def test_conv_fwd_dgrad_wgrad(case):
     ldy = (cout + 7) // 8 * 8
     y = torch.zeros(n, oh, oh, ldy, dtype=torch.bfloat16, device=DEV)
     yf = torch.zeros(n * oh * oh, cout, device=DEV)
-    stats = torch.zeros(2 * cout, device=DEV)
-    K.conv_fwd(x, w, cout, k, s, p, y=y, yf=yf, stats=stats)
+    sbuf = torch.zeros(K.rsum_floats(2 * cout), device=DEV)
+    K.conv_fwd(x, w, cout, k, s, p, y=y, yf=yf, stats=sbuf)
+    stats = K.rsum_result(sbuf, 2 * cout)
     torch.cuda.synchronize()
     assert rel(yf.view(n, oh, oh, cout), ref) < 1e-2
     assert rel(y[..., :cout], ref) < 1.5e-2
@@ -78,6 +79,38 @@ def test_conv_fwd_dgrad_wgrad(case):
     torch.cuda.synchronize()
     assert rel(dx.float() - add.float(), dx_ref) < 2e-2
     assert rel(dw, dw_ref) < 1e-2
+
+
+def test_stats_fold_fresh_across_repeated_launches():
+    """The cross-workgroup statistics fold (replicas + last-arriver) must see this
+    launch's values, not lines cached by an earlier launch's fold: run the conv
+    epilogue and the BN reduce repeatedly on changing inputs, re-zeroing the
+    buffer in between as the engine does, and check every round."""
+    from serverless_learn_amd.ops import cnn as K
+
+    n, h, c = 16, 16, 64
+    w = bf(torch.randn(c, 3, 3, c, device=DEV) / 24)
+    sbuf = torch.zeros(K.rsum_floats(2 * c), device=DEV)
+    rbuf = torch.zeros(K.rsum_floats(2 * c), device=DEV)
+    y = torch.empty(n, h, h, c, dtype=torch.bfloat16, device=DEV)
+    for it in range(6):
+        torch.manual_seed(100 + it)
+        x = bf(torch.randn(n, h, h, c, device=DEV) * (1 + it))
+        sbuf.zero_()
+        rbuf.zero_()
+        K.conv_fwd(x, w, c, 3, 1, 1, y=y, stats=sbuf)
+        dy = bf(torch.randn_like(y.float()))
+        K.bn_bwd_reduce(dy, None, y, rbuf)
+        ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1)
+        r2 = ref.permute(0, 2, 3, 1).reshape(-1, c)
+        st = K.rsum_result(sbuf, 2 * c)
+        su = K.rsum_result(rbuf, 2 * c)
+        torch.cuda.synchronize()
+        assert rel(st[:c], r2.sum(0)) < 1e-2, it
+        assert rel(st[c:], (r2 * r2).sum(0)) < 1e-2, it
+        yf, df = y.float().reshape(-1, c), dy.float().reshape(-1, c)
+        assert rel(su[:c], df.sum(0)) < 1e-3, it
+        assert rel(su[c:], (df * yf).sum(0)) < 1e-3, it
 
 
 def test_weight_transposer_matches_permute():
@@ -123,9 +156,10 @@ def test_bn_forward_backward_matches_torch():
 
     dy = bf(torch.randn_like(ref).permute(0, 2, 3, 1).contiguous())
     ref.backward(dy.float().permute(0, 3, 1, 2))
-    sums = torch.zeros(2 * c, device=DEV)
+    sbuf = torch.zeros(K.rsum_floats(2 * c), device=DEV)
     dz = torch.empty_like(x)
-    K.bn_bwd_reduce(dy, y, x, sums, dz_out=dz)
+    K.bn_bwd_reduce(dy, y, x, sbuf, dz_out=dz)
+    sums = K.rsum_result(sbuf, 2 * c)
     dcoef = torch.zeros(3 * c, device=DEV)
     gg, gb = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
     K.bn_bwd_finalize(sums, coef, dcoef, gg, gb, xf.shape[0])
