@@ -338,3 +338,44 @@ def test_resnet_engine_trains_and_graph_replays():
     last = tr.stats()
     assert math.isfinite(last.loss) and last.loss < first, (first, last)
     assert int(tr.cursor.item()) == 32  # 1 eager + 1 capture warmup + 30 replays (capture itself runs nothing)
+
+
+def test_resnet_bucketed_allreduce_hooks_cover_gradient_before_update():
+    """Bucket hooks fire during backward on disjoint ranges that tile the whole
+    flat gradient in reverse layout order, and the optimizer consumes what the
+    hooks leave behind: a hook that zeroes its bucket turns the step into pure
+    weight decay (deterministic, unlike atomics-order-dependent gradients)."""
+    from serverless_learn_amd.data.synthetic import make_cifar_like
+    from serverless_learn_amd.models.resnet_engine import FusedResNetTrainer
+
+    x, y = make_cifar_like(64, seed=8)
+    lr, wd = 0.1, 5e-4
+    b = FusedResNetTrainer(batch=32, device=DEV, seed=2, lr=lr, momentum=0.9, weight_decay=wd, world_size=2)
+    base = b.grad.data_ptr()
+    calls = []
+
+    class _H:
+        def wait(self):
+            calls.append("wait")
+
+    def hook(view):
+        calls.append(((view.data_ptr() - base) // 4, view.numel()))
+        view.zero_()
+        return _H()
+
+    b.bucket_bytes = 4 << 20
+    b.bucket_hook = hook
+    b.bucket_wait = lambda hs: [h.wait() for h in hs]
+    b.load_shard(torch.from_numpy(x), torch.from_numpy(y))
+    p0 = b.params.clone()
+    b.step()
+    torch.cuda.synchronize()
+    ranges = [c for c in calls if c != "wait"]
+    assert len(ranges) >= 4 and calls.count("wait") == len(ranges)
+    end = b.spec.n_flat
+    for off, n in ranges:  # contiguous, descending, covering [0, n_flat)
+        assert off + n == end, (off, n, end)
+        end = off
+    assert end == 0
+    expect = p0 - lr * (wd * p0)
+    assert torch.allclose(b.params, expect, rtol=1e-6, atol=1e-7)

@@ -99,3 +99,21 @@ def test_graph_replay_equals_eager():
         b.step()
     torch.cuda.synchronize()
     assert torch.equal(a.get_flat(), b.get_flat())
+
+
+def test_allreduce_hook_path_matches_single_rank():
+    """The eager data-parallel step (reduce -> all-reduce hook -> update) with a
+    simulated 2-rank all-reduce of identical replicas equals one rank's step."""
+    batch = 512
+    x, y = _data(batch * 2, seed=21)
+    flat = M.init_params(5)
+    a = M.FusedMLPTrainer(batch=batch, flat=flat)
+    b = M.FusedMLPTrainer(batch=batch, flat=flat, world_size=2)
+    b.allreduce = lambda g: g.mul_(2.0)  # sum over two identical ranks
+    a.load_shard(x, y)
+    b.load_shard(x, y)
+    for _ in range(3):
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.allclose(a.get_flat(), b.get_flat(), rtol=1e-5, atol=1e-6)
