@@ -57,11 +57,11 @@ IngestRing::~IngestRing() {
   } catch (...) {
   }
   for (int i = 0; i < nslots_; ++i) {
-    if (device_ >= 0 && events_[i]) hipEventDestroy((hipEvent_t)events_[i]);
-    if (pinned_) hipHostFree(slots_[i]);
+    if (device_ >= 0 && events_[i]) (void)hipEventDestroy((hipEvent_t)events_[i]);
+    if (pinned_) (void)hipHostFree(slots_[i]);
     else std::free(slots_[i]);
   }
-  if (stream_) hipStreamDestroy((hipStream_t)stream_);
+  if (stream_) (void)hipStreamDestroy((hipStream_t)stream_);
 }
 
 void IngestRing::wait_slot(int s) {
