@@ -55,6 +55,9 @@ def parse(argv=None):
                     help="grpc: file server -> ReceiveFile -> pinned ring -> HBM; local: host-generated shard; "
                          "device: shard synthesised in HBM by the Philox kernel (K8)")
     ap.add_argument("--bucket-mb", type=float, default=16.0, help="CNN all-reduce bucket size")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (= RCCL over xGMI, the production path); gloo only to rehearse several ranks "
+                         "sharing one GPU (RCCL refuses duplicate devices)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     mlp = a.model == "mlp"
@@ -80,11 +83,15 @@ def main(argv=None) -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    local_dev = local_rank % max(1, torch.cuda.device_count()) if args.dist_backend == "gloo" else local_rank
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     mlp = args.model == "mlp"
     dataset = "synthetic-mnist" if mlp else "synthetic-cifar"
@@ -188,6 +195,7 @@ def main(argv=None) -> int:
             "optimizer": f"sgd(lr={args.lr}, momentum={args.momentum}) fp32 master",
             "hipgraph": use_graph,
             "ingest": args.ingest,
+            "collective_backend": ("rccl" if args.dist_backend == "nccl" else "gloo") if world > 1 else None,
         },
         "baseline_note": "reference publishes no number; vs_baseline is vs its derived data-delivery "
                          "ceiling of 25,478 samples/s/worker (BASELINE.md)",

@@ -1,0 +1,133 @@
+"""CPU unit tests of the pure-Python pieces: gossip math,
+checkpoint format (§5.4), fault-injection rules and tracing (§5.1/§5.3), and
+config defaults (§5.6 -- every default equals the reference constant)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from serverless_learn_amd.ckpt import format as ckpt
+from serverless_learn_amd.config import Config
+from serverless_learn_amd.parallel.gossip import GossipState, exact_exchange
+from serverless_learn_amd.utils.fault import FaultInjector
+
+
+def _pair(rng, n):
+    mA, oA, mB, oB = (rng.standard_normal(n) for _ in range(4))
+    return mA, oA, mB, oB
+
+
+@pytest.mark.parametrize("compat", [True, False])
+def test_gossip_exchange_matches_closed_form(compat):
+    rng = np.random.default_rng(0)
+    mA, oA, mB, oB = _pair(rng, 37)
+    A = GossipState(torch.from_numpy(mA.copy()), alpha=0.5, compat=compat)
+    A.old = torch.from_numpy(oA.copy())
+    B = GossipState(torch.from_numpy(mB.copy()), alpha=0.5, compat=compat)
+    B.old = torch.from_numpy(oB.copy())
+    d = A.make_delta()
+    r = B.serve(d)
+    A.absorb(r, d)
+    mA2, oA2, mB2, oB2, r_ref = exact_exchange(mA, oA, mB, oB, 0.5, compat=compat)
+    np.testing.assert_allclose(r, r_ref, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(B.model.numpy(), mB2, atol=1e-12)
+    np.testing.assert_allclose(B.old.numpy(), oB2, atol=1e-12)
+    np.testing.assert_allclose(A.model.numpy(), mA2, atol=1e-12)
+    np.testing.assert_allclose(A.old.numpy(), oA2, atol=1e-12)
+
+
+def test_gossip_compat_has_alpha_squared_echo():
+    # only A made progress: dA = 1, dB = 0 -> compat A ends at mA + a^2 dA, echo-free at mA
+    mA, oA = np.ones(4), np.zeros(4)
+    mB, oB = np.zeros(4), np.zeros(4)
+    c = exact_exchange(mA, oA, mB, oB, 0.5, compat=True)[0]
+    e = exact_exchange(mA, oA, mB, oB, 0.5, compat=False)[0]
+    np.testing.assert_allclose(c, 1.25)
+    np.testing.assert_allclose(e, 1.0)
+
+
+def test_gossip_growable_vector_grows_with_zeros():
+    # reference worker.cc:85-89: a shorter model grows to the incoming length
+    B = GossipState(torch.zeros(2, dtype=torch.float64), growable=True)
+    r = B.serve(np.array([2.0, 2.0, 2.0, 2.0]))
+    np.testing.assert_allclose(r, [1.0, 1.0, 1.0, 1.0])
+    assert B.model.numel() == 4
+    fixed = GossipState(torch.zeros(2, dtype=torch.float64))
+    with pytest.raises(ValueError):
+        fixed.serve(np.ones(3))
+
+
+def test_checkpoint_roundtrip_and_update_compat():
+    from serverless_learn_amd.wire.codec import decode_update
+
+    rng = np.random.default_rng(1)
+    p = rng.standard_normal(1000).astype(np.float32)
+    m = rng.standard_normal(1000).astype(np.float32)
+    buf = ckpt.encode(p, {"model": "mlp", "step": 7, "epoch": 3}, momentum=m)
+    assert ckpt.looks_like_checkpoint(buf)
+    meta, p2, m2 = ckpt.decode(buf)
+    assert meta["step"] == 7 and meta["epoch"] == 3 and meta["n_params"] == 1000
+    np.testing.assert_array_equal(p2, p)
+    np.testing.assert_array_equal(m2, m)
+    # the parameter section is a plain serialized Update{repeated double delta}
+    mlen = int.from_bytes(buf[12:16], "little")
+    pos = 16 + mlen
+    n = int.from_bytes(buf[pos:pos + 8], "little")
+    np.testing.assert_array_equal(decode_update(bytes(buf[pos + 8:pos + 8 + n]), "float32"), p)
+    meta, p3, m3 = ckpt.decode(ckpt.encode(p, {"model": "mlp"}))
+    assert m3 is None
+    with pytest.raises(ValueError):
+        ckpt.decode(b"NOTACKPT" + bytes(8))
+    assert ckpt.is_checkpoint_file(ckpt.CKPT_BASE) and not ckpt.is_checkpoint_file(0)
+
+
+def test_fault_rules_parse_and_wrap():
+    fi = FaultInjector("kill:step=5; drop:CheckUp:p=1; delay:ExchangeUpdates:ms=1; hang:ReceiveFile")
+    assert fi.kill_step == 5 and fi.active
+    assert fi.drop == {"CheckUp": 1.0} and fi.delay == {"ExchangeUpdates": 0.001}
+    assert fi.hang == {"ReceiveFile"}
+    f = lambda req, ctx: "ok"  # noqa: E731
+    assert fi.wrap("RegisterBirth", f) is f
+
+    class Ctx:
+        def abort(self, code, msg):
+            raise RuntimeError(msg)
+
+    with pytest.raises(RuntimeError):
+        fi.wrap("CheckUp", f)(None, Ctx())
+    assert fi.wrap("ExchangeUpdates", f)(None, Ctx()) == "ok"
+    with pytest.raises(ValueError):
+        FaultInjector("explode:now")
+    assert not FaultInjector("").active
+
+
+def test_trace_spans_to_chrome_json(tmp_path, monkeypatch):
+    from serverless_learn_amd.utils import trace
+
+    monkeypatch.setattr(trace, "_path", str(tmp_path / "t.json"))
+    monkeypatch.setattr(trace, "_events", [])
+    with trace.span("step", step=1):
+        pass
+    trace.counter("samples_per_s", v=1.0)
+    trace.flush()
+    ev = json.load(open(tmp_path / "t.json"))["traceEvents"]
+    assert [e["ph"] for e in ev] == ["X", "C"] and ev[0]["name"] == "step" and ev[0]["args"] == {"step": 1}
+
+
+def test_config_defaults_equal_reference_constants(monkeypatch):
+    for k in list(__import__("os").environ):
+        if k.startswith("SL_"):
+            monkeypatch.delenv(k)
+    c = Config.from_env()
+    assert c.master_addr == "localhost:50052"            # serverless_learn.h:5
+    assert c.file_server_addr == "localhost:50053"       # serverless_learn.h:8
+    assert c.gossip_interval_ms == 5000                  # serverless_learn.h:10
+    assert c.simulated_train_interval_ms == 2000         # serverless_learn.h:12
+    assert c.push_interval_ms == 5000 and c.checkup_interval_ms == 5000  # master.cc:43,46
+    assert c.learn_rate == 0.5                           # master.cc:60
+    assert c.chunk_size == 1_000_000 and c.dummy_file_length == 100_000_000  # file_server.cc:40,46
+    monkeypatch.setenv("SL_GOSSIP_INTERVAL_MS", "250")
+    monkeypatch.setenv("SL_GOSSIP_COMPAT", "true")
+    c = Config.from_env()
+    assert c.gossip_interval == 0.25 and c.gossip_compat is True
