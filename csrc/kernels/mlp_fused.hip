@@ -458,7 +458,8 @@ __device__ __forceinline__ void wg_vmcnt(int n) {
 
 __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_NSLOT * WG_SLOT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int s = logical / A.total_tiles;
@@ -520,34 +521,46 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
   for (int j = 0; j < 4; ++j) b_addr[j] = wg_tr_addr(wn * 64 + j * 16, lane);
 
   for (int st = 0; st < 3 && st < nst; ++st) issue(st);
-  for (int st = 0; st < nst; ++st) {
-    wg_vmcnt(8 * min(2, nst - 1 - st));  // this wave's pieces of stage st have landed
-    __builtin_amdgcn_s_barrier();        // ... everyone's have; slot (st+3)%4 is free
-    if (st + 3 < nst) issue(st + 3);
-    if (m_live) {
-      const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
-      auto kstep = [&](auto koff) {
-        constexpr int KO = decltype(koff)::value;
-        short8_t af[4], bf[4];
+  // The main loop is instantiated per (live, bias) combination and selected by a
+  // scalar branch OUTSIDE it: with the conditions inside, hipcc treated them as
+  // divergent and copied all 64 accumulators AGPR<->VGPR on every stage
+  // (133 extra VALU per stage, measured in profiles/r01_v6).
+  auto mainloop = [&](auto live_c, auto bias_c) {
+    constexpr bool LIVE = decltype(live_c)::value, BIAS = decltype(bias_c)::value;
+    for (int st = 0; st < nst; ++st) {
+      wg_vmcnt(8 * min(2, nst - 1 - st));  // this wave's pieces of stage st have landed
+      __builtin_amdgcn_s_barrier();        // ... everyone's have; slot (st+3)%4 is free
+      if (st + 3 < nst) issue(st + 3);
+      if constexpr (LIVE) {
+        const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
+        auto kstep = [&](auto koff) {
+          constexpr int KO = decltype(koff)::value;
+          short8_t af[4], bf[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = wg_tr8<KO>(sb + a_addr[i]);
+          for (int i = 0; i < 4; ++i) af[i] = wg_tr8<KO>(sb + a_addr[i]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = wg_tr8<KO + WG_IMG * 2>(sb + b_addr[j]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
+          for (int j = 0; j < 4; ++j) bf[j] = wg_tr8<KO + WG_IMG * 2>(sb + b_addr[j]);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-        if (do_bias) {
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+          if constexpr (BIAS) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) accb[i] = mfma16(af[i], ones, accb[i]);
-        }
-      };
-      kstep(std::integral_constant<int, 0>{});
-      kstep(std::integral_constant<int, 32 * 128 * 2>{});
+            for (int i = 0; i < 4; ++i) accb[i] = mfma16(af[i], ones, accb[i]);
+          }
+        };
+        kstep(std::integral_constant<int, 0>{});
+        kstep(std::integral_constant<int, 32 * 128 * 2>{});
+      }
     }
-  }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (!m_live) mainloop(F_{}, F_{});
+  else if (do_bias) mainloop(T_{}, T_{});
+  else mainloop(T_{}, F_{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
