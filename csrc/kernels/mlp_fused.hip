@@ -39,13 +39,10 @@ constexpr int NCHUNK = D_INP / 64;
 constexpr int HID = 256;
 constexpr int NC = 10;
 constexpr int DZ_COLS = 16;  // dZ row stride in global memory
-constexpr int BM = 64;       // batch rows per workgroup
+constexpr int BM = 64;       // batch rows granularity (the rows kernel runs 64 or 128 per workgroup)
 constexpr int HS_LD = 264;   // [64][256] bf16 LDS images: 528-B rows
 constexpr int XC_LD = 72;    // X chunk image rows: 64 k + 8 pad = 144 B (ds_read_b128 conflict-free)
 constexpr int DZ_LD = 40;
-constexpr int REG = BM * HS_LD;  // one LDS region (elements) = 33,792 B
-static_assert(2 * BM * XC_LD <= REG, "X ring must fit region 0");
-constexpr int XN_LD = 896;       // normalised-X row stride (7 column tiles of 128 for K_wgrad)
 constexpr int KS1 = D_INP / 32, KS2 = HID / 32;  // 32-deep k-steps of layer 1 / of 256-wide layers
 
 // Flat parameter layout (torch nn.Linear order): W1 b1 W2 b2 W3 b3.
@@ -67,6 +64,20 @@ __host__ __device__ constexpr long frag_off(int n, int k, int ks_per_row) {
 __device__ __forceinline__ short8_t ld_frag(const uint16_t* w, int nt, int ks, int ks_per_row, int lane) {
   return ld8(w + ((long)nt * ks_per_row + ks) * 512 + lane * 8);
 }
+// Buffer-load form for the fully unrolled k-loops: a 32-bit per-lane voffset
+// plus a constant soffset per (fragment, k-step).  With flat addresses hipcc
+// kept one 64-bit SGPR address per unrolled load and spilled ~200 SGPRs.
+struct FragSrc {
+  __amdgpu_buffer_rsrc_t rs;
+  int voff;  // bytes: this wave's first fragment row block + lane * 16
+  __device__ __forceinline__ FragSrc(const uint16_t* w, int bytes, int nt0, int ks_per_row, int lane)
+      : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(w), 0, bytes, 0x00020000)),
+        voff((nt0 * ks_per_row * 512 + lane * 8) * 2) {}
+  // fragment (nt0 + n, ks)
+  __device__ __forceinline__ short8_t operator()(int n, int ks, int ks_per_row) const {
+    return __builtin_bit_cast(short8_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (n * ks_per_row + ks) * 1024, 0));
+  }
+};
 
 struct MlpRowArgs {
   const uint8_t* x;
@@ -77,38 +88,50 @@ struct MlpRowArgs {
   const float *b1, *b2, *b3;
   float xa, xb, grad_scale;
   uint16_t *h1, *h2, *dz, *dh2, *dh1;  // row-major [batch][256] ([batch][16] for dz)
-  uint16_t* xn;                         // normalised X, row-major [batch][XN_LD]
   float *loss, *correct, *logits;
+  unsigned long long* stamps;  // diagnostics: per-workgroup phase timestamps (nullptr in production)
 };
 
 // Fully unrolled K loop with a 4-deep register ring for the per-wave B
 // operand (weights, streamed from L2).  `after(s)` runs after step s's MFMAs
 // and its ring refill (chunk hand-offs / barriers of the A operand ring).
-template <int NSTEPS, class LoadB, class Step, class After>
+template <int NSTEPS, int NF, class LoadB, class Step, class After>
 __device__ __forceinline__ void kloop_ring4(LoadB&& loadb, Step&& step, After&& after) {
-  short8_t r0[4], r1[4], r2[4], r3[4];
+  // sched_barrier pins every refill right after the step that frees its slot:
+  // left alone, the scheduler sank the loads next to their use and the
+  // s_waitcnt inserter then kept ONE k-step in flight instead of four.
+  short8_t r0[NF], r1[NF], r2[NF], r3[NF];
   loadb(r0, 0);
   if (NSTEPS > 1) loadb(r1, 1);
   if (NSTEPS > 2) loadb(r2, 2);
   if (NSTEPS > 3) loadb(r3, 3);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int s = 0; s < NSTEPS; s += 4) {
     step(s, r0);
+    __builtin_amdgcn_sched_barrier(0);
     if (s + 4 < NSTEPS) loadb(r0, s + 4);
+    __builtin_amdgcn_sched_barrier(0);
     after(s);
     if (s + 1 < NSTEPS) {
       step(s + 1, r1);
+      __builtin_amdgcn_sched_barrier(0);
       if (s + 5 < NSTEPS) loadb(r1, s + 5);
+      __builtin_amdgcn_sched_barrier(0);
       after(s + 1);
     }
     if (s + 2 < NSTEPS) {
       step(s + 2, r2);
+      __builtin_amdgcn_sched_barrier(0);
       if (s + 6 < NSTEPS) loadb(r2, s + 6);
+      __builtin_amdgcn_sched_barrier(0);
       after(s + 2);
     }
     if (s + 3 < NSTEPS) {
       step(s + 3, r3);
+      __builtin_amdgcn_sched_barrier(0);
       if (s + 7 < NSTEPS) loadb(r3, s + 7);
+      __builtin_amdgcn_sched_barrier(0);
       after(s + 3);
     }
   }
@@ -119,29 +142,61 @@ __device__ __forceinline__ long batch_base(const int* cursor, int n_batches, int
   return b * batch;
 }
 
-// Copy a [64][ncols] bf16 LDS image (row stride ld) to global rows (stride gld): 16-B stores.
-template <int NCOLS>
+// Copy a [BM][ncols] bf16 LDS image (row stride ld) to global rows (stride gld): 16-B stores.
+template <int BM, int NT, int NCOLS>
 __device__ __forceinline__ void copy_out(const uint16_t* src, int ld, uint16_t* dst, int gld, int tid) {
   constexpr int CPR = NCOLS / 8;
 #pragma unroll
-  for (int q = tid; q < BM * CPR; q += 256) {
+  for (int q = tid; q < BM * CPR; q += NT) {
     const int r = q / CPR, c = (q - r * CPR) * 8;
     *reinterpret_cast<short8_t*>(dst + (long)r * gld + c) = *reinterpret_cast<const short8_t*>(src + r * ld + c);
   }
 }
 
-template <bool TRAIN>
-__global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * REG];
-  uint16_t* R0 = smem;        // X ring -> H2 image -> dH2 image
-  uint16_t* R1 = smem + REG;  // H1 image -> dZ image -> dH1 image
+// One of the 8 iterations of copy_out (per-thread share 1/8): lets the
+// activation stores be spread over the NEXT layer's k-loop.  A burst of 64 KB
+// of 16-B stores per workgroup is store-issue bound (~14 B/clk/CU,
+// MI355X_MICROARCH.md constants table) and left the MFMA pipe idle for ~5k
+// cycles per layer; interleaved, the stores drain under the MFMAs.
+template <int BM, int NT, int NCOLS>
+__device__ __forceinline__ void copy_part(const uint16_t* src, int ld, uint16_t* dst, int gld, int tid, int it) {
+  constexpr int CPR = NCOLS / 8;
+  static_assert(BM * CPR == 8 * NT, "copy_part splits the copy in 8 equal parts");
+  const int q = tid + it * NT;
+  const int r = q / CPR, c = (q - r * CPR) * 8;
+  *reinterpret_cast<short8_t*>(dst + (long)r * gld + c) = *reinterpret_cast<const short8_t*>(src + r * ld + c);
+}
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// BM batch rows per workgroup, BM/16 waves.  Wave w owns 16*NF output columns
+// (NF = 256 / (16 * waves)) for ALL BM rows, so one weight fragment a wave
+// streams from L2 feeds MF = BM/16 MFMAs: BM = 128 halves the weight traffic
+// per FLOP of BM = 64 (the rows kernel's limiter, profiles/r01_v6).
+template <bool TRAIN, int BM>
+__global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpRowArgs a) {
+  constexpr int MF = BM / 16;        // m-fragments per wave (= waves per workgroup)
+  constexpr int NT = BM * 4;         // threads
+  constexpr int NF = 16 / MF;        // n-fragments per wave
+  constexpr int REGB = BM * HS_LD;   // one LDS region (elements)
+  static_assert(2 * BM * XC_LD <= REGB, "X ring must fit region 0");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * REGB + BM * DZ_LD];
+  uint16_t* R0 = smem;             // X ring -> H2 image -> dH2 image
+  uint16_t* R1 = smem + REGB;      // H1 image -> dH1 image
+  uint16_t* RZ = smem + 2 * REGB;  // dZ image
+  // ReLU masks are NOT kept in registers: H1/H2 stay in LDS until the masked
+  // backward products overwrite them in place (hipcc held 64 compare masks per
+  // layer in SGPR pairs and spilled ~200 SGPRs).
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lg = lane >> 4;
   const int row0 = blockIdx.x * BM;
   const long srow0 = batch_base(a.cursor, a.n_batches, a.batch) + row0;
-  const int cw = wave * 64;  // this wave's 64 output columns
-  floatx4_t acc[4][4];
+  const int cw = wave * 16 * NF;  // this wave's output columns
+  floatx4_t acc[MF][NF];
+  auto stamp = [&](int i) {
+    if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
 
   // ---- layer 1: H1 = relu(X W1^T + b1), K = 832 streamed in 13 chunks of 64 ----
   const int xrow = tid >> 2, xcol = (tid & 3) * 16;
@@ -161,34 +216,69 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
     }
     *reinterpret_cast<short8_t*>(d) = lo;
     *reinterpret_cast<short8_t*>(d + 8) = hi;
-    if (TRAIN) {  // the weight gradient's B operand for dW1
-      uint16_t* g = a.xn + (long)(row0 + xrow) * XN_LD + c * 64 + xcol;
-      *reinterpret_cast<short8_t*>(g) = lo;
-      *reinterpret_cast<short8_t*>(g + 8) = hi;
+  };
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int m = 0; m < MF; ++m)
+#pragma unroll
+      for (int n = 0; n < NF; ++n) acc[m][n] = zero4();
+  };
+  // MFMAs of one 32-deep k-step: A fragments from an LDS image, B from the ring
+  auto mfma_step = [&](const uint16_t* abase, int ld, const short8_t* b) {
+    short8_t af[MF];
+#pragma unroll
+    for (int m = 0; m < MF; ++m) af[m] = lds8(abase + m * 16 * ld);
+#pragma unroll
+    for (int m = 0; m < MF; ++m)
+#pragma unroll
+      for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
+  };
+  // bias + ReLU epilogue into a [BM][HS_LD] image
+  auto relu_out = [&](const float* bias_v, uint16_t* img) {
+#pragma unroll
+    for (int n = 0; n < NF; ++n) {
+      const int col = cw + n * 16 + lr;
+      const float bias = bias_v[col];
+#pragma unroll
+      for (int m = 0; m < MF; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          img[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(fmaxf(acc[m][n][r] + bias, 0.f));
     }
   };
+  // in place: img holds the forward activation H (>= 0); write acc * 1[H > 0]
+  auto masked_out = [&](uint16_t* img) {
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+    for (int n = 0; n < NF; ++n) {
+      const int col = cw + n * 16 + lr;
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
+      for (int m = 0; m < MF; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          uint16_t* e = img + (m * 16 + 4 * lg + r) * HS_LD + col;
+          *e = f2bf(*e != 0 ? acc[m][n][r] : 0.f);
+        }
+    }
+  };
+
+  const FragSrc f_w1(a.w1h, HID * D_INP * 2, NF * wave, KS1, lane);
+  const FragSrc f_w2(a.w2h, HID * HID * 2, NF * wave, KS2, lane);
+  const FragSrc f_w2t(a.w2th, HID * HID * 2, NF * wave, KS2, lane);
+  const FragSrc f_w3(a.w3h, 16 * HID * 2, 0, KS2, lane);
+  const FragSrc f_w3t(a.w3th, HID * 32 * 2, NF * wave, 1, lane);
+
+  zero_acc();
   {
     uint4 xn1 = xload(1), xn2 = xload(2);
     xstore(0, xload(0));
     __syncthreads();
-    kloop_ring4<KS1>(
-        [&](short8_t (&r)[4], int st) {
+    kloop_ring4<KS1, NF>(
+        [&](short8_t (&r)[NF], int st) {
 #pragma unroll
-          for (int n = 0; n < 4; ++n) r[n] = ld_frag(a.w1h, 4 * wave + n, st, KS1, lane);
+          for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
         },
-        [&](int st, short8_t (&b)[4]) {
-          const uint16_t* xa_ = R0 + ((st >> 1) & 1) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg;
-          short8_t af[4];
-#pragma unroll
-          for (int m = 0; m < 4; ++m) af[m] = lds8(xa_ + m * 16 * XC_LD);
-#pragma unroll
-          for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
+        [&](int st, short8_t (&b)[NF]) {
+          mfma_step(R0 + ((st >> 1) & 1) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg, XC_LD, b);
         },
         [&](int st) {
           if (st & 1) {  // end of chunk c: publish chunk c+1, prefetch chunk c+3
@@ -200,71 +290,39 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
           }
         });
   }
-  uint64_t mask1 = 0;
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int col = cw + n * 16 + lr;
-    const float bias = a.b1[col];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float h = acc[m][n][r] + bias;
-        const bool pos = h > 0.f;
-        mask1 |= (uint64_t)pos << (m * 16 + n * 4 + r);
-        R1[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(pos ? h : 0.f);
-      }
-  }
+  stamp(1);
+  relu_out(a.b1, R1);
   __syncthreads();
-  if (TRAIN) copy_out<HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid);
+  stamp(2);
 
   // ---- layer 2: H2 = relu(H1 W2^T + b2), K = 256; A = R1, out -> R0 ----
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
+  zero_acc();
   {
     const uint16_t* ha = R1 + lr * HS_LD + 8 * lg;
-    kloop_ring4<KS2>(
-        [&](short8_t (&r)[4], int st) {
+    kloop_ring4<KS2, NF>(
+        [&](short8_t (&r)[NF], int st) {
 #pragma unroll
-          for (int n = 0; n < 4; ++n) r[n] = ld_frag(a.w2h, 4 * wave + n, st, KS2, lane);
+          for (int n = 0; n < NF; ++n) r[n] = f_w2(n, st, KS2);
         },
-        [&](int st, short8_t (&b)[4]) {
-          short8_t af[4];
-#pragma unroll
-          for (int m = 0; m < 4; ++m) af[m] = lds8(ha + m * 16 * HS_LD + st * 32);
-#pragma unroll
-          for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
-        },
-        [](int) {});
+        [&](int st, short8_t (&b)[NF]) { mfma_step(ha + st * 32, HS_LD, b); },
+        [&](int st) {
+          if (TRAIN) copy_part<BM, NT, HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid, st);
+        });
   }
-  uint64_t mask2 = 0;
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int col = cw + n * 16 + lr;
-    const float bias = a.b2[col];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float h = acc[m][n][r] + bias;
-        const bool pos = h > 0.f;
-        mask2 |= (uint64_t)pos << (m * 16 + n * 4 + r);
-        R0[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(pos ? h : 0.f);
-      }
-  }
+  stamp(3);
+  relu_out(a.b2, R0);
   __syncthreads();
-  if (TRAIN) copy_out<HID>(R0, HS_LD, a.h2 + (long)row0 * HID, HID, tid);
+  stamp(4);
 
   // ---- layer 3 + softmax cross-entropy: wave w owns rows 16w..16w+15; dZ -> R1 ----
   {
     floatx4_t z = zero4();
     const uint16_t* ha = R0 + (wave * 16 + lr) * HS_LD + 8 * lg;
 #pragma unroll
-    for (int ks = 0; ks < KS2; ++ks) z = mfma16(lds8(ha + ks * 32), ld_frag(a.w3h, 0, ks, KS2, lane), z);
+    for (int ks = 0; ks < KS2; ++ks) {
+      z = mfma16(lds8(ha + ks * 32), f_w3(0, ks, KS2), z);
+      if (TRAIN) copy_part<BM, NT, HID>(R0, HS_LD, a.h2 + (long)row0 * HID, HID, tid, ks);
+    }
     const int c = lr;
     const float bias3 = c < NC ? a.b3[c] : 0.f;
 #pragma unroll
@@ -298,79 +356,46 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       if (a.logits && c < NC) a.logits[(long)(row0 + row) * NC + c] = zz;
       if (TRAIN) {
         const float dzv = c < NC ? (e / s - (c == lab ? 1.f : 0.f)) * a.grad_scale : 0.f;
-        R1[row * DZ_LD + c] = f2bf(dzv);
-        R1[row * DZ_LD + 16 + c] = 0;
+        RZ[row * DZ_LD + c] = f2bf(dzv);
+        RZ[row * DZ_LD + 16 + c] = 0;
       }
     }
   }
   if (!TRAIN) return;
   __syncthreads();
-  copy_out<DZ_COLS>(R1, DZ_LD, a.dz + (long)row0 * DZ_COLS, DZ_COLS, tid);
+  stamp(5);
+  copy_out<BM, NT, DZ_COLS>(RZ, DZ_LD, a.dz + (long)row0 * DZ_COLS, DZ_COLS, tid);
 
   // ---- dH2 = (dZ W3) * 1[H2 > 0], K = 32 (10 classes, zero padded); out -> R0 ----
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
+  zero_acc();
   {
-    short8_t bf[4], af[4];
+    short8_t bf[NF];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) bf[n] = ld_frag(a.w3th, 4 * wave + n, 0, 1, lane);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) af[m] = lds8(R1 + (m * 16 + lr) * DZ_LD + 8 * lg);
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
+    for (int n = 0; n < NF; ++n) bf[n] = f_w3t(n, 0, 1);
+    mfma_step(RZ + lr * DZ_LD + 8 * lg, DZ_LD, bf);
   }
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int col = cw + n * 16 + lr;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        R0[(m * 16 + 4 * lg + r) * HS_LD + col] =
-            f2bf(((mask2 >> (m * 16 + n * 4 + r)) & 1) ? acc[m][n][r] : 0.f);
-  }
+  stamp(6);
+  masked_out(R0);
   __syncthreads();
-  copy_out<HID>(R0, HS_LD, a.dh2 + (long)row0 * HID, HID, tid);
+  stamp(7);
 
   // ---- dH1 = (dH2 W2) * 1[H1 > 0], K = 256; A = R0, out -> R1 ----
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
+  zero_acc();
   {
     const uint16_t* ha = R0 + lr * HS_LD + 8 * lg;
-    kloop_ring4<KS2>(
-        [&](short8_t (&r)[4], int st) {
+    kloop_ring4<KS2, NF>(
+        [&](short8_t (&r)[NF], int st) {
 #pragma unroll
-          for (int n = 0; n < 4; ++n) r[n] = ld_frag(a.w2th, 4 * wave + n, st, KS2, lane);
+          for (int n = 0; n < NF; ++n) r[n] = f_w2t(n, st, KS2);
         },
-        [&](int st, short8_t (&b)[4]) {
-          short8_t af[4];
-#pragma unroll
-          for (int m = 0; m < 4; ++m) af[m] = lds8(ha + m * 16 * HS_LD + st * 32);
-#pragma unroll
-          for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
-        },
-        [](int) {});
+        [&](int st, short8_t (&b)[NF]) { mfma_step(ha + st * 32, HS_LD, b); },
+        [&](int st) { copy_part<BM, NT, HID>(R0, HS_LD, a.dh2 + (long)row0 * HID, HID, tid, st); });
   }
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int col = cw + n * 16 + lr;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        R1[(m * 16 + 4 * lg + r) * HS_LD + col] =
-            f2bf(((mask1 >> (m * 16 + n * 4 + r)) & 1) ? acc[m][n][r] : 0.f);
-  }
+  stamp(8);
+  masked_out(R1);
   __syncthreads();
-  copy_out<HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid);
+  copy_out<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid);
+  stamp(9);
 }
 
 // ---------------------------------------------------------------------------
@@ -380,11 +405,20 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
 // Workgroup tile 128 (m) x 128 (n), 4 waves of 64 x 64.  One K slice of the
 // batch per workgroup; grid order is slice-major after the XCD remap, so all
 // tiles of one slice -- which read the same batch rows -- share an L2.
+//
+// dW1's B operand is the RAW u8 input, not a normalised bf16 copy: pixels
+// 0..255 are exact in bf16, so the kernel computes S = dH1^T X exactly and
+// the slab reduction applies the normalisation affinely,
+//   dW1 = dH1^T (a X + b) = a S + b * db1 (x) 1      (mlp_sgd_kernel).
+// That removes the 117 MB normalised-X write (rows kernel) and re-read (here)
+// per 65,536-row step.  The u8 image is read with ds_read_b64_tr_b8 (probed
+// lane map, scripts/probes/tr8_probe.hip: per 16-lane group, lane 2q+p
+// addresses row q bytes 8p..8p+7; lane i receives column i of the 8 rows).
 // ---------------------------------------------------------------------------
 struct WgProblem {
-  const uint16_t* a;  // [batch][lda] bf16: dH1 / dH2 / dZ
+  const void* a;  // [batch][lda] bf16: dH1 / dH2 / dZ
   int lda;
-  const uint16_t* b;  // [batch][ldb] bf16: normalised X / H1 / H2
+  const void* b;  // [batch][ldb]: u8 X (problem 0) / bf16 H1 / H2
   int ldb;
   int m_real, n_real;
   int tiles_m, tiles_n, tile_base;
@@ -396,6 +430,8 @@ struct WgArgs {
   int steps_per_slice, total_steps;  // 64-row stages
   float* slab;
   long slab_stride;
+  const int* cursor;  // X is the resident shard: rows start at batch_base(cursor)
+  int n_batches, batch;
 };
 
 constexpr int WG_NSLOT = 4;               // LDS ring slots; three stages in flight
@@ -410,6 +446,9 @@ static_assert(128 * WG_OUT_LD * 2 <= WG_NSLOT * WG_SLOT, "epilogue tile must fit
 // conflict-free; LDS-DMA writes the image linearly, so the same involution is
 // applied to the per-lane SOURCE address (cdna_hip_programming.md rule 21).
 __device__ __forceinline__ int wg_swz(int c, int r) { return c ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
+// u8 image: 128-B rows of 8 chunks; chunk ^ ((r >> 1) & 7) puts the 16 rows a
+// 32-lane half of ds_read_b64_tr_b8 touches on 16 distinct 4-bank groups.
+__device__ __forceinline__ int wg_swz8(int c, int r) { return c ^ ((r >> 1) & 7); }
 
 // Transposed B-style fragment (8 consecutive k rows of one column) from a
 // swizzled image.  Issued as inline asm on purpose: hipcc treats a visible
@@ -417,12 +456,6 @@ __device__ __forceinline__ int wg_swz(int c, int r) { return c ^ (((r & 3) | (((
 // front of it, which would serialise the ring; the caller waits lgkmcnt
 // itself and fences the MFMAs with sched_barrier (cdna_hip_programming.md
 // rules 18 and "Three .s-level traps" (b)).
-__device__ __forceinline__ short4_t ds_tr16_asm(const uint16_t* p) {
-  short4_t r;
-  const uint32_t a = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)p;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
 // LDS byte address (within one image) of this lane's first tr read for the
 // fragment at column n0, rows k0.. (k0 % 32 == 0).  The other reads of the
 // fragment family are fixed byte offsets: +1024 (rows +4), +8192 (k0 + 32),
@@ -433,10 +466,24 @@ __device__ __forceinline__ uint32_t wg_tr_addr(int n0, int lane) {
   const int ra = 8 * g + q;
   return (uint32_t)((ra * 128 + wg_swz(c, ra) * 8 + w) * 2);
 }
+// tr_b8 address in the u8 image for the fragment at byte column n0 (n0 % 16 == 0);
+// the second k-step (+32 rows) is +4096 B (f unchanged on rows 32 apart).
+__device__ __forceinline__ uint32_t wg_tr8_addr(int n0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 1, p = lane & 1;
+  const int r = 8 * g + q;
+  return (uint32_t)(r * 128 + wg_swz8(n0 >> 4, r) * 16 + 8 * p);
+}
 template <int OFF>
 __device__ __forceinline__ short4_t ds_tr16_off(uint32_t a) {
   short4_t r;
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+typedef uint32_t uint2v_t __attribute__((ext_vector_type(2)));
+template <int OFF>
+__device__ __forceinline__ uint2v_t ds_tr8_off(uint32_t a) {
+  uint2v_t r;
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
   return r;
 }
 template <int KOFF>
@@ -448,11 +495,28 @@ __device__ __forceinline__ short8_t wg_tr8(uint32_t a) {
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
+// 8 u8 -> 8 bf16, exact (integers < 256 have <= 8 significant bits):
+// v_cvt_f32_ubyteN per byte, then one v_perm_b32 keeps the high halves of two floats.
+__device__ __forceinline__ short8_t u8x8_exact_bf16(uint2v_t v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t x = v[h];
+    const uint32_t f0 = __float_as_uint((float)(x & 0xffu)), f1 = __float_as_uint((float)((x >> 8) & 0xffu));
+    const uint32_t f2 = __float_as_uint((float)((x >> 16) & 0xffu)), f3 = __float_as_uint((float)(x >> 24));
+    w[2 * h] = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
+    w[2 * h + 1] = __builtin_amdgcn_perm(f3, f2, 0x07060302u);
+  }
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(short8_t, u32x4{w[0], w[1], w[2], w[3]});
+}
 
-__device__ __forceinline__ void wg_vmcnt(int n) {
-  // vmcnt needs an immediate; LDS-DMA pieces per wave per stage = 8
-  if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+// vmcnt needs an immediate: wait until this wave has at most N younger stages
+// (of PPS LDS-DMA pieces each) in flight.
+template <int PPS>
+__device__ __forceinline__ void wg_vmcnt(int younger) {
+  if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPS) : "memory");
+  else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PPS) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -474,21 +538,34 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int nst = min(A.steps_per_slice, A.total_steps - st0);
   const bool do_bias = tn == 0 && wn == 0;
   const bool m_live = m0 + wm * 64 < P.m_real;  // wave-uniform: skip MFMAs on all-padding rows
+  const bool u8b = pi == 0;
 
-  // LDS-DMA map: wave w, piece j (0..3) covers image rows 4 (4w + j) .. +3;
+  // LDS-DMA map (bf16 images): wave w, piece j (0..3) covers image rows 4 (4w + j) .. +3;
   // lane -> row 4 (4w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row).
+  // u8 image: wave w, piece j (0..1) covers rows 8 (2w + j) .. +7; lane -> row + lane / 8,
+  // LDS chunk lane % 8 <- global chunk swz8(lane % 8, row).
   const int prow = lane >> 4;
   const uint16_t* asrc[4];
   const uint16_t* bsrc[4];
+  const uint8_t* bsrc8[2];
+  const long xrow0 = batch_base(A.cursor, A.n_batches, A.batch);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int row = 4 * (4 * wave + j) + prow;
     const int c = wg_swz(lane & 15, row);
     const int acol = min(m0 + c * 8, P.lda - 8);  // columns past dZ's 16 are don't-care rows of dW3
-    asrc[j] = P.a + (long)(st0 * 64 + row) * P.lda + acol;
-    bsrc[j] = P.b + (long)(st0 * 64 + row) * P.ldb + n0 + c * 8;
+    asrc[j] = static_cast<const uint16_t*>(P.a) + (long)(st0 * 64 + row) * P.lda + acol;
+    bsrc[j] = static_cast<const uint16_t*>(P.b) + (long)(st0 * 64 + row) * P.ldb + n0 + c * 8;
   }
-  auto issue = [&](int st) {  // stage st (relative to the slice) -> ring slot st % 4
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wave + j) + (lane >> 3);
+    const int c = wg_swz8(lane & 7, row);
+    const int col = min(n0 + c * 16, P.ldb - 16);  // columns >= 784 are don't-care columns of dW1
+    bsrc8[j] = static_cast<const uint8_t*>(P.b) + (xrow0 + st0 * 64 + row) * P.ldb + col;
+  }
+  auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % 4
+    constexpr bool U8 = decltype(u8_c)::value;
     uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
     uint16_t* Bi = Ai + WG_IMG;
 #pragma unroll
@@ -496,8 +573,16 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
       const int rbase = 4 * (4 * wave + j) * 128;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(asrc[j] + (long)st * 64 * P.lda),
                                        (SL_LDS void*)(Ai + rbase), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[j] + (long)st * 64 * P.ldb),
-                                       (SL_LDS void*)(Bi + rbase), 16, 0, 0);
+      if constexpr (!U8)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[j] + (long)st * 64 * P.ldb),
+                                         (SL_LDS void*)(Bi + rbase), 16, 0, 0);
+    }
+    if constexpr (U8) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc8[j] + (long)st * 64 * P.ldb),
+                                         (SL_LDS void*)(reinterpret_cast<uint8_t*>(Bi) + 8 * (2 * wave + j) * 128),
+                                         16, 0, 0);
     }
   };
 
@@ -518,34 +603,48 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) a_addr[i] = wg_tr_addr(wm * 64 + i * 16, lane);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) b_addr[j] = wg_tr_addr(wn * 64 + j * 16, lane);
+  for (int j = 0; j < 4; ++j) b_addr[j] = u8b ? wg_tr8_addr(wn * 64 + j * 16, lane) : wg_tr_addr(wn * 64 + j * 16, lane);
 
-  for (int st = 0; st < 3 && st < nst; ++st) issue(st);
-  // The main loop is instantiated per (live, bias) combination and selected by a
-  // scalar branch OUTSIDE it: with the conditions inside, hipcc treated them as
-  // divergent and copied all 64 accumulators AGPR<->VGPR on every stage
-  // (133 extra VALU per stage, measured in profiles/r01_v6).
-  auto mainloop = [&](auto live_c, auto bias_c) {
-    constexpr bool LIVE = decltype(live_c)::value, BIAS = decltype(bias_c)::value;
+  // The main loop is instantiated per (u8, live, bias) combination and selected
+  // by a scalar branch OUTSIDE it: with the conditions inside, hipcc treated
+  // them as divergent and copied all 64 accumulators AGPR<->VGPR on every stage.
+  auto mainloop = [&](auto u8_c, auto live_c, auto bias_c) {
+    constexpr bool U8 = decltype(u8_c)::value, LIVE = decltype(live_c)::value, BIAS = decltype(bias_c)::value;
+    constexpr int PPS = U8 ? 6 : 8;  // LDS-DMA pieces per wave per stage
+    for (int st = 0; st < 3 && st < nst; ++st) issue(st, u8_c);
     for (int st = 0; st < nst; ++st) {
-      wg_vmcnt(8 * min(2, nst - 1 - st));  // this wave's pieces of stage st have landed
-      __builtin_amdgcn_s_barrier();        // ... everyone's have; slot (st+3)%4 is free
-      if (st + 3 < nst) issue(st + 3);
+      wg_vmcnt<PPS>(min(2, nst - 1 - st));  // this wave's pieces of stage st have landed
+      __builtin_amdgcn_s_barrier();          // ... everyone's have; slot (st+3)%4 is free
+      if (st + 3 < nst) issue(st + 3, u8_c);
       if constexpr (LIVE) {
         const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
         auto kstep = [&](auto koff) {
-          constexpr int KO = decltype(koff)::value;
+          constexpr int KO = decltype(koff)::value;  // byte offset of the k-step in a bf16 image
           short8_t af[4], bf[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) af[i] = wg_tr8<KO>(sb + a_addr[i]);
+          if constexpr (U8) {
+            uint2v_t raw[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) bf[j] = wg_tr8<KO + WG_IMG * 2>(sb + b_addr[j]);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
+            for (int j = 0; j < 4; ++j) raw[j] = ds_tr8_off<KO / 2 + WG_IMG * 2>(sb + b_addr[j]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+              bf[j] = u8x8_exact_bf16(raw[j]);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+              for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bf[j] = wg_tr8<KO + WG_IMG * 2>(sb + b_addr[j]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+          }
           if constexpr (BIAS) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) accb[i] = mfma16(af[i], ones, accb[i]);
@@ -558,9 +657,16 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if (!m_live) mainloop(F_{}, F_{});
-  else if (do_bias) mainloop(T_{}, T_{});
-  else mainloop(T_{}, F_{});
+  if (u8b) {
+    if (do_bias) mainloop(T_{}, T_{}, T_{});
+    else mainloop(T_{}, T_{}, F_{});
+  } else if (!m_live) {
+    mainloop(F_{}, F_{}, F_{});
+  } else if (do_bias) {
+    mainloop(F_{}, T_{}, T_{});
+  } else {
+    mainloop(F_{}, T_{}, F_{});
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -606,6 +712,7 @@ struct SgdArgs {
   float* grad_out;       // reduced gradient written here (all-reduce hand-off)
   long n;
   float lr, mu, wd;
+  float xa, xb;  // input normalisation: the slabs hold dH1^T X for raw u8 X (see mlp_wgrad_kernel)
   int mode;  // 0: refresh bf16 shadows from w; 1: reduce only (grad_out); 2: reduce/read + update
   uint16_t *w1h, *w2h, *w2th, *w3h, *w3th;
   int* cursor;
@@ -653,6 +760,13 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
         const float4 v = *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride);
         g[0] += v.x; g[1] += v.y; g[2] += v.z; g[3] += v.w;
       }
+      if (p0 < P_B1) {  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per thread
+        const long m = p0 / D_IN;
+        float db = 0.f;
+        for (int t = 0; t < a.slices; ++t) db += a.slab[(long)t * a.slab_stride + P_B1 + m];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g[j] = a.xa * g[j] + a.xb * db;
+      }
     } else {
       for (int sidx = 0; sidx < a.slices; ++sidx)
         for (int j = 0; p0 + j < a.n; ++j) g[j] += a.slab[(long)sidx * a.slab_stride + p0 + j];
@@ -684,12 +798,28 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
 extern "C" {
 
 long sl_mlp_param_count() { return P_N; }
-int sl_mlp_xn_stride() { return XN_LD; }
+
+static unsigned long long* g_stamps = nullptr;
+int sl_mlp_set_stamps(unsigned long long* p) {
+  g_stamps = p;
+  return 0;
+}
+static int g_rows_bm = 0;  // 0: auto; 64 / 128 force a tile height (benchmarks, tests)
+int sl_mlp_set_rows_bm(int bm) {
+  g_rows_bm = bm;
+  return 0;
+}
+
+// Rows per workgroup: 128 (8 waves) once that still gives every CU a workgroup, else 64.
+int sl_mlp_rows_bm(int batch) {
+  if (g_rows_bm == 64 || (g_rows_bm == 128 && batch % 128 == 0)) return g_rows_bm;
+  return (batch % 128 == 0 && batch / 128 >= 256) ? 128 : 64;
+}
 
 int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_batches, int batch,
                 const uint16_t* w1h, const uint16_t* w2h, const uint16_t* w3h, const uint16_t* w2th,
                 const uint16_t* w3th, const float* params, float xa, float xb, float grad_scale,
-                uint16_t* h1, uint16_t* h2, uint16_t* dz, uint16_t* dh2, uint16_t* dh1, uint16_t* xn,
+                uint16_t* h1, uint16_t* h2, uint16_t* dz, uint16_t* dh2, uint16_t* dh1,
                 float* loss, float* correct, float* logits, int train, hipStream_t stream) {
   if (batch <= 0 || batch % BM != 0) return -1;
   MlpRowArgs a;
@@ -697,13 +827,17 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th;
   a.b1 = params + P_B1; a.b2 = params + P_B2; a.b3 = params + P_B3;
   a.xa = xa; a.xb = xb; a.grad_scale = grad_scale;
-  a.h1 = h1; a.h2 = h2; a.dz = dz; a.dh2 = dh2; a.dh1 = dh1; a.xn = xn;
+  a.h1 = h1; a.h2 = h2; a.dz = dz; a.dh2 = dh2; a.dh1 = dh1;
   a.loss = loss; a.correct = correct; a.logits = logits;
-  if (train) {
-    if (!h1 || !h2 || !dz || !dh2 || !dh1 || !xn) return -2;
-    hipLaunchKernelGGL(mlp_rows_kernel<true>, dim3(batch / BM), dim3(256), 0, stream, a);
+  a.stamps = g_stamps;
+  if (train && (!h1 || !h2 || !dz || !dh2 || !dh1)) return -2;
+  const int bm = sl_mlp_rows_bm(batch);
+  if (bm == 128) {
+    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128>), dim3(batch / 128), dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128>), dim3(batch / 128), dim3(512), 0, stream, a);
   } else {
-    hipLaunchKernelGGL(mlp_rows_kernel<false>, dim3(batch / BM), dim3(256), 0, stream, a);
+    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64>), dim3(batch / 64), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 64>), dim3(batch / 64), dim3(256), 0, stream, a);
   }
   SL_CHECK_LAUNCH();
   return 0;
@@ -720,14 +854,16 @@ int sl_mlp_wgrad_slices(int batch, int requested) {
   return (total + spp - 1) / spp;
 }
 
-int sl_mlp_wgrad(int batch, const uint16_t* xn, const uint16_t* h1, const uint16_t* h2, const uint16_t* dz,
-                 const uint16_t* dh2, const uint16_t* dh1, float* slab, int slices, long slab_stride,
-                 hipStream_t stream) {
+// x: the resident u8 shard [n_batches * batch][784]; the batch rows are the
+// ones the rows kernel used (cursor not yet bumped: mlp_sgd_kernel bumps it).
+int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, const uint16_t* h1,
+                 const uint16_t* h2, const uint16_t* dz, const uint16_t* dh2, const uint16_t* dh1, float* slab,
+                 int slices, long slab_stride, hipStream_t stream) {
   const int s_eff = sl_mlp_wgrad_slices(batch, slices);
   if (s_eff <= 0 || s_eff != slices) return -1;
   WgArgs a;
   // dW1, db1 = dH1^T [256 x B] . Xn
-  a.p[0] = WgProblem{dh1, HID, xn, XN_LD, HID, D_IN, HID / 128, (D_IN + 127) / 128, 0, P_W1, P_B1};
+  a.p[0] = WgProblem{dh1, HID, x, D_IN, HID, D_IN, HID / 128, (D_IN + 127) / 128, 0, P_W1, P_B1};
   // dW2, db2 = dH2^T . H1
   a.p[1] = WgProblem{dh2, HID, h1, HID, HID, HID, HID / 128, HID / 128, 0, P_W2, P_B2};
   // dW3, db3 = dZ^T . H2
@@ -741,17 +877,21 @@ int sl_mlp_wgrad(int batch, const uint16_t* xn, const uint16_t* h1, const uint16
   a.total_steps = batch / 64;
   a.steps_per_slice = (a.total_steps + slices - 1) / slices;
   a.slab = slab; a.slab_stride = slab_stride;
+  a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
+  if (((uintptr_t)x & 15) != 0) return -2;  // LDS-DMA pieces are 16-B
   hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
 
 int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_stride, const float* grad_in,
-               float* grad_out, float lr, float mu, float wd, int mode, uint16_t* w1h, uint16_t* w2h,
+               float* grad_out, float lr, float mu, float wd, float xa, float xb, int mode, uint16_t* w1h,
+               uint16_t* w2h,
                uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, hipStream_t stream) {
   SgdArgs a;
   a.w = w; a.mom = mom; a.slab = slab; a.slices = slices; a.slab_stride = slab_stride;
   a.grad_in = grad_in; a.grad_out = grad_out; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = mode;
+  a.xa = xa; a.xb = xb;
   a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
   if (mode != 0 && !slab && !grad_in) return -1;
   if (mode == 1 && !grad_out) return -1;

@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase s_memtime stamps of the MLP rows kernel (workgroup-lead lane).
+Prints the median cycles of each phase over workgroups for a steady-state step."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from serverless_learn_amd.data.synthetic import make_mnist_like
+from serverless_learn_amd.models.mlp import FusedMLPTrainer
+from serverless_learn_amd.ops import _native
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+x, y = make_mnist_like(B * 2, seed=0)
+tr = FusedMLPTrainer(batch=B, device="cuda:0")
+tr.load_shard(torch.from_numpy(x), torch.from_numpy(y))
+for _ in range(5):
+    tr.step()
+bm = _native.lib().sl_mlp_rows_bm(B)
+st = torch.zeros(B // bm * 16, dtype=torch.int64, device="cuda:0")
+_native.call("sl_mlp_set_stamps", st.data_ptr())
+tr._lc = None; tr._lkey = None
+tr.step()
+torch.cuda.synchronize()
+_native.call("sl_mlp_set_stamps", None)
+s = st.view(-1, 16)[:, :10].cpu().double()
+d = s[:, 1:] - s[:, :-1]
+names = ["layer1", "relu1+h1", "layer2", "relu2+h2", "layer3+ce+dz", "dH2 mfma", "mask+dh2", "dH1 mfma", "mask+dh1"]
+print(f"B={B} BM={bm} workgroups={s.shape[0]}  total median cycles {float((s[:, 9] - s[:, 0]).median()):.0f}")
+for i, n in enumerate(names):
+    print(f"  {n:14s} median {float(d[:, i].median()):8.0f}  mean {float(d[:, i].mean()):8.0f}")
+t0 = s[:, 0] - s[:, 0].min()
+print(f"  start spread: median {float(t0.median()):.0f} max {float(t0.max()):.0f}")

@@ -20,6 +20,7 @@ that takes its place, in three forms:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -136,7 +137,10 @@ def reference_grads_bf16(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor
     dz = r((torch.softmax(z, 1) - F.one_hot(yl, CLASSES).float()) * grad_scale)
     dh2 = r((dz @ w3) * (p2 > 0).float())
     dh1 = r((dh2 @ w2) * (p1 > 0).float())
-    g = torch.cat([(dh1.t() @ xn).reshape(-1), dh1.sum(0), (dh2.t() @ h1).reshape(-1), dh2.sum(0),
+    # dW1 uses the exact normalised input: the weight-gradient kernel multiplies the raw
+    # u8 pixels (exact in bf16) and applies the normalisation affinely afterwards
+    xe = x_u8.reshape(-1, D_IN).float() * a + b
+    g = torch.cat([(dh1.t() @ xe).reshape(-1), dh1.sum(0), (dh2.t() @ h1).reshape(-1), dh2.sum(0),
                    (dz.t() @ h2).reshape(-1), dz.sum(0)])
     correct = (z.argmax(1) == yl).float().sum()
     return losses.sum(), correct, g
@@ -237,6 +241,8 @@ class FusedMLPTrainer:
             raise ValueError(f"batch must be a multiple of {BLOCK_ROWS}")
         self._n = _native
         _native.lib()  # fail loudly if the HIP library cannot be loaded
+        if os.environ.get("SL_MLP_ROWS_BM"):  # force the rows kernel's tile height (64 / 128)
+            _native.call("sl_mlp_set_rows_bm", int(os.environ["SL_MLP_ROWS_BM"]))
         dev = torch.device(device)
         self.device = dev
         self.batch = batch
@@ -265,8 +271,6 @@ class FusedMLPTrainer:
         self.dh1t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
         self.dh2t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
         self.dzt = torch.empty(batch, 16, dtype=bf, device=dev)
-        # normalised input (bf16) written by the row kernel for dW1; columns >= 784 stay zero
-        self.xn = torch.zeros(batch, int(_native.lib().sl_mlp_xn_stride()), dtype=bf, device=dev)
         self.loss = torch.zeros(batch, dtype=torch.float32, device=dev)
         self.correct = torch.zeros(batch, dtype=torch.float32, device=dev)
         self.slab = torch.empty(self.slices, self.n_pad, dtype=torch.float32, device=dev)
@@ -304,7 +308,7 @@ class FusedMLPTrainer:
     # ---- kernels ----
     def refresh_shadows(self) -> None:
         n = self._n
-        n.call("sl_mlp_sgd", n.ptr(self.params), None, None, 0, 0, None, None, 0.0, 0.0, 0.0, 0,
+        n.call("sl_mlp_sgd", n.ptr(self.params), None, None, 0, 0, None, None, 0.0, 0.0, 0.0, self.xa, self.xb, 0,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
                None, n.stream_ptr())
 
@@ -320,10 +324,11 @@ class FusedMLPTrainer:
             "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
                              p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
                              p(self.params), self.xa, self.xb, self.grad_scale,
-                             p(self.h1t), p(self.h2t), p(self.dzt), p(self.dh2t), p(self.dh1t), p(self.xn),
+                             p(self.h1t), p(self.h2t), p(self.dzt), p(self.dh2t), p(self.dh1t),
                              p(self.loss), p(self.correct), None, 1),
-            "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.xn), p(self.h1t), p(self.h2t), p(self.dzt),
-                              p(self.dh2t), p(self.dh1t), p(self.slab), self.slices, self.n_pad),
+            "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
+                              p(self.h1t), p(self.h2t), p(self.dzt), p(self.dh2t), p(self.dh1t), p(self.slab),
+                              self.slices, self.n_pad),
         }
         for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
                                                         "reduce": (1, False, True, False),
@@ -331,7 +336,7 @@ class FusedMLPTrainer:
             lc[name] = n.Launch("sl_mlp_sgd", p(self.params), p(self.mom),
                                 None if from_grad else p(self.slab), self.slices, self.n_pad,
                                 p(self.grad) if from_grad else None, p(self.grad) if grad_out else None,
-                                self.lr, self.momentum, self.weight_decay, mode, *ws,
+                                self.lr, self.momentum, self.weight_decay, self.xa, self.xb, mode, *ws,
                                 p(self.cursor) if bump else None)
         self._lc, self._lkey = lc, key
         return lc
@@ -343,7 +348,7 @@ class FusedMLPTrainer:
         n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, self.grad_scale,
-               n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t), n.ptr(self.xn),
+               n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t),
                n.ptr(self.loss), n.ptr(self.correct), None, 0, n.stream_ptr())
 
     def _wgrad(self):
@@ -405,7 +410,7 @@ class FusedMLPTrainer:
         corr = torch.zeros(rows, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None,
                n.ptr(loss), n.ptr(corr), None, 0, n.stream_ptr())
         return StepStats(float(loss.mean()), float(corr.mean()), rows)
 
@@ -418,7 +423,7 @@ class FusedMLPTrainer:
         out = torch.empty(rows, CLASSES, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None,
                None, None, n.ptr(out), 0, n.stream_ptr())
         return out
 

@@ -17,7 +17,9 @@ def _rel(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
 
-def test_logits_match_reference():
+@pytest.mark.parametrize("bm", [64, 128])
+def test_logits_match_reference(bm, rows_bm):
+    rows_bm(bm)
     x, y = _data(256)
     flat = M.init_params(1)
     tr = M.FusedMLPTrainer(batch=256, flat=flat)
@@ -27,8 +29,20 @@ def test_logits_match_reference():
     assert (got.argmax(1) == ref.argmax(1)).float().mean() > 0.97
 
 
-@pytest.mark.parametrize("batch", [64, 512, 2048])
-def test_gradients_match_reference(batch):
+@pytest.fixture
+def rows_bm():
+    from serverless_learn_amd.ops import _native
+
+    yield lambda bm: _native.call("sl_mlp_set_rows_bm", bm)
+    _native.call("sl_mlp_set_rows_bm", 0)
+
+
+@pytest.mark.parametrize("batch,bm", [(64, 64), (512, 64), (2048, 64), (512, 128), (2048, 128)])
+def test_gradients_match_reference(batch, bm, rows_bm):
+    from serverless_learn_amd.ops import _native
+
+    rows_bm(bm)
+    assert _native.lib().sl_mlp_rows_bm(batch) == bm
     x, y = _data(batch, seed=3)
     flat = M.init_params(2)
     tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
