@@ -153,6 +153,31 @@ __device__ __forceinline__ void copy_out(const uint16_t* src, int ld, uint16_t* 
   }
 }
 
+// Reductions over a DPP row (16 lanes): xor 1 and xor 2 by quad_perm, then
+// row_half_mirror (i -> 7 - i) and row_mirror (i -> 15 - i) pair the halves.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __int_as_float(dpp_i<CTRL>(__float_as_int(v))); }
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+__device__ __forceinline__ int row16_min(int v) {
+  v = min(v, dpp_i<0xB1>(v));
+  v = min(v, dpp_i<0x4E>(v));
+  v = min(v, dpp_i<0x141>(v));
+  return min(v, dpp_i<0x140>(v));
+}
+
 // One of the 8 iterations of copy_out (per-thread share 1/8): lets the
 // activation stores be spread over the NEXT layer's k-loop.  A burst of 64 KB
 // of 16-B stores per workgroup is store-issue bound (~14 B/clk/CU,
@@ -267,6 +292,9 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   const FragSrc f_w3(a.w3h, 16 * HID * 2, 0, KS2, lane);
   const FragSrc f_w3t(a.w3th, HID * 32 * 2, NF * wave, 1, lane);
 
+  // labels of this lane's 4 softmax rows (wave * 16 + 4 lg + r), fetched long before use
+  const uint32_t lab4 = a.y ? *reinterpret_cast<const uint32_t*>(a.y + srow0 + wave * 16 + 4 * lg) : 0u;
+
   zero_acc();
   {
     uint4 xn1 = xload(1), xn2 = xload(2);
@@ -310,17 +338,23 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
         });
   }
   stamp(3);
+  short8_t w3f[KS2];  // layer-3 weights, prefetched under the ReLU-2 epilogue
+#pragma unroll
+  for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
   relu_out(a.b2, R0);
   __syncthreads();
   stamp(4);
 
-  // ---- layer 3 + softmax cross-entropy: wave w owns rows 16w..16w+15; dZ -> R1 ----
+  // ---- layer 3 + softmax cross-entropy: wave w owns rows 16w..16w+15; dZ -> RZ ----
+  // Row reductions over the 16 lanes holding one row's logits run on DPP
+  // (quad perms + row half-mirror + row mirror), not ds_bpermute shuffles whose
+  // LDS round trips made this phase ~10k cycles; W3 and labels were prefetched.
   {
     floatx4_t z = zero4();
     const uint16_t* ha = R0 + (wave * 16 + lr) * HS_LD + 8 * lg;
 #pragma unroll
     for (int ks = 0; ks < KS2; ++ks) {
-      z = mfma16(lds8(ha + ks * 32), f_w3(0, ks, KS2), z);
+      z = mfma16(lds8(ha + ks * 32), w3f[ks], z);
       if (TRAIN) copy_part<BM, NT, HID>(R0, HS_LD, a.h2 + (long)row0 * HID, HID, tid, ks);
     }
     const int c = lr;
@@ -329,25 +363,13 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     for (int r = 0; r < 4; ++r) {
       const int row = wave * 16 + 4 * lg + r;
       const float zz = c < NC ? z[r] + bias3 : -INFINITY;
-      float mx = zz;
-      mx = fmaxf(mx, __shfl_xor(mx, 1));
-      mx = fmaxf(mx, __shfl_xor(mx, 2));
-      mx = fmaxf(mx, __shfl_xor(mx, 4));
-      mx = fmaxf(mx, __shfl_xor(mx, 8));
+      const float mx = row16_max(zz);
       const float e = c < NC ? __expf(zz - mx) : 0.f;
-      float s = e;
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
-      s += __shfl_xor(s, 4);
-      s += __shfl_xor(s, 8);
-      int lab = a.y ? (int)a.y[srow0 + row] : 0;
+      int lab = (int)((lab4 >> (8 * r)) & 0xffu);
       lab = lab < NC ? lab : 0;
-      const float zl = __shfl(zz, (lane & ~15) | lab);
-      int idx = (zz == mx) ? c : 16;
-      idx = min(idx, __shfl_xor(idx, 1));
-      idx = min(idx, __shfl_xor(idx, 2));
-      idx = min(idx, __shfl_xor(idx, 4));
-      idx = min(idx, __shfl_xor(idx, 8));
+      const float s = row16_sum(e);
+      const float zl = row16_sum(c == lab ? zz : 0.f);
+      const int idx = row16_min((zz == mx) ? c : 16);
       const float lse = mx + __logf(s);
       if (c == 0) {
         if (a.loss) a.loss[row0 + row] = lse - zl;
@@ -434,11 +456,11 @@ struct WgArgs {
   int n_batches, batch;
 };
 
-constexpr int WG_NSLOT = 4;               // LDS ring slots; three stages in flight
+constexpr int WG_NSLOT = 4;               // LDS ring slots (128 KB): three stages in flight (5 measured no better)
 constexpr int WG_IMG = 64 * 128;          // one [64 k][128] bf16 image, unpadded (swizzled)
 constexpr int WG_SLOT = 2 * WG_IMG;       // A image + B image = 32 KB
 constexpr int WG_OUT_LD = 128 + 4;        // fp32 epilogue tile
-static_assert(128 * WG_OUT_LD * 2 <= WG_NSLOT * WG_SLOT, "epilogue tile must fit the ring");
+static_assert((128 * WG_OUT_LD + 128) * 4 <= WG_NSLOT * WG_SLOT * 2, "epilogue tile must fit the ring");
 
 // 16-B chunk position inside a 256-B image row.  XOR on chunk-pair bits with
 // f(r) = (r & 3) | ((r >> 3) & 1) << 2 makes every ds_read_b64_tr_b16 of the
@@ -515,15 +537,23 @@ __device__ __forceinline__ short8_t u8x8_exact_bf16(uint2v_t v) {
 // (of PPS LDS-DMA pieces each) in flight.
 template <int PPS>
 __device__ __forceinline__ void wg_vmcnt(int younger) {
-  if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPS) : "memory");
+  if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * PPS) : "memory");
+  else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPS) : "memory");
   else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PPS) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-__global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
+// 8 waves: waves 0-3 take k-step 0 (batch rows 0-31) of every 64-row stage,
+// waves 4-7 k-step 1 (rows 32-63), each as a 2 x 2 grid of 64 x 64 sub-tiles;
+// the two k-halves are summed through LDS in the epilogue.  Two waves per SIMD
+// let one wave's LDS reads / barrier wait run under the other's MFMAs (at one
+// wave per SIMD the pipe was busy 25 % of the time, profiles/r01_v6).
+constexpr int WG_NT = 512;
+__global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_NSLOT * WG_SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
+  const int kg = wave >> 2, w4 = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int s = logical / A.total_tiles;
@@ -533,57 +563,52 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int lt = t - P.tile_base;
   const int tm = lt / P.tiles_n, tn = lt - tm * P.tiles_n;
   const int m0 = tm * 128, n0 = tn * 128;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = w4 >> 1, wn = w4 & 1;
   const int st0 = s * A.steps_per_slice;
   const int nst = min(A.steps_per_slice, A.total_steps - st0);
   const bool do_bias = tn == 0 && wn == 0;
   const bool m_live = m0 + wm * 64 < P.m_real;  // wave-uniform: skip MFMAs on all-padding rows
   const bool u8b = pi == 0;
 
-  // LDS-DMA map (bf16 images): wave w, piece j (0..3) covers image rows 4 (4w + j) .. +3;
-  // lane -> row 4 (4w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row).
-  // u8 image: wave w, piece j (0..1) covers rows 8 (2w + j) .. +7; lane -> row + lane / 8,
+  // LDS-DMA map (bf16 images): wave w, piece j (0..1) covers image rows 4 (2w + j) .. +3;
+  // lane -> row 4 (2w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row).
+  // u8 image: wave w covers rows 8w .. 8w+7; lane -> row + lane / 8,
   // LDS chunk lane % 8 <- global chunk swz8(lane % 8, row).
   const int prow = lane >> 4;
-  const uint16_t* asrc[4];
-  const uint16_t* bsrc[4];
-  const uint8_t* bsrc8[2];
+  const uint16_t* asrc[2];
+  const uint16_t* bsrc[2];
   const long xrow0 = batch_base(A.cursor, A.n_batches, A.batch);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = 4 * (4 * wave + j) + prow;
+  for (int j = 0; j < 2; ++j) {
+    const int row = 4 * (2 * wave + j) + prow;
     const int c = wg_swz(lane & 15, row);
     const int acol = min(m0 + c * 8, P.lda - 8);  // columns past dZ's 16 are don't-care rows of dW3
     asrc[j] = static_cast<const uint16_t*>(P.a) + (long)(st0 * 64 + row) * P.lda + acol;
     bsrc[j] = static_cast<const uint16_t*>(P.b) + (long)(st0 * 64 + row) * P.ldb + n0 + c * 8;
   }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = 8 * (2 * wave + j) + (lane >> 3);
+  const uint8_t* bsrc8;
+  {
+    const int row = 8 * wave + (lane >> 3);
     const int c = wg_swz8(lane & 7, row);
     const int col = min(n0 + c * 16, P.ldb - 16);  // columns >= 784 are don't-care columns of dW1
-    bsrc8[j] = static_cast<const uint8_t*>(P.b) + (xrow0 + st0 * 64 + row) * P.ldb + col;
+    bsrc8 = static_cast<const uint8_t*>(P.b) + (xrow0 + st0 * 64 + row) * P.ldb + col;
   }
   auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % 4
     constexpr bool U8 = decltype(u8_c)::value;
     uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
     uint16_t* Bi = Ai + WG_IMG;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int rbase = 4 * (4 * wave + j) * 128;
+    for (int j = 0; j < 2; ++j) {
+      const int rbase = 4 * (2 * wave + j) * 128;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(asrc[j] + (long)st * 64 * P.lda),
                                        (SL_LDS void*)(Ai + rbase), 16, 0, 0);
       if constexpr (!U8)
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[j] + (long)st * 64 * P.ldb),
                                          (SL_LDS void*)(Bi + rbase), 16, 0, 0);
     }
-    if constexpr (U8) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc8[j] + (long)st * 64 * P.ldb),
-                                         (SL_LDS void*)(reinterpret_cast<uint8_t*>(Bi) + 8 * (2 * wave + j) * 128),
-                                         16, 0, 0);
-    }
+    if constexpr (U8)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc8 + (long)st * 64 * P.ldb),
+                                       (SL_LDS void*)(reinterpret_cast<uint8_t*>(Bi) + 8 * wave * 128), 16, 0, 0);
   };
 
   floatx4_t acc[4][4], accb[4];
@@ -597,61 +622,57 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
 
-  // per-lane tr-read addresses, computed once (slot base and k offsets are immediates/one add)
+  // per-lane tr-read addresses, computed once; this wave's k-half is a constant byte offset
   const uint32_t lds_base = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
   uint32_t a_addr[4], b_addr[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) a_addr[i] = wg_tr_addr(wm * 64 + i * 16, lane);
+  for (int i = 0; i < 4; ++i) a_addr[i] = wg_tr_addr(wm * 64 + i * 16, lane) + kg * (32 * 128 * 2);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) b_addr[j] = u8b ? wg_tr8_addr(wn * 64 + j * 16, lane) : wg_tr_addr(wn * 64 + j * 16, lane);
+  for (int j = 0; j < 4; ++j)
+    b_addr[j] = u8b ? wg_tr8_addr(wn * 64 + j * 16, lane) + kg * (32 * 128) : wg_tr_addr(wn * 64 + j * 16, lane) + kg * (32 * 128 * 2);
 
   // The main loop is instantiated per (u8, live, bias) combination and selected
   // by a scalar branch OUTSIDE it: with the conditions inside, hipcc treated
   // them as divergent and copied all 64 accumulators AGPR<->VGPR on every stage.
   auto mainloop = [&](auto u8_c, auto live_c, auto bias_c) {
     constexpr bool U8 = decltype(u8_c)::value, LIVE = decltype(live_c)::value, BIAS = decltype(bias_c)::value;
-    constexpr int PPS = U8 ? 6 : 8;  // LDS-DMA pieces per wave per stage
-    for (int st = 0; st < 3 && st < nst; ++st) issue(st, u8_c);
+    constexpr int PPS = U8 ? 3 : 4;  // LDS-DMA pieces per wave per stage
+    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, u8_c);
     for (int st = 0; st < nst; ++st) {
-      wg_vmcnt<PPS>(min(2, nst - 1 - st));  // this wave's pieces of stage st have landed
-      __builtin_amdgcn_s_barrier();          // ... everyone's have; slot (st+3)%4 is free
-      if (st + 3 < nst) issue(st + 3, u8_c);
+      wg_vmcnt<PPS>(min(WG_NSLOT - 2, nst - 1 - st));  // this wave's pieces of stage st have landed
+      __builtin_amdgcn_s_barrier();  // ... everyone's have; the slot of stage st-1 is free
+      if (st + WG_NSLOT - 1 < nst) issue(st + WG_NSLOT - 1, u8_c);
       if constexpr (LIVE) {
         const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
-        auto kstep = [&](auto koff) {
-          constexpr int KO = decltype(koff)::value;  // byte offset of the k-step in a bf16 image
-          short8_t af[4], bf[4];
+        short8_t af[4], bf[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) af[i] = wg_tr8<KO>(sb + a_addr[i]);
-          if constexpr (U8) {
-            uint2v_t raw[4];
+        for (int i = 0; i < 4; ++i) af[i] = wg_tr8<0>(sb + a_addr[i]);
+        if constexpr (U8) {
+          uint2v_t raw[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) raw[j] = ds_tr8_off<KO / 2 + WG_IMG * 2>(sb + b_addr[j]);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
+          for (int j = 0; j < 4; ++j) raw[j] = ds_tr8_off<WG_IMG * 2>(sb + b_addr[j]);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              bf[j] = u8x8_exact_bf16(raw[j]);
+          for (int j = 0; j < 4; ++j) {
+            bf[j] = u8x8_exact_bf16(raw[j]);
 #pragma unroll
-              for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-            }
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bf[j] = wg_tr8<KO + WG_IMG * 2>(sb + b_addr[j]);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+            for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
           }
-          if constexpr (BIAS) {
+        } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) accb[i] = mfma16(af[i], ones, accb[i]);
-          }
-        };
-        kstep(std::integral_constant<int, 0>{});
-        kstep(std::integral_constant<int, 32 * 128 * 2>{});
+          for (int j = 0; j < 4; ++j) bf[j] = wg_tr8<WG_IMG * 2>(sb + b_addr[j]);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+        }
+        if constexpr (BIAS) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) accb[i] = mfma16(af[i], ones, accb[i]);
+        }
       }
     }
   };
@@ -670,27 +691,46 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(WgArgs A) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---- epilogue: fp32 tile through LDS -> 16-B row stores into the slab ----
+  // ---- epilogue: k-half 1 parks its tile in LDS, k-half 0 adds and stores fp32 rows to the slab ----
   float* Os = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Os[(wm * 64 + i * 16 + 4 * lg + r) * WG_OUT_LD + wn * 64 + j * 16 + lr] = acc[i][j][r];
-  float* out = A.slab + (long)s * A.slab_stride;
-  if (do_bias && lr == 0) {
+  float* Ob = Os + 128 * WG_OUT_LD;  // bias partials of k-half 1
+  if (kg == 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + 4 * lg + r;
-        if (m < P.m_real) out[P.b_off + m] = accb[i][r];
-      }
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Os[(wm * 64 + i * 16 + 4 * lg + r) * WG_OUT_LD + wn * 64 + j * 16 + lr] = acc[i][j][r];
+    if (do_bias && lr == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ob[wm * 64 + i * 16 + 4 * lg + r] = accb[i][r];
+    }
   }
   __syncthreads();
-  for (int q = tid; q < 128 * 32; q += 256) {
+  float* out = A.slab + (long)s * A.slab_stride;
+  if (kg == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Os[(wm * 64 + i * 16 + 4 * lg + r) * WG_OUT_LD + wn * 64 + j * 16 + lr] += acc[i][j][r];
+    if (do_bias && lr == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ml = wm * 64 + i * 16 + 4 * lg + r;
+          if (m0 + ml < P.m_real) out[P.b_off + m0 + ml] = accb[i][r] + Ob[ml];
+        }
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < 128 * 32; q += WG_NT) {
     const int rl = q >> 5, c4 = (q & 31) * 4;
     const int m = m0 + rl, n = n0 + c4;
     if (m < P.m_real && n < P.n_real)
@@ -810,10 +850,13 @@ int sl_mlp_set_rows_bm(int bm) {
   return 0;
 }
 
-// Rows per workgroup: 128 (8 waves) once that still gives every CU a workgroup, else 64.
+// Rows per workgroup (64 by default; 128 = one 8-wave workgroup per CU on request).
 int sl_mlp_rows_bm(int batch) {
   if (g_rows_bm == 64 || (g_rows_bm == 128 && batch % 128 == 0)) return g_rows_bm;
-  return (batch % 128 == 0 && batch / 128 >= 256) ? 128 : 64;
+  // 64 (two co-resident workgroups per CU overlap each other's epilogues) measured
+  // ahead of 128 at every batch size tried (profiles/r01_v7)
+  (void)batch;
+  return 64;
 }
 
 int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_batches, int batch,
@@ -879,7 +922,7 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
   a.slab = slab; a.slab_stride = slab_stride;
   a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
   if (((uintptr_t)x & 15) != 0) return -2;  // LDS-DMA pieces are 16-B
-  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(WG_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
