@@ -801,11 +801,17 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
         g[0] += v.x; g[1] += v.y; g[2] += v.z; g[3] += v.w;
       }
       if (p0 < P_B1) {  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per thread
-        const long m = p0 / D_IN;
-        float db = 0.f;
-        for (int t = 0; t < a.slices; ++t) db += a.slab[(long)t * a.slab_stride + P_B1 + m];
+        const float* dbs = a.slab + P_B1 + p0 / D_IN;
+        float db[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent chains: the loads stay in flight together
+        int t = 0;
+        for (; t + 4 <= a.slices; t += 4) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) g[j] = a.xa * g[j] + a.xb * db;
+          for (int u = 0; u < 4; ++u) db[u] += dbs[(long)(t + u) * a.slab_stride];
+        }
+        for (; t < a.slices; ++t) db[0] += dbs[(long)t * a.slab_stride];
+        const float dbt = (db[0] + db[1]) + (db[2] + db[3]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g[j] = a.xa * g[j] + a.xb * dbt;
       }
     } else {
       for (int sidx = 0; sidx < a.slices; ++sidx)
