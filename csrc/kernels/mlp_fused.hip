@@ -32,6 +32,15 @@
 
 using namespace sl;
 
+#ifndef SL_MLP_RING4
+#define SL_MLP_RING4 4
+#endif
+#ifndef SL_MLP_RING2
+#define SL_MLP_RING2 4
+#endif
+#ifndef SL_MLP_XSTORE_EARLY
+#define SL_MLP_XSTORE_EARLY 1
+#endif
 namespace {
 constexpr int D_IN = 784;   // input features (28x28)
 constexpr int D_INP = 832;  // layer-1 K padded to 13 chunks of 64 (w1h row stride)
@@ -95,45 +104,28 @@ struct MlpRowArgs {
 // Fully unrolled K loop with a 4-deep register ring for the per-wave B
 // operand (weights, streamed from L2).  `after(s)` runs after step s's MFMAs
 // and its ring refill (chunk hand-offs / barriers of the A operand ring).
-template <int NSTEPS, int NF, class LoadB, class Step, class After>
-__device__ __forceinline__ void kloop_ring4(LoadB&& loadb, Step&& step, After&& after) {
-  // sched_barrier pins every refill right after the step that frees its slot:
-  // left alone, the scheduler sank the loads next to their use and the
-  // s_waitcnt inserter then kept ONE k-step in flight instead of four.
-  short8_t r0[NF], r1[NF], r2[NF], r3[NF];
-  loadb(r0, 0);
-  if (NSTEPS > 1) loadb(r1, 1);
-  if (NSTEPS > 2) loadb(r2, 2);
-  if (NSTEPS > 3) loadb(r3, 3);
+// Fully unrolled K loop with a D-deep register ring for the per-wave B operand
+// (weights, streamed from L2).  `after(s)` runs after step s's MFMAs and its
+// ring refill (chunk hand-offs / barriers / spread-out stores).
+// sched_barrier pins every refill right after the step that frees its slot:
+// left alone, the scheduler sank the loads next to their use and the
+// s_waitcnt inserter then kept ONE k-step in flight instead of D.  The depth
+// matters beyond L2 latency: vmcnt retires in order, so an X load or an
+// activation store issued at step s must complete before the weights issued
+// after it are consumed, i.e. within D k-steps.
+template <int NSTEPS, int NF, int D, class LoadB, class Step, class After>
+__device__ __forceinline__ void kloop_ring(LoadB&& loadb, Step&& step, After&& after) {
+  short8_t r[D][NF];
+#pragma unroll
+  for (int i = 0; i < D && i < NSTEPS; ++i) loadb(r[i], i);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int s = 0; s < NSTEPS; s += 4) {
-    step(s, r0);
+  for (int s = 0; s < NSTEPS; ++s) {
+    step(s, r[s % D]);
     __builtin_amdgcn_sched_barrier(0);
-    if (s + 4 < NSTEPS) loadb(r0, s + 4);
+    if (s + D < NSTEPS) loadb(r[s % D], s + D);
     __builtin_amdgcn_sched_barrier(0);
     after(s);
-    if (s + 1 < NSTEPS) {
-      step(s + 1, r1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 5 < NSTEPS) loadb(r1, s + 5);
-      __builtin_amdgcn_sched_barrier(0);
-      after(s + 1);
-    }
-    if (s + 2 < NSTEPS) {
-      step(s + 2, r2);
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 6 < NSTEPS) loadb(r2, s + 6);
-      __builtin_amdgcn_sched_barrier(0);
-      after(s + 2);
-    }
-    if (s + 3 < NSTEPS) {
-      step(s + 3, r3);
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 7 < NSTEPS) loadb(r3, s + 7);
-      __builtin_amdgcn_sched_barrier(0);
-      after(s + 3);
-    }
   }
 }
 
@@ -196,11 +188,16 @@ __device__ __forceinline__ void copy_part(const uint16_t* src, int ld, uint16_t*
 // (NF = 256 / (16 * waves)) for ALL BM rows, so one weight fragment a wave
 // streams from L2 feeds MF = BM/16 MFMAs: BM = 128 halves the weight traffic
 // per FLOP of BM = 64 (the rows kernel's limiter, profiles/r01_v6).
-template <bool TRAIN, int BM>
+// WMG > 1 splits the waves into WMG row groups (each 16 * MF rows) so that the
+// NF weight fragments a wave streams feed MF m-fragments while halving the
+// LDS A-fragment traffic of the 1 x 8 layout at BM = 128.
+template <bool TRAIN, int BM, int WMG>
 __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpRowArgs a) {
-  constexpr int MF = BM / 16;        // m-fragments per wave (= waves per workgroup)
+  constexpr int NWV = BM / 16;       // waves per workgroup
+  constexpr int MF = BM / 16 / WMG;  // m-fragments per wave
   constexpr int NT = BM * 4;         // threads
-  constexpr int NF = 16 / MF;        // n-fragments per wave
+  constexpr int NF = 16 * WMG / NWV; // n-fragments per wave
+  constexpr int RING = NF >= 4 ? SL_MLP_RING4 : SL_MLP_RING2;  // weight ring depth (k-steps)
   constexpr int REGB = BM * HS_LD;   // one LDS region (elements)
   static_assert(2 * BM * XC_LD <= REGB, "X ring must fit region 0");
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * REGB + BM * DZ_LD];
@@ -216,12 +213,18 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   const int lr = lane & 15, lg = lane >> 4;
   const int row0 = blockIdx.x * BM;
   const long srow0 = batch_base(a.cursor, a.n_batches, a.batch) + row0;
-  const int cw = wave * 16 * NF;  // this wave's output columns
+  const int wmg = wave / (NWV / WMG), wng = wave % (NWV / WMG);
+  const int cw = wng * 16 * NF;  // this wave's output columns
+  const int rw = wmg * 16 * MF;  // ... and rows
   floatx4_t acc[MF][NF];
   auto stamp = [&](int i) {
     if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
+  if (a.stamps && tid == 0) {  // placement: HW_ID (CU / SH / SE) and XCC_ID
+    a.stamps[(long)blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    a.stamps[(long)blockIdx.x * 16 + 11] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
 
   // ---- layer 1: H1 = relu(X W1^T + b1), K = 832 streamed in 13 chunks of 64 ----
   const int xrow = tid >> 2, xcol = (tid & 3) * 16;
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   auto mfma_step = [&](const uint16_t* abase, int ld, const short8_t* b) {
     short8_t af[MF];
 #pragma unroll
-    for (int m = 0; m < MF; ++m) af[m] = lds8(abase + m * 16 * ld);
+    for (int m = 0; m < MF; ++m) af[m] = lds8(abase + (rw + m * 16) * ld);
 #pragma unroll
     for (int m = 0; m < MF; ++m)
 #pragma unroll
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
       for (int m = 0; m < MF; ++m)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          img[(m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(fmaxf(acc[m][n][r] + bias, 0.f));
+          img[(rw + m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(fmaxf(acc[m][n][r] + bias, 0.f));
     }
   };
   // in place: img holds the forward activation H (>= 0); write acc * 1[H > 0]
@@ -280,17 +283,17 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
       for (int m = 0; m < MF; ++m)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          uint16_t* e = img + (m * 16 + 4 * lg + r) * HS_LD + col;
+          uint16_t* e = img + (rw + m * 16 + 4 * lg + r) * HS_LD + col;
           *e = f2bf(*e != 0 ? acc[m][n][r] : 0.f);
         }
     }
   };
 
-  const FragSrc f_w1(a.w1h, HID * D_INP * 2, NF * wave, KS1, lane);
-  const FragSrc f_w2(a.w2h, HID * HID * 2, NF * wave, KS2, lane);
-  const FragSrc f_w2t(a.w2th, HID * HID * 2, NF * wave, KS2, lane);
+  const FragSrc f_w1(a.w1h, HID * D_INP * 2, NF * wng, KS1, lane);
+  const FragSrc f_w2(a.w2h, HID * HID * 2, NF * wng, KS2, lane);
+  const FragSrc f_w2t(a.w2th, HID * HID * 2, NF * wng, KS2, lane);
   const FragSrc f_w3(a.w3h, 16 * HID * 2, 0, KS2, lane);
-  const FragSrc f_w3t(a.w3th, HID * 32 * 2, NF * wave, 1, lane);
+  const FragSrc f_w3t(a.w3th, HID * 32 * 2, NF * wng, 1, lane);
 
   // labels of this lane's 4 softmax rows (wave * 16 + 4 lg + r), fetched long before use
   const uint32_t lab4 = a.y ? *reinterpret_cast<const uint32_t*>(a.y + srow0 + wave * 16 + 4 * lg) : 0u;
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     uint4 xn1 = xload(1), xn2 = xload(2);
     xstore(0, xload(0));
     __syncthreads();
-    kloop_ring4<KS1, NF>(
+    kloop_ring<KS1, NF, RING>(
         [&](short8_t (&r)[NF], int st) {
 #pragma unroll
           for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
@@ -309,6 +312,19 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
           mfma_step(R0 + ((st >> 1) & 1) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg, XC_LD, b);
         },
         [&](int st) {
+#if SL_MLP_XSTORE_EARLY
+          // chunk c+1 is converted into the free ring slot after the FIRST k-step of
+          // chunk c (that slot's readers all passed the barrier that ended chunk c-1),
+          // so the conversion overlaps the second k-step instead of preceding the barrier
+          const int c = st >> 1;
+          if (!(st & 1)) {
+            if (c + 1 < NCHUNK) xstore(c + 1, xn1);
+            xn1 = xn2;
+            if (c + 3 < NCHUNK) xn2 = xload(c + 3);
+          } else {
+            __syncthreads();
+          }
+#else
           if (st & 1) {  // end of chunk c: publish chunk c+1, prefetch chunk c+3
             const int c = st >> 1;
             if (c + 1 < NCHUNK) xstore(c + 1, xn1);
@@ -316,6 +332,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
             if (c + 3 < NCHUNK) xn2 = xload(c + 3);
             __syncthreads();
           }
+#endif
         });
   }
   stamp(1);
@@ -327,7 +344,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   zero_acc();
   {
     const uint16_t* ha = R1 + lr * HS_LD + 8 * lg;
-    kloop_ring4<KS2, NF>(
+    kloop_ring<KS2, NF, RING>(
         [&](short8_t (&r)[NF], int st) {
 #pragma unroll
           for (int n = 0; n < NF; ++n) r[n] = f_w2(n, st, KS2);
@@ -405,7 +422,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   zero_acc();
   {
     const uint16_t* ha = R0 + lr * HS_LD + 8 * lg;
-    kloop_ring4<KS2, NF>(
+    kloop_ring<KS2, NF, RING>(
         [&](short8_t (&r)[NF], int st) {
 #pragma unroll
           for (int n = 0; n < NF; ++n) r[n] = f_w2t(n, st, KS2);
@@ -882,11 +899,11 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   if (train && (!h1 || !h2 || !dz || !dh2 || !dh1)) return -2;
   const int bm = sl_mlp_rows_bm(batch);
   if (bm == 128) {
-    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128>), dim3(batch / 128), dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128>), dim3(batch / 128), dim3(512), 0, stream, a);
+    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 2>), dim3(batch / 128), dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, 2>), dim3(batch / 128), dim3(512), 0, stream, a);
   } else {
-    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64>), dim3(batch / 64), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<false, 64>), dim3(batch / 64), dim3(256), 0, stream, a);
+    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
   }
   SL_CHECK_LAUNCH();
   return 0;

@@ -32,3 +32,36 @@ for i, n in enumerate(names):
     print(f"  {n:14s} median {float(d[:, i].median()):8.0f}  mean {float(d[:, i].mean()):8.0f}")
 t0 = s[:, 0] - s[:, 0].min()
 print(f"  start spread: median {float(t0.median()):.0f} max {float(t0.max()):.0f}")
+
+# ---- occupancy reconstruction from placement ids ----
+raw = st.view(-1, 16).cpu()
+hw = raw[:, 10].numpy().astype("int64")
+xcc = raw[:, 11].numpy().astype("int64") & 0xF
+cu = (hw >> 8) & 0xF
+sh = (hw >> 12) & 0x1
+se = (hw >> 13) & 0x7
+key = xcc * 1000 + se * 100 + sh * 16 + cu
+import collections
+import numpy as np
+t0s = raw[:, 0].numpy().astype("int64")
+t1s = raw[:, 9].numpy().astype("int64")
+by = collections.defaultdict(list)
+for i in range(len(key)):
+    by[int(key[i])].append((t0s[i], t1s[i]))
+spans, conc, busy = [], [], []
+for k, iv in by.items():
+    iv.sort()
+    lo, hi = min(a for a, _ in iv), max(b for _, b in iv)
+    spans.append(hi - lo)
+    busy.append(sum(b - a for a, b in iv))
+    ev = sorted([(a, 1) for a, _ in iv] + [(b, -1) for _, b in iv])
+    c = m = 0
+    for _, d in ev:
+        c += d
+        m = max(m, c)
+    conc.append(m)
+print(f"CUs seen {len(by)}  WGs/CU median {np.median([len(v) for v in by.values()]):.0f}  "
+      f"max concurrency median {np.median(conc):.0f}  span median {np.median(spans):.0f}  "
+      f"sum(WG time)/span median {np.median(np.array(busy) / np.array(spans)):.2f}")
+xs = collections.Counter(int(x) for x in xcc)
+print("WGs per XCC:", dict(sorted(xs.items())))
