@@ -791,68 +791,68 @@ __device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) 
   }
 }
 
+// Four threads per float4 group of parameters: each sums every fourth slab
+// slice and the quad combines by DPP; thread `part` then updates element
+// p0 + part.  (One thread per group gave ~4 waves per CU for a chain of 24
+// dependent-latency slab loads: latency-bound at ~9 us.)
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+
 __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
-  const long p0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (p0 >= a.n) return;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int part = (int)(t & 3);
+  const long p0 = (t >> 2) * 4;
+  if (p0 >= a.n) return;  // whole quads exit together (n groups are quad-aligned in t)
+  const long p = p0 + part;
+  const bool mine = p < a.n;
   if (a.mode == 0) {
     // shadow refresh only (after init / checkpoint load / gossip mixing)
-    for (int j = 0; j < 4 && p0 + j < a.n; ++j) write_shadow(a, p0 + j, a.w[p0 + j]);
+    if (mine) write_shadow(a, p, a.w[p]);
     return;
   }
   const bool full = p0 + 4 <= a.n;
   float g[4] = {0.f, 0.f, 0.f, 0.f};
+  float gme;
   if (a.slab) {
     if (full) {
       const float* src = a.slab + p0;
-      int sidx = 0;
-      for (; sidx + 4 <= a.slices; sidx += 4) {  // 4 independent 16-B loads in flight per thread
-        float4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(src + (long)(sidx + u) * a.slab_stride);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { g[0] += v[u].x; g[1] += v[u].y; g[2] += v[u].z; g[3] += v[u].w; }
-      }
-      for (; sidx < a.slices; ++sidx) {
+      for (int sidx = part; sidx < a.slices; sidx += 4) {
         const float4 v = *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride);
         g[0] += v.x; g[1] += v.y; g[2] += v.z; g[3] += v.w;
       }
-      if (p0 < P_B1) {  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per thread
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = quad_sum(g[j]);
+      gme = g[part];
+      if (p0 < P_B1) {  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per quad
         const float* dbs = a.slab + P_B1 + p0 / D_IN;
-        float db[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent chains: the loads stay in flight together
-        int t = 0;
-        for (; t + 4 <= a.slices; t += 4) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) db[u] += dbs[(long)(t + u) * a.slab_stride];
-        }
-        for (; t < a.slices; ++t) db[0] += dbs[(long)t * a.slab_stride];
-        const float dbt = (db[0] + db[1]) + (db[2] + db[3]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) g[j] = a.xa * g[j] + a.xb * dbt;
+        float db = 0.f;
+        for (int sidx = part; sidx < a.slices; sidx += 4) db += dbs[(long)sidx * a.slab_stride];
+        db = quad_sum(db);
+        gme = a.xa * gme + a.xb * db;
       }
     } else {
-      for (int sidx = 0; sidx < a.slices; ++sidx)
-        for (int j = 0; p0 + j < a.n; ++j) g[j] += a.slab[(long)sidx * a.slab_stride + p0 + j];
+      gme = 0.f;
+      if (mine)
+        for (int sidx = 0; sidx < a.slices; ++sidx) gme += a.slab[(long)sidx * a.slab_stride + p];
     }
   } else {
-    for (int j = 0; j < 4 && p0 + j < a.n; ++j) g[j] = a.grad_in[p0 + j];
+    gme = mine ? a.grad_in[p] : 0.f;
   }
-  if (a.grad_out) {
-    for (int j = 0; j < 4 && p0 + j < a.n; ++j) a.grad_out[p0 + j] = g[j];
-  }
+  if (!mine) return;
+  if (a.grad_out) a.grad_out[p] = gme;
   if (a.mode == 1) return;
-  for (int j = 0; j < 4 && p0 + j < a.n; ++j) {
-    const long p = p0 + j;
-    float w = a.w[p];
-    float d = g[j] + a.wd * w;
-    if (a.mom) {
-      d = a.mu * a.mom[p] + d;
-      a.mom[p] = d;
-    }
-    w -= a.lr * d;
-    a.w[p] = w;
-    write_shadow(a, p, w);
+  float w = a.w[p];
+  float d = gme + a.wd * w;
+  if (a.mom) {
+    d = a.mu * a.mom[p] + d;
+    a.mom[p] = d;
   }
+  w -= a.lr * d;
+  a.w[p] = w;
+  write_shadow(a, p, w);
 }
 
 // ---------------------------------------------------------------------------
@@ -963,7 +963,7 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   if (mode == 1 && !grad_out) return -1;
   if (slab && (slab_stride & 3)) return -1;
   const long groups = (P_N + 3) / 4;
-  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups + 255) / 256), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * 4 + 255) / 256), dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
