@@ -65,7 +65,9 @@ def parse(argv=None):
     a.warmup = a.warmup if a.warmup is not None else (20 if mlp else 5)
     # MLP: 65,536 rows per GPU -- 1,024 row blocks, i.e. 4 per CU (16,384 leaves one per CU and the
     # step latency-bound); the shard (4 batches, 205 MB u8) is a sliver of the 288 GB of HBM.
-    a.batch = a.batch or (65536 if mlp else 256)
+    # ResNet-18: 1,024 images per GPU (82 K img/s vs 71 K at 512 and 54 K at 256 on one MI355X;
+    # ~3 GB of activations).
+    a.batch = a.batch or (65536 if mlp else 1024)
     a.shard_batches = a.shard_batches or (4 if mlp else 4)
     a.lr = a.lr if a.lr is not None else (0.05 if mlp else 0.1)
     return a
