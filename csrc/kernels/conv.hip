@@ -636,6 +636,10 @@ static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) 
 }
 
 extern "C" {
+// conv3x3_halo.hip: direct kernel for 3x3/s1/p1 64->64 convolutions on 32-wide images
+int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldw);
+int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int flip, int N, int H, uint16_t* y, int ldy,
+                   const uint16_t* add, float* stats, hipStream_t stream);
 
 // Forward: x [N][H][W][C] -> y [N][OH][OW][ldy] (cols < cout), w [cout][KH][KW][C].
 int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w, int cout, int KH, int KW,
@@ -645,6 +649,8 @@ int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w
   if (fill_geom(g, x, N, H, W, C, OH, OW, KH, KW, stride, pad)) return -1;
   if (y && (ldy < cout || (ldy & 7))) return -2;
   if ((g.K & 7) || (((uintptr_t)x | (uintptr_t)w) & 15)) return -3;
+  if (y && !yf && !bias && OH == H && OW == W && sl_conv3x3_c64_applicable(H, W, C, cout, KH, KW, stride, pad, C))
+    return sl_conv3x3_c64(x, w, 0, N, H, y, ldy, nullptr, stats, stream);
   ConvEpi e{w, cout, y, ldy, yf, bias, nullptr, stats};
   return launch_gemm<false>(g, e, stream);
 }
@@ -657,6 +663,8 @@ int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint
   if (fill_geom(g, dy, N, OH, OW, ldd, H, W, KH, KW, stride, pad)) return -1;
   if (cin & 7) return -2;
   if (((uintptr_t)dy | (uintptr_t)wt) & 15) return -3;
+  if (H == OH && W == OW && sl_conv3x3_c64_applicable(OH, OW, ldd, cin, KH, KW, stride, pad, ldd))
+    return sl_conv3x3_c64(dy, wt, 1, N, OH, dx, cin, add, nullptr, stream);
   ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr};
   return launch_gemm<true>(g, e, stream);
 }

@@ -1,0 +1,253 @@
+// Direct 3x3 / stride-1 / pad-1 convolution for 64 -> 64 channels on 32-wide
+// NHWC images (ResNet-18 layer 1 on CIFAR-shaped input), forward and data
+// gradient.  Part of the compute layer that replaces the reference's
+// simulated training (/root/reference/src/worker.cc:221-231).
+//
+// Why a second conv kernel: the implicit-GEMM path (conv.hip) gathers every
+// input pixel once per tap, nine times over, through LDS-DMA; at 64 output
+// channels the A operand dominates and the kernel is L2->LDS bound at ~25 %
+// of the MFMA rate (profiles/r01_v7).  Here one persistent workgroup per CU
+//   * keeps ALL 64 x 576 weights resident in LDS (75 KB, loaded once),
+//   * stages one halo tile per step -- 8 output rows x 32 columns need 10 x 34
+//     input pixels (54 KB) -- so each input byte crosses L2 -> LDS ~1.3 times
+//     instead of 9, and prefetches the next tile's halo into registers while
+//     the current one is on the matrix cores,
+//   * forms every tap's A fragments from the halo image with plain ds_read_b128
+//     at constant offsets (tap (kh, kw) = +(34 kh + kw) pixels).
+// 4 waves, each 64 output pixels x 64 channels (16 MFMA 16x16x32 per k-step,
+// 8 fragment reads).  Pixel rows of the halo are 10 chunks of 16 B (8 data +
+// 2 pad) and weight rows 74 chunks: both strides are = 10 (mod 16) chunks,
+// which puts the 16 lanes of every ds_read_b128 lane group on 16 distinct
+// 4-bank blocks (brute-forced over the gfx950 lane groups).
+//
+// Data gradient = the same correlation with the flipped, transposed weights:
+// dX[h][w][ci] = sum_{kh,kw,co} dY[h-1+kh][w-1+kw][co] Wt[ci][2-kh][2-kw][co].
+// Epilogue: bf16 output (+ residual add), optional per-channel BatchNorm
+// statistics of the fp32 accumulator (sum, sum of squares) kept per lane over
+// all tiles of the workgroup and folded once through the replica buffers.
+#include "common.h"
+
+#include <stdlib.h>
+
+using namespace sl;
+
+namespace {
+constexpr int HC = 64;                 // channels in = out
+constexpr int IW = 32;                 // image width
+constexpr int TR = 8;                  // output rows per tile
+constexpr int TPIX = TR * IW;          // 256 output pixels per tile
+constexpr int HR = TR + 2, HCOL = IW + 2;  // halo 10 x 34 pixels
+constexpr int PIX_CH = 10;             // 16-B chunks per halo pixel (8 data + 2 pad)
+constexpr int W_CH = 74;               // 16-B chunks per weight row (72 data + 2 pad)
+constexpr int HALO_BYTES = HR * HCOL * PIX_CH * 16;  // 54,400
+constexpr int W_BYTES = HC * W_CH * 16;              // 75,776
+constexpr int NTH = 256;
+constexpr int HALO_CHUNKS = HR * HCOL * 8;           // 2,720 data chunks
+constexpr int HALO_LOADS = (HALO_CHUNKS + NTH - 1) / NTH;  // 11 per thread
+constexpr int OUT_LD = 72;             // staging row stride (elements)
+static_assert(TPIX * OUT_LD * 2 <= HALO_BYTES, "output staging reuses the halo region");
+}  // namespace
+
+struct HaloArgs {
+  const uint16_t* src;  // [N][H][32][64] bf16
+  const uint16_t* w;    // [64 n][3][3][64 k] bf16 (fwd: W[co][kh][kw][ci]; dgrad: Wt[ci][kh][kw][co])
+  int flip;             // dgrad: tap (kh, kw) uses weight tap (2-kh, 2-kw)
+  int N, H;             // H % 8 == 0
+  uint16_t* y;          // [N*H*32][ldy]
+  int ldy;
+  const uint16_t* add;  // [N*H*32][ldy] residual (nullable)
+  float* stats;         // rsum buffer for 2*64 values (nullable)
+  int tiles;
+};
+
+__global__ __launch_bounds__(NTH, 1) void conv3x3_c64_kernel(HaloArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[HALO_BYTES + W_BYTES];
+  uint8_t* Hs = smem;
+  uint8_t* Ws = smem + HALO_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int tiles_per_img = a.H / TR;
+
+  // ---- weights -> LDS, once (flip applied here, so the k-loop is tap-agnostic) ----
+  for (int q = tid; q < HC * 72; q += NTH) {
+    const int n = q / 72, c = q - n * 72;
+    const int tap = c >> 3, kc = c & 7;
+    const int wtap = a.flip ? 8 - tap : tap;
+    const uint4 v = *reinterpret_cast<const uint4*>(a.w + ((long)n * 9 + wtap) * HC + kc * 8);
+    *reinterpret_cast<uint4*>(Ws + (n * W_CH + c) * 16) = v;
+  }
+
+  // ---- halo tile: global -> registers (prefetch) -> LDS ----
+  uint4 hv[HALO_LOADS];
+  auto halo_load = [&](int tile) {
+    const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
+#pragma unroll
+    for (int i = 0; i < HALO_LOADS; ++i) {
+      const int q = tid + i * NTH;
+      const int pix = q >> 3, c = q & 7;
+      const int hr = pix / HCOL, hc = pix - hr * HCOL;
+      const int ih = r0 - 1 + hr, iw = hc - 1;
+      const bool ok = q < HALO_CHUNKS && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW;
+      hv[i] = ok ? *reinterpret_cast<const uint4*>(a.src + (((long)img * a.H + ih) * IW + iw) * HC + c * 8)
+                 : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto halo_store = [&]() {
+#pragma unroll
+    for (int i = 0; i < HALO_LOADS; ++i) {
+      const int q = tid + i * NTH;
+      if (q < HALO_CHUNKS) *reinterpret_cast<uint4*>(Hs + ((q >> 3) * PIX_CH + (q & 7)) * 16) = hv[i];
+    }
+  };
+
+  // ---- per-lane fragment addresses ----
+  // wave w owns tile pixels [64 w, 64 w + 64) = output rows 2w, 2w+1; m-fragment i covers
+  // row 2w + (i >> 1), columns 16 (i & 1) .. +15; lane (lg, lr) reads pixel column + lr,
+  // channels 8 lg .. +7 (+32 for the second k-step).
+  uint32_t a_base[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int orow = 2 * wave + (i >> 1), ocol = (i & 1) * 16 + lr;
+    a_base[i] = (uint32_t)(((orow * HCOL + ocol) * PIX_CH + lg) * 16);
+  }
+  const uint32_t b_base = (uint32_t)((lr * W_CH + lg) * 16);
+
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+
+  int t = blockIdx.x;
+  if (t < a.tiles) halo_load(t);
+  halo_store();
+  __syncthreads();
+  for (; t < a.tiles; t += gridDim.x) {
+    const int next = t + gridDim.x;
+    if (next < a.tiles) halo_load(next);  // lands under this tile's MFMAs
+
+    floatx4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        short8_t af[4], bf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + ((kh * HCOL + kw) * PIX_CH + ks * 4) * 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bf[j] = *reinterpret_cast<const short8_t*>(Ws + b_base + ((j * 16 * W_CH) + tap * 8 + ks * 4) * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+      }
+    }
+    __syncthreads();  // every wave is done with this halo
+
+    // ---- epilogue: statistics in registers, bf16 tile staged through LDS ----
+    if (a.stats) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = acc[i][j][r];
+            ssum[j] += v;
+            ssq[j] += v * v;
+          }
+    }
+    uint16_t* Cs = reinterpret_cast<uint16_t*>(Hs);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wave * 64 + i * 16 + 4 * lg + r) * OUT_LD + j * 16 + lr] = f2bf(acc[i][j][r]);
+    __syncthreads();
+    const long pix0 = (long)t * TPIX;  // tiles are whole 8-row bands: pixel index = tile * 256
+#pragma unroll
+    for (int k = 0; k < TPIX * 8 / NTH; ++k) {
+      const int q = tid + k * NTH;
+      const int p = q >> 3, c = (q & 7) * 8;
+      short8_t v = *reinterpret_cast<const short8_t*>(Cs + p * OUT_LD + c);
+      const long m = pix0 + p;
+      if (a.add) {
+        const short8_t ad = ld8(a.add + m * a.ldy + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (short)f2bf(bf2f((uint16_t)v[e]) + bf2f((uint16_t)ad[e]));
+      }
+      *reinterpret_cast<short8_t*>(a.y + m * a.ldy + c) = v;
+    }
+    __syncthreads();  // staging reads done before the next halo lands
+    if (next < a.tiles) {
+      halo_store();
+      __syncthreads();
+    }
+  }
+
+  if (a.stats) {
+    // lanes lg = 0..3 hold partials of channel 16 j + lr over different rows
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = ssum[j], q = ssq[j];
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (lg == 0) {
+        float* rep = rsum_replica(a.stats, 2 * HC);
+        atomicAdd(rep + j * 16 + lr, s);
+        atomicAdd(rep + HC + j * 16 + lr, q);
+      }
+    }
+    int* flag = reinterpret_cast<int*>(smem);
+    rsum_finish(a.stats, 2 * HC, flag);
+  }
+}
+
+static int g_halo_enabled = -1;  // -1: from SL_CONV_HALO (default on)
+static int g_num_cus = 0;
+
+extern "C" {
+
+int sl_conv_set_halo(int on) {
+  g_halo_enabled = on;
+  return 0;
+}
+
+// Whether the direct kernel serves this convolution (caller falls back to the implicit GEMM).
+int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldw) {
+  if (g_halo_enabled < 0) {
+    const char* e = getenv("SL_CONV_HALO");
+    g_halo_enabled = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_halo_enabled && KH == 3 && KW == 3 && stride == 1 && pad == 1 && W == IW && C == HC && cout == HC &&
+         ldw == HC && H > 0 && H % TR == 0;
+}
+
+int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int flip, int N, int H, uint16_t* y, int ldy,
+                   const uint16_t* add, float* stats, hipStream_t stream) {
+  if (N <= 0 || H <= 0 || H % TR || ldy < HC || (ldy & 7) || !y) return -1;
+  if ((((uintptr_t)src) | ((uintptr_t)w) | ((uintptr_t)y) | ((uintptr_t)add)) & 15) return -3;
+  if (g_num_cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
+      g_num_cus = 256;
+  }
+  HaloArgs a;
+  a.src = src; a.w = w; a.flip = flip; a.N = N; a.H = H; a.y = y; a.ldy = ldy; a.add = add; a.stats = stats;
+  a.tiles = N * (H / TR);
+  const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;  // persistent: one workgroup per CU (130 KB LDS)
+  hipLaunchKernelGGL(conv3x3_c64_kernel, dim3(grid), dim3(NTH), 0, stream, a);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"
