@@ -128,23 +128,37 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_c64_kernel(HaloArgs a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
+    // 18 k-steps (9 taps x 2 channel halves), software-pipelined by one step:
+    // the 8 fragment reads of step s+1 are issued ahead of step s's 16 MFMAs
+    // (ping-pong register sets, sched_barrier keeps the order).
+    short8_t a0[4], b0[4], a1[4], b1[4];
+    auto frag_reads = [&](int s, short8_t (&af)[4], short8_t (&bf)[4]) {
+      const int tap = s >> 1, ks = s & 1;
       const int kh = tap / 3, kw = tap - 3 * (tap / 3);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        short8_t af[4], bf[4];
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + ((kh * HCOL + kw) * PIX_CH + ks * 4) * 16);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + ((kh * HCOL + kw) * PIX_CH + ks * 4) * 16);
+      for (int j = 0; j < 4; ++j)
+        bf[j] = *reinterpret_cast<const short8_t*>(Ws + b_base + ((j * 16 * W_CH) + tap * 8 + ks * 4) * 16);
+    };
+    auto mfmas = [&](const short8_t (&af)[4], const short8_t (&bf)[4]) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          bf[j] = *reinterpret_cast<const short8_t*>(Ws + b_base + ((j * 16 * W_CH) + tap * 8 + ks * 4) * 16);
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+    };
+    frag_reads(0, a0, b0);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-      }
+    for (int s = 0; s < 18; s += 2) {
+      frag_reads(s + 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 2 < 18) frag_reads(s + 2, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // every wave is done with this halo
 
