@@ -33,6 +33,12 @@
 
 using namespace sl;
 
+#ifndef SL_WGRAD128_SLOTS
+#define SL_WGRAD128_SLOTS 2  // LDS ring slots of the 128-wide weight-gradient tile (2: two workgroups per CU)
+#endif
+#ifndef SL_GEMM128_SLOTS
+#define SL_GEMM128_SLOTS 2
+#endif
 namespace {
 constexpr int BK = 64;     // reduction depth per stage
 constexpr int WG_M = 64;   // wgrad: batch*pixel rows per stage
@@ -627,7 +633,7 @@ static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) 
   const int tiles_m = (g.M + BMv - 1) / BMv, tiles_n = (e.ncols + BNv - 1) / BNv;
   dim3 grid(tiles_m * tiles_n), block(256);
   // LDS ring sized for two workgroups per CU (<= 72 KB each)
-  if (BMv == 128 && BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 128, T, 2>), grid, block, 0, stream, g, e, tiles_n);
+  if (BMv == 128 && BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 128, T, SL_GEMM128_SLOTS>), grid, block, 0, stream, g, e, tiles_n);
   else if (BMv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 64, T, 3>), grid, block, 0, stream, g, e, tiles_n);
   else if (BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<64, 128, T, 3>), grid, block, 0, stream, g, e, tiles_n);
   else hipLaunchKernelGGL((conv_gemm_kernel<64, 64, T, 4>), grid, block, 0, stream, g, e, tiles_n);
@@ -638,7 +644,7 @@ static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) 
 extern "C" {
 // conv3x3_halo.hip: direct kernel for 3x3/s1/p1 64->64 convolutions on 32-wide images
 int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldw);
-int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int flip, int N, int H, uint16_t* y, int ldy,
+int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
                    const uint16_t* add, float* stats, hipStream_t stream);
 
 // Forward: x [N][H][W][C] -> y [N][OH][OW][ldy] (cols < cout), w [cout][KH][KW][C].
@@ -650,7 +656,7 @@ int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w
   if (y && (ldy < cout || (ldy & 7))) return -2;
   if ((g.K & 7) || (((uintptr_t)x | (uintptr_t)w) & 15)) return -3;
   if (y && !yf && !bias && OH == H && OW == W && sl_conv3x3_c64_applicable(H, W, C, cout, KH, KW, stride, pad, C))
-    return sl_conv3x3_c64(x, w, 0, N, H, y, ldy, nullptr, stats, stream);
+    return sl_conv3x3_c64(x, w, C, 0, N, H, y, ldy, nullptr, stats, stream);
   ConvEpi e{w, cout, y, ldy, yf, bias, nullptr, stats};
   return launch_gemm<false>(g, e, stream);
 }
@@ -663,8 +669,8 @@ int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint
   if (fill_geom(g, dy, N, OH, OW, ldd, H, W, KH, KW, stride, pad)) return -1;
   if (cin & 7) return -2;
   if (((uintptr_t)dy | (uintptr_t)wt) & 15) return -3;
-  if (H == OH && W == OW && sl_conv3x3_c64_applicable(OH, OW, ldd, cin, KH, KW, stride, pad, ldd))
-    return sl_conv3x3_c64(dy, wt, 1, N, OH, dx, cin, add, nullptr, stream);
+  if (H == OH && W == OW && ldd == 64 && sl_conv3x3_c64_applicable(OH, OW, ldd, cin, KH, KW, stride, pad, ldd))
+    return sl_conv3x3_c64(dy, wt, 64, 1, N, OH, dx, cin, add, nullptr, stream);
   ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr};
   return launch_gemm<true>(g, e, stream);
 }
@@ -691,7 +697,7 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   a.slices = (total_steps + a.steps_per_slice - 1) / a.steps_per_slice;
   dim3 grid(tiles * a.slices), block(256);
   if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3>), grid, block, 0, stream, a);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<128, 2>), grid, block, 0, stream, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS>), grid, block, 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }

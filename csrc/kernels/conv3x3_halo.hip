@@ -32,20 +32,35 @@
 using namespace sl;
 
 namespace {
-constexpr int HC = 64;                 // channels in = out
+constexpr int HC = 64;                 // output channels (and input channels of the 64-channel variant)
 constexpr int IW = 32;                 // image width
 constexpr int TR = 8;                  // output rows per tile
 constexpr int TPIX = TR * IW;          // 256 output pixels per tile
 constexpr int HR = TR + 2, HCOL = IW + 2;  // halo 10 x 34 pixels
-constexpr int PIX_CH = 10;             // 16-B chunks per halo pixel (8 data + 2 pad)
-constexpr int W_CH = 74;               // 16-B chunks per weight row (72 data + 2 pad)
-constexpr int HALO_BYTES = HR * HCOL * PIX_CH * 16;  // 54,400
-constexpr int W_BYTES = HC * W_CH * 16;              // 75,776
 constexpr int NTH = 256;
-constexpr int HALO_CHUNKS = HR * HCOL * 8;           // 2,720 data chunks
-constexpr int HALO_LOADS = (HALO_CHUNKS + NTH - 1) / NTH;  // 11 per thread
 constexpr int OUT_LD = 72;             // staging row stride (elements)
-static_assert(TPIX * OUT_LD * 2 <= HALO_BYTES, "output staging reuses the halo region");
+constexpr int STAGE_BYTES = TPIX * OUT_LD * 2;
+
+// Per input-channel-count layout.  CIN = 64 (layer 1): a 32-deep k-step is one
+// tap x 32 channels; 18 k-steps.  CIN = 8 (the CIFAR stem, 3 real channels
+// zero-padded to 8): a k-step is 4 taps x 8 channels -- lane group g of the
+// MFMA operand takes tap 4s + g -- so 3 k-steps cover the 9 taps (taps 9-11
+// have zero weights).  Pixel / weight-row strides in 16-B chunks are chosen
+// = 10 (mod 16) or brute-forced so ds_read_b128 lane groups stay (near)
+// conflict-free.
+template <int CIN>
+struct Lay {
+  static constexpr int DCH = CIN / 8;                    // data chunks per halo pixel
+  static constexpr int PIX_CH = CIN == 64 ? 10 : 1;      // chunks per halo pixel (with pad)
+  static constexpr int NKS = CIN == 64 ? 18 : 3;         // 32-deep k-steps
+  static constexpr int WROW = CIN == 64 ? 72 : 12;       // weight chunks per output channel
+  static constexpr int W_CH = CIN == 64 ? 74 : 14;       // ... with pad
+  static constexpr int HALO_CHUNKS = HR * HCOL * DCH;
+  static constexpr int HALO_LOADS = (HALO_CHUNKS + NTH - 1) / NTH;
+  static constexpr int HALO_BYTES = HR * HCOL * PIX_CH * 16;
+  static constexpr int REGION = HALO_BYTES > STAGE_BYTES ? HALO_BYTES : STAGE_BYTES;  // halo / output staging
+  static constexpr int W_BYTES = HC * W_CH * 16;
+};
 }  // namespace
 
 struct HaloArgs {
@@ -60,44 +75,48 @@ struct HaloArgs {
   int tiles;
 };
 
-__global__ __launch_bounds__(NTH, 1) void conv3x3_c64_kernel(HaloArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[HALO_BYTES + W_BYTES];
+template <int CIN>
+__global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
+  using L = Lay<CIN>;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[L::REGION + L::W_BYTES];
   uint8_t* Hs = smem;
-  uint8_t* Ws = smem + HALO_BYTES;
+  uint8_t* Ws = smem + L::REGION;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lg = lane >> 4;
   const int tiles_per_img = a.H / TR;
 
   // ---- weights -> LDS, once (flip applied here, so the k-loop is tap-agnostic) ----
-  for (int q = tid; q < HC * 72; q += NTH) {
-    const int n = q / 72, c = q - n * 72;
-    const int tap = c >> 3, kc = c & 7;
+  for (int q = tid; q < HC * L::WROW; q += NTH) {
+    const int n = q / L::WROW, c = q - n * L::WROW;
+    const int tap = c / L::DCH, kc = c - tap * L::DCH;
     const int wtap = a.flip ? 8 - tap : tap;
-    const uint4 v = *reinterpret_cast<const uint4*>(a.w + ((long)n * 9 + wtap) * HC + kc * 8);
-    *reinterpret_cast<uint4*>(Ws + (n * W_CH + c) * 16) = v;
+    const uint4 v = tap < 9 ? *reinterpret_cast<const uint4*>(a.w + ((long)n * 9 + wtap) * CIN + kc * 8)
+                            : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(Ws + (n * L::W_CH + c) * 16) = v;
   }
 
   // ---- halo tile: global -> registers (prefetch) -> LDS ----
-  uint4 hv[HALO_LOADS];
+  uint4 hv[L::HALO_LOADS];
   auto halo_load = [&](int tile) {
     const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
 #pragma unroll
-    for (int i = 0; i < HALO_LOADS; ++i) {
+    for (int i = 0; i < L::HALO_LOADS; ++i) {
       const int q = tid + i * NTH;
-      const int pix = q >> 3, c = q & 7;
+      const int pix = q / L::DCH, c = q - pix * L::DCH;
       const int hr = pix / HCOL, hc = pix - hr * HCOL;
       const int ih = r0 - 1 + hr, iw = hc - 1;
-      const bool ok = q < HALO_CHUNKS && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW;
-      hv[i] = ok ? *reinterpret_cast<const uint4*>(a.src + (((long)img * a.H + ih) * IW + iw) * HC + c * 8)
+      const bool ok = q < L::HALO_CHUNKS && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW;
+      hv[i] = ok ? *reinterpret_cast<const uint4*>(a.src + (((long)img * a.H + ih) * IW + iw) * CIN + c * 8)
                  : make_uint4(0, 0, 0, 0);
     }
   };
   auto halo_store = [&]() {
 #pragma unroll
-    for (int i = 0; i < HALO_LOADS; ++i) {
+    for (int i = 0; i < L::HALO_LOADS; ++i) {
       const int q = tid + i * NTH;
-      if (q < HALO_CHUNKS) *reinterpret_cast<uint4*>(Hs + ((q >> 3) * PIX_CH + (q & 7)) * 16) = hv[i];
+      const int pix = q / L::DCH, c = q - pix * L::DCH;
+      if (q < L::HALO_CHUNKS) *reinterpret_cast<uint4*>(Hs + (pix * L::PIX_CH + c) * 16) = hv[i];
     }
   };
 
@@ -105,13 +124,23 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_c64_kernel(HaloArgs a) {
   // wave w owns tile pixels [64 w, 64 w + 64) = output rows 2w, 2w+1; m-fragment i covers
   // row 2w + (i >> 1), columns 16 (i & 1) .. +15; lane (lg, lr) reads pixel column + lr,
   // channels 8 lg .. +7 (+32 for the second k-step).
+  // CIN = 8: lane group lg takes tap 4s + lg of k-step s (per-lane offset, taps >= 9 read
+  // pixel 0 against zero weights); CIN = 64: lg is the channel chunk.
   uint32_t a_base[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int orow = 2 * wave + (i >> 1), ocol = (i & 1) * 16 + lr;
-    a_base[i] = (uint32_t)(((orow * HCOL + ocol) * PIX_CH + lg) * 16);
+    a_base[i] = (uint32_t)(((orow * HCOL + ocol) * L::PIX_CH + (CIN == 64 ? lg : 0)) * 16);
   }
-  const uint32_t b_base = (uint32_t)((lr * W_CH + lg) * 16);
+  uint32_t toff[3] = {0u, 0u, 0u};
+  if (CIN == 8) {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int tap = 4 * s + lg;
+      toff[s] = tap < 9 ? (uint32_t)(((tap / 3) * HCOL + tap % 3) * L::PIX_CH * 16) : 0u;
+    }
+  }
+  const uint32_t b_base = (uint32_t)((lr * L::W_CH + lg) * 16);
 
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
 
@@ -133,14 +162,19 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_c64_kernel(HaloArgs a) {
     // (ping-pong register sets, sched_barrier keeps the order).
     short8_t a0[4], b0[4], a1[4], b1[4];
     auto frag_reads = [&](int s, short8_t (&af)[4], short8_t (&bf)[4]) {
-      const int tap = s >> 1, ks = s & 1;
-      const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+      if constexpr (CIN == 64) {
+        const int tap = s >> 1, ks = s & 1;
+        const int kh = tap / 3, kw = tap - 3 * (tap / 3);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + ((kh * HCOL + kw) * PIX_CH + ks * 4) * 16);
+        for (int i = 0; i < 4; ++i)
+          af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + ((kh * HCOL + kw) * L::PIX_CH + ks * 4) * 16);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + toff[s]);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        bf[j] = *reinterpret_cast<const short8_t*>(Ws + b_base + ((j * 16 * W_CH) + tap * 8 + ks * 4) * 16);
+        bf[j] = *reinterpret_cast<const short8_t*>(Ws + b_base + ((j * 16 * L::W_CH) + s * 4) * 16);
     };
     auto mfmas = [&](const short8_t (&af)[4], const short8_t (&bf)[4]) {
 #pragma unroll
@@ -150,14 +184,14 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_c64_kernel(HaloArgs a) {
     };
     frag_reads(0, a0, b0);
 #pragma unroll
-    for (int s = 0; s < 18; s += 2) {
-      frag_reads(s + 1, a1, b1);
+    for (int s = 0; s < L::NKS; s += 2) {
+      if (s + 1 < L::NKS) frag_reads(s + 1, a1, b1);
       __builtin_amdgcn_sched_barrier(0);
       mfmas(a0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 2 < 18) frag_reads(s + 2, a0, b0);
+      if (s + 2 < L::NKS) frag_reads(s + 2, a0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      mfmas(a1, b1);
+      if (s + 1 < L::NKS) mfmas(a1, b1);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // every wave is done with this halo
@@ -236,18 +270,23 @@ int sl_conv_set_halo(int on) {
 }
 
 // Whether the direct kernel serves this convolution (caller falls back to the implicit GEMM).
+// Whether the direct kernel serves this convolution: 3x3 / s1 / p1, 32-wide, 64 output channels,
+// 64 input channels (fwd + dgrad) or 8 (fwd only: the padded CIFAR stem); the caller falls back
+// to the implicit GEMM otherwise.
 int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldw) {
   if (g_halo_enabled < 0) {
     const char* e = getenv("SL_CONV_HALO");
     g_halo_enabled = (e && e[0] == '0') ? 0 : 1;
   }
-  return g_halo_enabled && KH == 3 && KW == 3 && stride == 1 && pad == 1 && W == IW && C == HC && cout == HC &&
-         ldw == HC && H > 0 && H % TR == 0;
+  return g_halo_enabled && KH == 3 && KW == 3 && stride == 1 && pad == 1 && W == IW && (C == HC || C == 8) &&
+         cout == HC && ldw == C && H > 0 && H % TR == 0;
 }
 
-int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int flip, int N, int H, uint16_t* y, int ldy,
+// cin: 64 (forward or, with flip, data gradient) or 8 (forward only).
+int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
                    const uint16_t* add, float* stats, hipStream_t stream) {
-  if (N <= 0 || H <= 0 || H % TR || ldy < HC || (ldy & 7) || !y) return -1;
+  if (N <= 0 || H <= 0 || H % TR || ldy < HC || (ldy & 7) || !y || (cin != 64 && cin != 8) || (cin == 8 && flip))
+    return -1;
   if ((((uintptr_t)src) | ((uintptr_t)w) | ((uintptr_t)y) | ((uintptr_t)add)) & 15) return -3;
   if (g_num_cus <= 0) {
     int dev = 0;
@@ -259,7 +298,8 @@ int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int flip, int N, int 
   a.src = src; a.w = w; a.flip = flip; a.N = N; a.H = H; a.y = y; a.ldy = ldy; a.add = add; a.stats = stats;
   a.tiles = N * (H / TR);
   const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;  // persistent: one workgroup per CU (130 KB LDS)
-  hipLaunchKernelGGL(conv3x3_c64_kernel, dim3(grid), dim3(NTH), 0, stream, a);
+  if (cin == 64) hipLaunchKernelGGL(conv3x3_kernel<64>, dim3(grid), dim3(NTH), 0, stream, a);
+  else hipLaunchKernelGGL(conv3x3_kernel<8>, dim3(grid), dim3(NTH), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -381,23 +381,24 @@ def test_resnet_bucketed_allreduce_hooks_cover_gradient_before_update():
     assert torch.allclose(b.params, expect, rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("n,h", [(3, 32), (5, 8)])
-def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h):
-    """conv3x3_halo.hip (3x3/s1/p1, 64->64, width 32) vs fp32 torch and vs the implicit GEMM."""
+@pytest.mark.parametrize("n,h,cin", [(3, 32, 64), (5, 8, 64), (3, 32, 8), (2, 16, 8)])
+def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h, cin):
+    """conv3x3_halo.hip (3x3/s1/p1 -> 64 channels, width 32; 64 input channels fwd + dgrad,
+    8 = the padded CIFAR stem fwd) vs fp32 torch and vs the implicit GEMM."""
     from serverless_learn_amd.ops import _native, cnn as K
 
     torch.manual_seed(1)
     c = 64
-    x = bf(torch.randn(n, h, 32, c, device=DEV))
-    w = bf(torch.randn(c, 3, 3, c, device=DEV) / math.sqrt(9 * c))
+    x = bf(torch.randn(n, h, 32, cin, device=DEV))
+    w = bf(torch.randn(c, 3, 3, cin, device=DEV) / math.sqrt(9 * cin))
     xr, wr = x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)
     ref = F.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1)
     dy = bf(torch.randn(n, h, 32, c, device=DEV))
     xg = xr.clone().requires_grad_(True)
     F.conv2d(xg, wr, padding=1).backward(dy.float().permute(0, 3, 1, 2))
     dx_ref = xg.grad.permute(0, 2, 3, 1)
-    wt = w.reshape(c, 9, c).permute(2, 1, 0).contiguous()  # [ci][tap][co]
-    add = bf(torch.randn(n, h, 32, c, device=DEV))
+    wt = w.reshape(c, 9, cin).permute(2, 1, 0).contiguous()  # [ci][tap][co]
+    add = bf(torch.randn(n, h, 32, cin, device=DEV))
 
     outs = {}
     try:
@@ -406,8 +407,9 @@ def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h):
             y = torch.zeros(n, h, 32, c, dtype=torch.bfloat16, device=DEV)
             sbuf = torch.zeros(K.rsum_floats(2 * c), device=DEV)
             K.conv_fwd(x, w, c, 3, 1, 1, y=y, stats=sbuf)
-            dx = torch.empty(n, h, 32, c, dtype=torch.bfloat16, device=DEV)
-            K.conv_dgrad(dy, wt.reshape(-1), c, 3, 1, 1, dx, add=add)
+            dx = torch.empty(n, h, 32, cin, dtype=torch.bfloat16, device=DEV)
+            if cin == 64:
+                K.conv_dgrad(dy, wt.reshape(-1), cin, 3, 1, 1, dx, add=add)
             torch.cuda.synchronize()
             outs[halo] = (y.float(), K.rsum_result(sbuf, 2 * c).clone(), dx.float())
     finally:
@@ -416,6 +418,8 @@ def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h):
     r2 = ref.reshape(-1, c)
     assert rel(y, ref) < 1.5e-2
     assert rel(st[:c], r2.sum(0)) < 1e-2 and rel(st[c:], (r2 * r2).sum(0)) < 1e-2
-    assert rel(dx - add.float(), dx_ref) < 2e-2
     # same bf16 products, fp32 sums in a different order: the two paths agree closely
-    assert rel(y, outs[0][0]) < 5e-3 and rel(dx, outs[0][2]) < 5e-3
+    assert rel(y, outs[0][0]) < 5e-3
+    if cin == 64:
+        assert rel(dx - add.float(), dx_ref) < 2e-2
+        assert rel(dx, outs[0][2]) < 5e-3
