@@ -55,8 +55,17 @@ struct ConvGeom {
   int KH, KW, stride, pad;
   int kw_magic;         // tap / KW == (tap * kw_magic) >> 16 for the tap counts used here
   int s_shift;          // log2(stride) (strides are powers of two)
-  int K;                // KH*KW*SC
+  int K;                // KH*KW*SC (phase mode: ntaps*SC)
   int M;                // N*OH*OW
+  int wld;              // B-operand row stride (elements): K, or KH*KW*SC in phase mode
+  // Phase mode (stride-2 3x3 data gradient): the GEMM covers only the
+  // output pixels (2i+ph, 2j+pw) of one parity class, whose gradient comes from
+  // a fixed subset of taps -- tap t reads dY[i+dh[t]][j+dw[t]] against weight
+  // tap tapw[t] -- so no MFMA is spent on the 3 of 4 taps that the plain
+  // transposed gather zeroes.  ph < 0: off.  OH/OW are then the parity-class
+  // grid and FH/FW the full output.
+  int ph, pw, ntaps, FH, FW;
+  int dh[4], dw[4], tapw[4];
 };
 
 struct ConvEpi {
@@ -137,6 +146,9 @@ __device__ __forceinline__ RowG row_gather(const ConvGeom& g, const Pix& p, int 
   if (!TRANSPOSED) {
     r.ih0 = p.oh * g.stride - g.pad;
     r.iw0 = p.ow * g.stride - g.pad;
+  } else if (g.ph >= 0) {
+    r.ih0 = p.oh;
+    r.iw0 = p.ow;
   } else {
     r.ih0 = p.oh + g.pad;
     r.iw0 = p.ow + g.pad;
@@ -148,7 +160,7 @@ __device__ __forceinline__ RowG row_gather(const ConvGeom& g, const Pix& p, int 
 template <bool TRANSPOSED>
 __device__ __forceinline__ const uint16_t* gather_tap(const ConvGeom& g, const RowG& r, int kh, int kw, int ch0) {
   int ih, iw;
-  if (!TRANSPOSED) {
+  if (!TRANSPOSED || g.ph >= 0) {  // phase mode: (kh, kw) carry the parity class's (dh, dw)
     ih = r.ih0 + kh;
     iw = r.iw0 + kw;
   } else {
@@ -234,15 +246,21 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
   for (int j = 0; j < PB; ++j) {
     const int row = 8 * (wave * PB + j) + (lane >> 3);
     const int col = n0 + row;
-    pb[j] = col < e.ncols ? e.w + (long)col * g.K : nullptr;
+    pb[j] = col < e.ncols ? e.w + (long)col * g.wld : nullptr;
     cb[j] = swz64(lane & 7, row);
   }
   auto issue = [&](int kt) {
     uint16_t* As = smem + (kt % NSLOT) * SLOT;
     uint16_t* Bs = As + BM * BK;
+    int kb = kt * BK;  // B-operand column of this stage
     if (uniform_tap) {
       const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
-      const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
+      int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
+      if (TRANSPOSED && g.ph >= 0) {
+        kh = g.dh[tap];
+        kw = g.dw[tap];
+        kb = g.tapw[tap] * g.SC + ch0;
+      }
 #pragma unroll
       for (int j = 0; j < PA; ++j)
         glds16(gather_tap<TRANSPOSED>(g, ra[j], kh, kw, ch0), (SL_LDS void*)(As + (wave * PA + j) * 8 * BK));
@@ -254,7 +272,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
       const int k0 = kt * BK + cb[j] * 8;
-      glds16((pb[j] && k0 < g.K) ? pb[j] + k0 : g_conv_zero, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK));
+      glds16((pb[j] && k0 < g.K) ? pb[j] + (kb + cb[j] * 8) : g_conv_zero, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK));
     }
   };
 
@@ -368,10 +386,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     const int row = m0 + rl, col = n0 + cc;
     if (row >= g.M || col >= e.ncols) continue;
     short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
-    uint16_t* dst = e.y + (long)row * e.ldy + col;
+    long orow = row;  // phase mode: parity-class pixel -> full-output pixel
+    if (TRANSPOSED && g.ph >= 0) {
+      const Pix q = decode_pix(g, row);
+      orow = ((long)q.n * g.FH + 2 * q.oh + g.ph) * g.FW + 2 * q.ow + g.pw;
+    }
+    uint16_t* dst = e.y + orow * e.ldy + col;
     if (col + 8 <= e.ncols) {
       if (e.add) {
-        const short8_t a = ld8(e.add + (long)row * e.ldy + col);
+        const short8_t a = ld8(e.add + orow * e.ldy + col);
 #pragma unroll
         for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)a[t]));
       }
@@ -379,7 +402,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     } else {
       for (int t = 0; t < 8 && col + t < e.ncols; ++t) {
         float f = bf2f((uint16_t)v[t]);
-        if (e.add) f += bf2f(e.add[(long)row * e.ldy + col + t]);
+        if (e.add) f += bf2f(e.add[orow * e.ldy + col + t]);
         dst[t] = f2bf(f);
       }
     }
@@ -616,6 +639,11 @@ static int fill_geom(ConvGeom& g, const uint16_t* src, int N, int SH, int SW, in
   g.kw_magic = (65536 + KW - 1) / KW;  // exact for tap < 65536 / KW^2 (taps here <= 49)
   g.s_shift = ilog2(stride);
   g.K = KH * KW * SC;
+  g.wld = g.K;
+  g.ph = g.pw = -1;
+  g.ntaps = 0;
+  g.FH = OH;
+  g.FW = OW;
   const long M = (long)N * OH * OW;
   if (g.c_shift < 3 || M <= 0 || M > (1L << 30) || g.s_shift < 0 || OH <= 0 || OW <= 0 || KH * KW > 64) return -1;
   g.M = (int)M;
@@ -641,7 +669,13 @@ static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) 
   return 0;
 }
 
+static int g_conv_phase = 1;  // stride-2 dgrad by parity classes (sl_conv_set_phase)
+
 extern "C" {
+int sl_conv_set_phase(int on) {
+  g_conv_phase = on;
+  return 0;
+}
 // conv3x3_halo.hip: direct kernel for 3x3/s1/p1 64->64 convolutions on 32-wide images
 int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldw);
 int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
@@ -672,6 +706,28 @@ int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint
   if (H == OH && W == OW && ldd == 64 && sl_conv3x3_c64_applicable(OH, OW, ldd, cin, KH, KW, stride, pad, ldd))
     return sl_conv3x3_c64(dy, wt, 64, 1, N, OH, dx, cin, add, nullptr, stream);
   ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr};
+  if (g_conv_phase && stride == 2 && KH == 3 && KW == 3 && pad == 1 && (ldd & 63) == 0) {
+    // four parity classes of dX, each a dense GEMM over its own taps (1, 2, 2, 4 of the 9)
+    for (int ph = 0; ph < 2; ++ph)
+      for (int pw = 0; pw < 2; ++pw) {
+        ConvGeom q = g;
+        const int Hp = (H - ph + 1) / 2, Wp = (W - pw + 1) / 2;
+        if (Hp <= 0 || Wp <= 0) continue;
+        q.OH = Hp; q.OW = Wp; q.hw_shift = ilog2(Hp * Wp); q.w_shift = ilog2(Wp); q.M = N * Hp * Wp;
+        q.ph = ph; q.pw = pw; q.FH = H; q.FW = W; q.wld = 9 * ldd;
+        int t = 0;
+        for (int kh = 1 - ph; kh < 3; kh += 2)
+          for (int kw = 1 - pw; kw < 3; kw += 2) {
+            q.dh[t] = (ph + 1 - kh) / 2; q.dw[t] = (pw + 1 - kw) / 2; q.tapw[t] = kh * 3 + kw;
+            ++t;
+          }
+        q.ntaps = t;
+        q.K = t * ldd;
+        const int rc = launch_gemm<true>(q, e, stream);
+        if (rc) return rc;
+      }
+    return 0;
+  }
   return launch_gemm<true>(g, e, stream);
 }
 

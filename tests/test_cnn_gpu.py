@@ -30,6 +30,7 @@ CONV_CASES = [
     (2, 20, 8, 64, 7, 2, 3),     # ImageNet-style stem
     (8, 1, 512, 10, 1, 1, 0),    # FC as a 1x1 conv (cout not a multiple of 8)
     (2, 4, 512, 512, 3, 1, 1),
+    (3, 7, 64, 64, 3, 2, 1),     # stride-2 dgrad by parity classes, odd extent (4 + 3 rows)
 ]
 
 
