@@ -680,6 +680,8 @@ int sl_conv_set_phase(int on) {
 int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldw);
 int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
                    const uint16_t* add, float* stats, hipStream_t stream);
+int sl_conv3x3_wgrad_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldy);
+int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, hipStream_t stream);
 
 // Forward: x [N][H][W][C] -> y [N][OH][OW][ldy] (cols < cout), w [cout][KH][KW][C].
 int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w, int cout, int KH, int KW,
@@ -739,6 +741,8 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   if (fill_geom(a.g, x, N, H, W, C, OH, OW, KH, KW, stride, pad)) return -1;
   if ((ldy & 7) || ldy < cout) return -2;
   if (((uintptr_t)x | (uintptr_t)dy) & 15) return -3;
+  if (OH == H && OW == W && sl_conv3x3_wgrad_c64_applicable(H, W, C, cout, KH, KW, stride, pad, ldy))
+    return sl_conv3x3_wgrad_c64(x, dy, ldy, N, H, dw, stream);
   a.dy = dy; a.ldy = ldy; a.cout = cout; a.dw = dw;
   const int BMO = cout <= 64 ? 64 : 128;
   a.tiles_co = (cout + BMO - 1) / BMO;

@@ -305,3 +305,201 @@ int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, in
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Weight gradient of the same 3x3 / s1 / p1 64 -> 64 convolution:
+//   dW[co][tap][ci] += sum_p dY[p][co] X[p + off(tap)][ci]
+// GEMM with M = co (64), N = (tap, ci) (576), K = pixels.  One persistent
+// workgroup per CU walks 8-row x 32-column pixel tiles: dY tile (256 px) and
+// the 10 x 34 X halo land in LDS (register-prefetched one tile ahead), and a
+// k-step of 32 pixels is exactly one output row, so every operand fragment is
+// two ds_read_b64_tr_b16 at constant offsets from a per-lane base: tap (kh, kw)
+// shifts the X rows by 34 kh + kw pixels.  8 waves (two per SIMD): wave w owns
+// channels ci 16 (w & 3) .. +15 of taps 0-4 (w < 4) or 5-8, i.e. 20 or 16
+// accumulator tiles; the workgroup's partial dW is added with fp32 atomics
+// once at the end (one adder per CU per address).
+// Pixel stride 144 B: the worst tr-read lane half is 2-way (brute-forced); the
+// implicit-GEMM path re-gathered X 9 times through LDS-DMA instead.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int WNT = 512;                    // threads
+constexpr int WPS = 144;                    // pixel stride (bytes) of both LDS images
+constexpr int WX_BYTES = HR * HCOL * WPS;   // 48,960
+constexpr int WY_BYTES = TPIX * WPS;        // 36,864
+constexpr int WX_CHUNKS = HR * HCOL * 8, WY_CHUNKS = TPIX * 8;
+constexpr int WLOADS = (WX_CHUNKS + WY_CHUNKS + WNT - 1) / WNT;  // 10 x 16 B per thread
+}  // namespace
+
+struct WgradHaloArgs {
+  const uint16_t* x;   // [N][H][32][64]
+  const uint16_t* dy;  // [N][H][32][ldy]
+  int ldy;
+  int N, H, tiles;
+  float* dw;           // [64][9][64] fp32, accumulated
+};
+
+template <int OFF>
+__device__ __forceinline__ short4_t tr16_at(uint32_t a) {
+  short4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+template <int OFF0, int OFF1>
+__device__ __forceinline__ short8_t tr16_frag(uint32_t a) {
+  const short4_t lo = tr16_at<OFF0>(a), hi = tr16_at<OFF1>(a);
+  short8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+// X fragment for tap T at output row S: halo pixel (S + T / 3, col + T % 3)
+template <int S, int T>
+__device__ __forceinline__ short8_t xfrag(uint32_t xb) {
+  return tr16_frag<((S + T / 3) * HCOL + T % 3) * WPS, ((S + T / 3) * HCOL + T % 3 + 4) * WPS>(xb);
+}
+template <int S, int I>
+__device__ __forceinline__ short8_t yfrag(uint32_t yb) {
+  return tr16_frag<(S * 32) * WPS + 32 * I, (S * 32 + 4) * WPS + 32 * I>(yb);
+}
+
+template <int T0, int NTAP>
+__device__ __forceinline__ void wgrad_tile_mfmas(uint32_t xb, uint32_t yb, floatx4_t (&acc)[4][5]) {
+  auto kstep = [&](auto s_c) {
+    constexpr int S = decltype(s_c)::value;
+    short8_t af[4], bf[5];
+    af[0] = yfrag<S, 0>(yb);
+    af[1] = yfrag<S, 1>(yb);
+    af[2] = yfrag<S, 2>(yb);
+    af[3] = yfrag<S, 3>(yb);
+    bf[0] = xfrag<S, T0 + 0>(xb);
+    bf[1] = xfrag<S, T0 + 1>(xb);
+    bf[2] = xfrag<S, T0 + 2>(xb);
+    bf[3] = xfrag<S, T0 + 3>(xb);
+    if constexpr (NTAP > 4) bf[4] = xfrag<S, T0 + 4>(xb);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < NTAP; ++t) acc[i][t] = mfma16(af[i], bf[t], acc[i][t]);
+  };
+  kstep(std::integral_constant<int, 0>{});
+  kstep(std::integral_constant<int, 1>{});
+  kstep(std::integral_constant<int, 2>{});
+  kstep(std::integral_constant<int, 3>{});
+  kstep(std::integral_constant<int, 4>{});
+  kstep(std::integral_constant<int, 5>{});
+  kstep(std::integral_constant<int, 6>{});
+  kstep(std::integral_constant<int, 7>{});
+}
+
+__global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[WX_BYTES + WY_BYTES];
+  uint8_t* Xs = smem;
+  uint8_t* Ys = smem + WX_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cb = wave & 3, th = wave >> 2;
+  const int lg = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int tiles_per_img = a.H / TR;
+
+  uint4 pv[WLOADS];
+  auto tile_load = [&](int tile) {
+    const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
+#pragma unroll
+    for (int i = 0; i < WLOADS; ++i) {
+      const int c = tid + i * WNT;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (c < WX_CHUNKS) {
+        const int pix = c >> 3, ch = c & 7;
+        const int hr = pix / HCOL, hc = pix - hr * HCOL;
+        const int ih = r0 - 1 + hr, iw = hc - 1;
+        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW)
+          v = *reinterpret_cast<const uint4*>(a.x + (((long)img * a.H + ih) * IW + iw) * HC + ch * 8);
+      } else if (c < WX_CHUNKS + WY_CHUNKS) {
+        const int cc = c - WX_CHUNKS, pix = cc >> 3, ch = cc & 7;
+        v = *reinterpret_cast<const uint4*>(a.dy + ((long)tile * TPIX + pix) * a.ldy + ch * 8);
+      }
+      pv[i] = v;
+    }
+  };
+  auto tile_store = [&]() {
+#pragma unroll
+    for (int i = 0; i < WLOADS; ++i) {
+      const int c = tid + i * WNT;
+      if (c < WX_CHUNKS) {
+        *reinterpret_cast<uint4*>(Xs + (c >> 3) * WPS + (c & 7) * 16) = pv[i];
+      } else if (c < WX_CHUNKS + WY_CHUNKS) {
+        const int cc = c - WX_CHUNKS;
+        *reinterpret_cast<uint4*>(Ys + (cc >> 3) * WPS + (cc & 7) * 16) = pv[i];
+      }
+    }
+  };
+
+  // tr16 lane addressing: rows = pixels 8 lg + q (+4 for the second read), columns = 4 p .. 4 p + 3
+  const uint32_t xb = (uint32_t)(uintptr_t)(SL_LDS const uint8_t*)Xs + (uint32_t)((8 * lg + q) * WPS + (16 * cb + 4 * p) * 2);
+  const uint32_t yb = (uint32_t)(uintptr_t)(SL_LDS const uint8_t*)Ys + (uint32_t)((8 * lg + q) * WPS + 4 * p * 2);
+
+  floatx4_t acc[4][5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 5; ++t) acc[i][t] = zero4();
+
+  // The tile loop is instantiated per tap half and selected by a scalar branch outside it.
+  auto run = [&](auto t0_c) {
+    constexpr int T0 = decltype(t0_c)::value, NTAP = T0 == 0 ? 5 : 4;
+    int tile = blockIdx.x;
+    if (tile < a.tiles) tile_load(tile);
+    tile_store();
+    __syncthreads();
+    for (; tile < a.tiles; tile += gridDim.x) {
+      const int next = tile + gridDim.x;
+      if (next < a.tiles) tile_load(next);
+      wgrad_tile_mfmas<T0, NTAP>(xb, yb, acc);
+      __syncthreads();  // all waves done with this tile's images
+      if (next < a.tiles) {
+        tile_store();
+        __syncthreads();
+      }
+    }
+    // acc[i][t]: lane (lg, lr) holds dW[co = 16 i + 4 lg + r][tap T0 + t][ci = 16 cb + lr]
+    const int lr = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          atomicAdd(a.dw + ((long)(16 * i + 4 * lg + r) * 9 + T0 + t) * HC + 16 * cb + lr, acc[i][t][r]);
+  };
+  if (th == 0) run(std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, 5>{});
+}
+
+extern "C" {
+
+int sl_conv3x3_wgrad_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldy) {
+  return sl_conv3x3_c64_applicable(H, W, C, cout, KH, KW, stride, pad, C) && C == HC && ldy == HC;
+}
+
+int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw,
+                         hipStream_t stream) {
+  if (N <= 0 || H <= 0 || H % TR || ldy != HC || !dw) return -1;
+  if ((((uintptr_t)x) | ((uintptr_t)dy)) & 15) return -3;
+  if (g_num_cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
+      g_num_cus = 256;
+  }
+  WgradHaloArgs a;
+  a.x = x; a.dy = dy; a.ldy = ldy; a.N = N; a.H = H; a.dw = dw;
+  a.tiles = N * (H / TR);
+  const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;
+  hipLaunchKernelGGL(conv3x3_wgrad_c64_kernel, dim3(grid), dim3(WNT), 0, stream, a);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

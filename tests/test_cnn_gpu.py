@@ -401,6 +401,10 @@ def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h, cin):
     wt = w.reshape(c, 9, cin).permute(2, 1, 0).contiguous()  # [ci][tap][co]
     add = bf(torch.randn(n, h, 32, cin, device=DEV))
 
+    wg = wr.clone().requires_grad_(True)
+    F.conv2d(xr, wg, padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    dw_ref = wg.grad.permute(0, 2, 3, 1)
+
     outs = {}
     try:
         for halo in (1, 0):
@@ -409,13 +413,17 @@ def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h, cin):
             sbuf = torch.zeros(K.rsum_floats(2 * c), device=DEV)
             K.conv_fwd(x, w, c, 3, 1, 1, y=y, stats=sbuf)
             dx = torch.empty(n, h, 32, cin, dtype=torch.bfloat16, device=DEV)
+            dw = torch.full((c, 3, 3, cin), 0.25, device=DEV)  # accumulates onto what is there
             if cin == 64:
                 K.conv_dgrad(dy, wt.reshape(-1), cin, 3, 1, 1, dx, add=add)
+            K.conv_wgrad(x, dy, c, 3, 1, 1, dw)
             torch.cuda.synchronize()
-            outs[halo] = (y.float(), K.rsum_result(sbuf, 2 * c).clone(), dx.float())
+            outs[halo] = (y.float(), K.rsum_result(sbuf, 2 * c).clone(), dx.float(), dw - 0.25)
     finally:
         _native.call("sl_conv_set_halo", 1)
-    y, st, dx = outs[1]
+    y, st, dx, dw = outs[1]
+    assert rel(dw, dw_ref) < 1e-2
+    assert rel(dw, outs[0][3]) < 1e-3
     r2 = ref.reshape(-1, c)
     assert rel(y, ref) < 1.5e-2
     assert rel(st[:c], r2.sum(0)) < 1e-2 and rel(st[c:], (r2 * r2).sum(0)) < 1e-2
