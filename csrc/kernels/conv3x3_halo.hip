@@ -38,6 +38,12 @@ constexpr int TR = 8;                  // output rows per tile
 constexpr int TPIX = TR * IW;          // 256 output pixels per tile
 constexpr int HR = TR + 2, HCOL = IW + 2;  // halo 10 x 34 pixels
 constexpr int NTH = 256;
+#ifndef SL_HALO_WAVES
+#define SL_HALO_WAVES 8  // 8 measured +1% over 4 (two waves per SIMD)
+#endif
+constexpr int NWF = SL_HALO_WAVES;     // waves of the forward / dgrad kernel
+constexpr int NTF = 64 * NWF;
+constexpr int MF = TPIX / NWF / 16;    // m-fragments (16 output pixels) per wave
 constexpr int OUT_LD = 72;             // staging row stride (elements)
 constexpr int STAGE_BYTES = TPIX * OUT_LD * 2;
 
@@ -56,7 +62,6 @@ struct Lay {
   static constexpr int WROW = CIN == 64 ? 72 : 12;       // weight chunks per output channel
   static constexpr int W_CH = CIN == 64 ? 74 : 14;       // ... with pad
   static constexpr int HALO_CHUNKS = HR * HCOL * DCH;
-  static constexpr int HALO_LOADS = (HALO_CHUNKS + NTH - 1) / NTH;
   static constexpr int HALO_BYTES = HR * HCOL * PIX_CH * 16;
   static constexpr int REGION = HALO_BYTES > STAGE_BYTES ? HALO_BYTES : STAGE_BYTES;  // halo / output staging
   static constexpr int W_BYTES = HC * W_CH * 16;
@@ -76,8 +81,9 @@ struct HaloArgs {
 };
 
 template <int CIN>
-__global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
+__global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   using L = Lay<CIN>;
+  constexpr int HL = (L::HALO_CHUNKS + NTF - 1) / NTF;  // halo chunks per thread
   __shared__ __attribute__((aligned(16))) uint8_t smem[L::REGION + L::W_BYTES];
   uint8_t* Hs = smem;
   uint8_t* Ws = smem + L::REGION;
@@ -87,7 +93,7 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
   const int tiles_per_img = a.H / TR;
 
   // ---- weights -> LDS, once (flip applied here, so the k-loop is tap-agnostic) ----
-  for (int q = tid; q < HC * L::WROW; q += NTH) {
+  for (int q = tid; q < HC * L::WROW; q += NTF) {
     const int n = q / L::WROW, c = q - n * L::WROW;
     const int tap = c / L::DCH, kc = c - tap * L::DCH;
     const int wtap = a.flip ? 8 - tap : tap;
@@ -97,12 +103,12 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
   }
 
   // ---- halo tile: global -> registers (prefetch) -> LDS ----
-  uint4 hv[L::HALO_LOADS];
+  uint4 hv[HL];
   auto halo_load = [&](int tile) {
     const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
 #pragma unroll
-    for (int i = 0; i < L::HALO_LOADS; ++i) {
-      const int q = tid + i * NTH;
+    for (int i = 0; i < HL; ++i) {
+      const int q = tid + i * NTF;
       const int pix = q / L::DCH, c = q - pix * L::DCH;
       const int hr = pix / HCOL, hc = pix - hr * HCOL;
       const int ih = r0 - 1 + hr, iw = hc - 1;
@@ -113,8 +119,8 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
   };
   auto halo_store = [&]() {
 #pragma unroll
-    for (int i = 0; i < L::HALO_LOADS; ++i) {
-      const int q = tid + i * NTH;
+    for (int i = 0; i < HL; ++i) {
+      const int q = tid + i * NTF;
       const int pix = q / L::DCH, c = q - pix * L::DCH;
       if (q < L::HALO_CHUNKS) *reinterpret_cast<uint4*>(Hs + (pix * L::PIX_CH + c) * 16) = hv[i];
     }
@@ -126,10 +132,11 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
   // channels 8 lg .. +7 (+32 for the second k-step).
   // CIN = 8: lane group lg takes tap 4s + lg of k-step s (per-lane offset, taps >= 9 read
   // pixel 0 against zero weights); CIN = 64: lg is the channel chunk.
-  uint32_t a_base[4];
+  uint32_t a_base[MF];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int orow = 2 * wave + (i >> 1), ocol = (i & 1) * 16 + lr;
+  for (int i = 0; i < MF; ++i) {
+    const int px = wave * (TPIX / NWF) + 16 * i;
+    const int orow = px / IW, ocol = px % IW + lr;
     a_base[i] = (uint32_t)(((orow * HCOL + ocol) * L::PIX_CH + (CIN == 64 ? lg : 0)) * 16);
   }
   uint32_t toff[3] = {0u, 0u, 0u};
@@ -152,33 +159,33 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
     const int next = t + gridDim.x;
     if (next < a.tiles) halo_load(next);  // lands under this tile's MFMAs
 
-    floatx4_t acc[4][4];
+    floatx4_t acc[MF][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MF; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
     // 18 k-steps (9 taps x 2 channel halves), software-pipelined by one step:
     // the 8 fragment reads of step s+1 are issued ahead of step s's 16 MFMAs
     // (ping-pong register sets, sched_barrier keeps the order).
-    short8_t a0[4], b0[4], a1[4], b1[4];
-    auto frag_reads = [&](int s, short8_t (&af)[4], short8_t (&bf)[4]) {
+    short8_t a0[MF], b0[4], a1[MF], b1[4];
+    auto frag_reads = [&](int s, short8_t (&af)[MF], short8_t (&bf)[4]) {
       if constexpr (CIN == 64) {
         const int tap = s >> 1, ks = s & 1;
         const int kh = tap / 3, kw = tap - 3 * (tap / 3);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < MF; ++i)
           af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + ((kh * HCOL + kw) * L::PIX_CH + ks * 4) * 16);
       } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + toff[s]);
+        for (int i = 0; i < MF; ++i) af[i] = *reinterpret_cast<const short8_t*>(Hs + a_base[i] + toff[s]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         bf[j] = *reinterpret_cast<const short8_t*>(Ws + b_base + ((j * 16 * L::W_CH) + s * 4) * 16);
     };
-    auto mfmas = [&](const short8_t (&af)[4], const short8_t (&bf)[4]) {
+    auto mfmas = [&](const short8_t (&af)[MF], const short8_t (&bf)[4]) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MF; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
     };
@@ -201,7 +208,7 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < MF; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float v = acc[i][j][r];
@@ -211,17 +218,17 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_kernel(HaloArgs a) {
     }
     uint16_t* Cs = reinterpret_cast<uint16_t*>(Hs);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MF; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          Cs[(wave * 64 + i * 16 + 4 * lg + r) * OUT_LD + j * 16 + lr] = f2bf(acc[i][j][r]);
+          Cs[(wave * (TPIX / NWF) + i * 16 + 4 * lg + r) * OUT_LD + j * 16 + lr] = f2bf(acc[i][j][r]);
     __syncthreads();
     const long pix0 = (long)t * TPIX;  // tiles are whole 8-row bands: pixel index = tile * 256
 #pragma unroll
-    for (int k = 0; k < TPIX * 8 / NTH; ++k) {
-      const int q = tid + k * NTH;
+    for (int k = 0; k < TPIX * 8 / NTF; ++k) {
+      const int q = tid + k * NTF;
       const int p = q >> 3, c = (q & 7) * 8;
       short8_t v = *reinterpret_cast<const short8_t*>(Cs + p * OUT_LD + c);
       const long m = pix0 + p;
@@ -298,8 +305,8 @@ int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, in
   a.src = src; a.w = w; a.flip = flip; a.N = N; a.H = H; a.y = y; a.ldy = ldy; a.add = add; a.stats = stats;
   a.tiles = N * (H / TR);
   const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;  // persistent: one workgroup per CU (130 KB LDS)
-  if (cin == 64) hipLaunchKernelGGL(conv3x3_kernel<64>, dim3(grid), dim3(NTH), 0, stream, a);
-  else hipLaunchKernelGGL(conv3x3_kernel<8>, dim3(grid), dim3(NTH), 0, stream, a);
+  if (cin == 64) hipLaunchKernelGGL(conv3x3_kernel<64>, dim3(grid), dim3(NTF), 0, stream, a);
+  else hipLaunchKernelGGL(conv3x3_kernel<8>, dim3(grid), dim3(NTF), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
