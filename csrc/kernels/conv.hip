@@ -36,6 +36,12 @@ using namespace sl;
 #ifndef SL_WGRAD128_SLOTS
 #define SL_WGRAD128_SLOTS 2  // LDS ring slots of the 128-wide weight-gradient tile (2: two workgroups per CU)
 #endif
+#ifndef SL_WGRAD128_KS
+#define SL_WGRAD128_KS 1
+#endif
+#ifndef SL_WGRAD128_KS2_SLOTS
+#define SL_WGRAD128_KS2_SLOTS 4
+#endif
 #ifndef SL_GEMM128_SLOTS
 #define SL_GEMM128_SLOTS 2
 #endif
@@ -451,22 +457,28 @@ struct WgradArgs {
   int tiles_k, tiles_co, slices, steps_per_slice;
 };
 
-template <int BMO, int NSLOT>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
+// KS = 2: 8 waves, waves 4-7 take the second 32 pixels of every 64-pixel stage
+// (two waves per SIMD inside one workgroup); the k-halves are summed through LDS.
+template <int BMO, int NSLOT, int KS>
+__global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
   constexpr int BNO = 128;
   constexpr int WA = BMO / 8, WB = BNO / 8;       // 16-B chunks per image row
   constexpr int MT = BMO / 32, NT = BNO / 32;     // per-wave MFMA tiles (2x2 waves)
   constexpr int RA = 64 / WA, RB = 64 / WB;       // rows per 1-KB DMA piece
-  constexpr int PA = (WG_M / RA) / 4, PB = (WG_M / RB) / 4;  // pieces per wave per stage
+  constexpr int NTW = 256 * KS;
+  constexpr int PA = (WG_M / RA) / (4 * KS), PB = (WG_M / RB) / (4 * KS);  // pieces per wave per stage
   constexpr int PS = PA + PB;
   constexpr int IMG_A = WG_M * BMO, IMG_B = WG_M * BNO;      // elements
   constexpr int SLOT = IMG_A + IMG_B;
   constexpr int OUT_LD = BNO + 4;
   constexpr int SMEM = NSLOT * SLOT > BMO * OUT_LD * 2 ? NSLOT * SLOT : BMO * OUT_LD * 2;  // ring / fp32 epilogue
+  static_assert(PA >= 1 && PB >= 1, "pieces per wave");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
   const ConvGeom& g = a.g;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = wave >> 2, w4 = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles = a.tiles_k * a.tiles_co;
@@ -474,7 +486,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   const int t = logical - s * tiles;
   const int tco = t / a.tiles_k, tk = t - tco * a.tiles_k;
   const int co0 = tco * BMO, k0 = tk * BNO;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = w4 >> 1, wn = w4 & 1;
   const int mbeg = s * a.steps_per_slice * WG_M;
   const int nst = min(a.steps_per_slice, (g.M - mbeg + WG_M - 1) / WG_M);
 
@@ -551,23 +563,43 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
     };
-    half(std::integral_constant<int, 0>{});
-    half(std::integral_constant<int, 1>{});
+    if constexpr (KS == 1) {
+      half(std::integral_constant<int, 0>{});
+      half(std::integral_constant<int, 1>{});
+    } else if (kg == 0) {
+      half(std::integral_constant<int, 0>{});
+    } else {
+      half(std::integral_constant<int, 1>{});
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   // fp32 tile through LDS so each wave's atomics cover 256 contiguous bytes
   float* Os = reinterpret_cast<float*>(smem);
+  if (kg == KS - 1) {
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+      for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Os[(wm * (BMO / 2) + i * 16 + 4 * lg + r) * OUT_LD + wn * (BNO / 2) + j * 16 + lr] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r)
+          Os[(wm * (BMO / 2) + i * 16 + 4 * lg + r) * OUT_LD + wn * (BNO / 2) + j * 16 + lr] = acc[i][j][r];
+  }
+  if (KS == 2) {
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Os[(wm * (BMO / 2) + i * 16 + 4 * lg + r) * OUT_LD + wn * (BNO / 2) + j * 16 + lr] += acc[i][j][r];
+    }
+  }
   __syncthreads();
-  for (int q = tid; q < BMO * BNO; q += 256) {
+  for (int q = tid; q < BMO * BNO; q += NTW) {
     const int rl = q >> 7, cl = q & 127;
     const int co = co0 + rl, k = k0 + cl;
     if (co < a.cout && k < g.K) {
@@ -755,9 +787,11 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   if (slices < 1) slices = 1;
   a.steps_per_slice = (total_steps + slices - 1) / slices;
   a.slices = (total_steps + a.steps_per_slice - 1) / a.steps_per_slice;
-  dim3 grid(tiles * a.slices), block(256);
-  if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3>), grid, block, 0, stream, a);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS>), grid, block, 0, stream, a);
+  dim3 grid(tiles * a.slices);
+  if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3, 1>), grid, dim3(256), 0, stream, a);
+  else if (SL_WGRAD128_KS == 2)
+    hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_KS2_SLOTS, 2>), grid, dim3(512), 0, stream, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS, 1>), grid, dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
