@@ -44,6 +44,7 @@ class Config:
     max_misses: int = 3                # evict after this many failed heartbeats
     max_message_bytes: int = 256 << 20
     rendezvous_port: int = 0           # master's collective rendezvous store (0 = pick free)
+    metrics_port: int = 0              # > 0: serve Prometheus /metrics on this port (0 = off)
     # --- worker training ---
     sync: str = "allreduce"            # allreduce | gossip | ps | none
     gossip_compat: bool = False        # reproduce the reference's alpha^2 echo exactly

@@ -31,6 +31,7 @@ from ..ckpt.format import CKPT_BASE
 from ..data.synthetic import make_shard
 from ..proto import messages as pb
 from ..utils.log import Logger
+from ..utils.metrics import Metrics
 from ..wire.codec import chunk_payload, iter_chunks
 from .transport import Channels, RpcFailure, RpcServer, metadata_dict
 
@@ -42,7 +43,8 @@ class FileServer:
     def __init__(self, config: Config | None = None, addr: str | None = None):
         self.cfg = config or Config.from_env()
         self.addr_requested = addr or self.cfg.file_server_addr
-        self.log = Logger("file_server", self.addr_requested)
+        self.metrics = Metrics("file_server")
+        self.log = Logger("file_server", self.addr_requested, self.metrics)
         self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
         self._files: dict[int, bytes] = {}
         self._lock = threading.Lock()
@@ -172,10 +174,13 @@ class FileServer:
         self.server.start()
         self.addr = self.server.addr
         self.log.addr = self.addr
+        if self.cfg.metrics_port > 0:
+            self.metrics.serve(self.cfg.metrics_port)
         self.log.info("serving", dataset=self.cfg.dataset)
         return self
 
     def stop(self) -> None:
+        self.metrics.close()
         if self.server:
             self.server.stop()
         self.channels.close()

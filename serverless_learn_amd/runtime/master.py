@@ -36,6 +36,7 @@ from ..config import Config
 from ..parallel.ps import ParameterServer
 from ..proto import messages as pb
 from ..utils.log import Logger
+from ..utils.metrics import Metrics
 from ..wire.codec import decode_update, encode_update
 from .transport import Channels, RpcFailure, RpcServer
 
@@ -53,7 +54,8 @@ class Master:
         self.cfg = config or Config.from_env()
         self.addr_requested = addr or self.cfg.master_addr
         self.clock = clock
-        self.log = Logger("master", self.addr_requested)
+        self.metrics = Metrics("master")
+        self.log = Logger("master", self.addr_requested, self.metrics)
         self.registry = core().Registry()
         self.ps = ParameterServer(self.cfg.learn_rate)
         self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
@@ -87,7 +89,8 @@ class Master:
                                                       info.incarnation, self.clock())
         with self._lock:
             self.incarnation[info.addr] = info.incarnation
-        self.log.info("register_birth", worker=info.addr, epoch=epoch, changed=changed, gpus=info.num_gpus)
+        self.log.info("register_birth", worker=info.addr, epoch=epoch, changed=changed, gpus=info.num_gpus,
+                      world=len(self.registry.members()))
         if changed:
             self._notify()  # disseminate the new view now, not in up to 5 s
         return pb.RegisterBirthAck(ok=True, epoch=epoch).SerializeToString()
@@ -98,7 +101,8 @@ class Master:
         with self._lock:
             self.delivered.pop(info.addr, None)
             self.ckpt_delivered.pop(info.addr, None)
-        self.log.info("deregister", worker=info.addr, existed=existed, epoch=self.registry.epoch())
+        self.log.info("deregister", worker=info.addr, existed=existed, epoch=self.registry.epoch(),
+                      world=len(self.registry.members()))
         if existed:
             self._notify()
         return pb.RegisterBirthAck(ok=existed, epoch=self.registry.epoch()).SerializeToString()
@@ -156,7 +160,7 @@ class Master:
                     self.delivered.pop(addr, None)
                     self.ckpt_delivered.pop(addr, None)
                     self.feedback.pop(addr, None)
-                self.log.info("evicted", worker=addr, epoch=self.registry.epoch())
+                self.log.info("evicted", worker=addr, epoch=self.registry.epoch(), world=len(self.registry.members()))
                 self._notify()
 
     def checkup_once(self) -> None:
@@ -246,6 +250,8 @@ class Master:
         self.addr = self.server.addr
         self.log.addr = self.addr
         self._start_rendezvous()
+        if self.cfg.metrics_port > 0:
+            self.metrics.serve(self.cfg.metrics_port)
         self.log.info("serving", rendezvous=self.rendezvous)
         if loops:
             for fn, iv, name in ((self.checkup_once, self.cfg.checkup_interval, "checkup"),
@@ -258,6 +264,7 @@ class Master:
         return self
 
     def stop(self) -> None:
+        self.metrics.close()
         self._stop.set()
         self._notify()
         for t in self._threads:

@@ -46,6 +46,7 @@ from ..proto import messages as pb
 from ..utils import trace
 from ..utils.fault import FaultInjector
 from ..utils.log import Logger
+from ..utils.metrics import Metrics
 from ..wire.codec import chunk_payload, decode_update, encode_update, iter_chunks
 from .file_server import FILE_NUM_MD, FILE_SIZE_MD
 from .transport import Channels, RpcFailure, RpcServer, metadata_dict
@@ -67,7 +68,8 @@ class Worker:
         self.cfg = config or Config.from_env()
         self.addr_requested = addr
         self.addr = addr
-        self.log = Logger("worker", addr)
+        self.metrics = Metrics("worker")
+        self.log = Logger("worker", addr, self.metrics)
         self.incarnation = (time.time_ns() ^ (os.getpid() << 20) ^ random.getrandbits(40)) & ((1 << 63) - 1)
         self.device = resolve_device(self.cfg.device)
         self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
@@ -415,6 +417,8 @@ class Worker:
             t = threading.Thread(target=fn, daemon=True, name="sl-worker-" + fn.__name__)
             t.start()
             self._threads.append(t)
+        if self.cfg.metrics_port > 0:
+            self.metrics.serve(self.cfg.metrics_port)
         self.log.info("serving", device=str(self.device), sync=self.cfg.sync, model=self.cfg.model)
         return self
 
@@ -427,6 +431,7 @@ class Worker:
             pass
 
     def stop(self, leave: bool = True) -> None:
+        self.metrics.close()
         if leave:
             self.leave()
         self._stop.set()

@@ -29,12 +29,15 @@ def _out():
 
 
 class Logger:
-    def __init__(self, role: str, addr: str = ""):
+    def __init__(self, role: str, addr: str = "", metrics=None):
         self.role = role
         self.addr = addr
+        self.metrics = metrics  # utils.metrics.Metrics fed with every event (any level)
         self.min_level = _LEVELS.get(os.environ.get("SL_LOG_LEVEL", "info"), 20)
 
     def _emit(self, level: str, event: str, **fields):
+        if self.metrics is not None:
+            self.metrics.observe(level, event, fields)
         if _LEVELS[level] < self.min_level:
             return
         rec = {"ts": round(time.time(), 6), "level": level, "role": self.role, "addr": self.addr, "event": event}

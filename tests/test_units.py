@@ -131,3 +131,30 @@ def test_config_defaults_equal_reference_constants(monkeypatch):
     monkeypatch.setenv("SL_GOSSIP_COMPAT", "true")
     c = Config.from_env()
     assert c.gossip_interval == 0.25 and c.gossip_compat is True
+
+
+def test_metrics_from_log_events_and_http_exposition():
+    import urllib.request
+
+    from serverless_learn_amd.utils.log import Logger
+    from serverless_learn_amd.utils.metrics import Metrics
+
+    m = Metrics("worker")
+    log = Logger("worker", "127.0.0.1:1", m)
+    log.info("train", step=50, loss=0.25, acc=0.9, samples_per_sec=1.5e6, epoch=3)
+    log.info("received_file", file_num=0, kind="shard", bytes=1000, s=0.01)
+    log.warn("collective_failed", error="x")
+    log.debug("below_level")  # filtered from the log, still counted
+    txt = m.text()
+    assert 'sl_step{role="worker"} 50.0' in txt
+    assert 'sl_loss{role="worker"} 0.25' in txt
+    assert 'sl_membership_epoch{role="worker"} 3.0' in txt
+    assert 'sl_ingested_bytes_total{role="worker"} 1000.0' in txt
+    assert 'sl_events_total{event="collective_failed",level="warn",role="worker"} 1.0' in txt
+    assert 'event="below_level"' in txt
+    port = m.serve(0, addr="127.0.0.1")
+    try:
+        body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+        assert 'sl_samples_per_second{role="worker"} 1.5e+06' in body
+    finally:
+        m.close()
