@@ -39,6 +39,9 @@ using namespace sl;
 #ifndef SL_WGRAD128_KS
 #define SL_WGRAD128_KS 1
 #endif
+#ifndef SL_WGRAD128_WGM
+#define SL_WGRAD128_WGM 64  // pixels per stage of the 128-wide weight-gradient tile (32: half-depth stages)
+#endif
 #ifndef SL_WGRAD128_KS2_SLOTS
 #define SL_WGRAD128_KS2_SLOTS 4
 #endif
@@ -459,16 +462,16 @@ struct WgradArgs {
 
 // KS = 2: 8 waves, waves 4-7 take the second 32 pixels of every 64-pixel stage
 // (two waves per SIMD inside one workgroup); the k-halves are summed through LDS.
-template <int BMO, int NSLOT, int KS>
+template <int BMO, int NSLOT, int KS, int WGM = WG_M>
 __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
   constexpr int BNO = 128;
   constexpr int WA = BMO / 8, WB = BNO / 8;       // 16-B chunks per image row
   constexpr int MT = BMO / 32, NT = BNO / 32;     // per-wave MFMA tiles (2x2 waves)
   constexpr int RA = 64 / WA, RB = 64 / WB;       // rows per 1-KB DMA piece
   constexpr int NTW = 256 * KS;
-  constexpr int PA = (WG_M / RA) / (4 * KS), PB = (WG_M / RB) / (4 * KS);  // pieces per wave per stage
+  constexpr int PA = (WGM / RA) / (4 * KS), PB = (WGM / RB) / (4 * KS);  // pieces per wave per stage
   constexpr int PS = PA + PB;
-  constexpr int IMG_A = WG_M * BMO, IMG_B = WG_M * BNO;      // elements
+  constexpr int IMG_A = WGM * BMO, IMG_B = WGM * BNO;      // elements
   constexpr int SLOT = IMG_A + IMG_B;
   constexpr int OUT_LD = BNO + 4;
   constexpr int SMEM = NSLOT * SLOT > BMO * OUT_LD * 2 ? NSLOT * SLOT : BMO * OUT_LD * 2;  // ring / fp32 epilogue
@@ -487,8 +490,8 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
   const int tco = t / a.tiles_k, tk = t - tco * a.tiles_k;
   const int co0 = tco * BMO, k0 = tk * BNO;
   const int wm = w4 >> 1, wn = w4 & 1;
-  const int mbeg = s * a.steps_per_slice * WG_M;
-  const int nst = min(a.steps_per_slice, (g.M - mbeg + WG_M - 1) / WG_M);
+  const int mbeg = s * a.steps_per_slice * WGM;
+  const int nst = min(a.steps_per_slice, (g.M - mbeg + WGM - 1) / WGM);
 
   // A (dY) pieces: row = RA * (wave * PA + j) + lane / WA, LDS chunk lane % WA
   int arow[PA];
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
   auto issue = [&](int st) {
     uint16_t* Ai = smem + (st % NSLOT) * SLOT;
     uint16_t* Bi = Ai + IMG_A;
-    const int mb = mbeg + st * WG_M;
+    const int mb = mbeg + st * WGM;
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const int m = mb + arow[j];
@@ -563,7 +566,9 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
     };
-    if constexpr (KS == 1) {
+    if constexpr (KS == 1 && WGM == 32) {
+      half(std::integral_constant<int, 0>{});
+    } else if constexpr (KS == 1) {
       half(std::integral_constant<int, 0>{});
       half(std::integral_constant<int, 1>{});
     } else if (kg == 0) {
@@ -780,7 +785,8 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   a.tiles_co = (cout + BMO - 1) / BMO;
   a.tiles_k = (a.g.K + 127) / 128;
   const int tiles = a.tiles_co * a.tiles_k;
-  const int total_steps = (a.g.M + WG_M - 1) / WG_M;
+  const int wgm = BMO == 64 ? WG_M : SL_WGRAD128_WGM;  // pixels per stage
+  const int total_steps = (a.g.M + wgm - 1) / wgm;
   if (target_wgs <= 0) target_wgs = 512;  // two workgroups per CU (64-72 KB LDS ring each)
   int slices = tiles >= target_wgs / 2 ? 1 : (target_wgs + tiles - 1) / tiles;
   if (slices > total_steps) slices = total_steps;
@@ -791,7 +797,7 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3, 1>), grid, dim3(256), 0, stream, a);
   else if (SL_WGRAD128_KS == 2)
     hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_KS2_SLOTS, 2>), grid, dim3(512), 0, stream, a);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS, 1>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS, 1, SL_WGRAD128_WGM>), grid, dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
