@@ -51,6 +51,8 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
+    ap.add_argument("--unroll", type=int, default=8,
+                    help="MLP: steps per hipGraph replay (each step still runs all its kernels on its own batch)")
     ap.add_argument("--ingest", choices=["grpc", "local", "device"], default="grpc",
                     help="grpc: file server -> ReceiveFile -> pinned ring -> HBM; local: host-generated shard; "
                          "device: shard synthesised in HBM by the Philox kernel (K8)")
@@ -148,10 +150,13 @@ def main(argv=None) -> int:
     warm_eager = min(args.warmup, 3)
     for _ in range(warm_eager):
         tr.step()
+    run = getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
     if use_graph:
-        tr.capture(warmup=0)
-    for _ in range(args.warmup - warm_eager):
-        tr.step()
+        if mlp:
+            tr.capture(warmup=0, unroll=args.unroll)
+        else:
+            tr.capture(warmup=0)
+    run(args.warmup - warm_eager)
     torch.cuda.synchronize()
     first_loss = tr.stats().loss
 
@@ -160,8 +165,7 @@ def main(argv=None) -> int:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tr.step()
+    run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -196,6 +200,7 @@ def main(argv=None) -> int:
             "parallelism": f"dp{world}",
             "optimizer": f"sgd(lr={args.lr}, momentum={args.momentum}) fp32 master",
             "hipgraph": use_graph,
+            "steps_per_graph": (args.unroll if mlp else 1) if use_graph else 0,
             "ingest": args.ingest,
             "collective_backend": ("rccl" if args.dist_backend == "nccl" else "gloo") if world > 1 else None,
         },

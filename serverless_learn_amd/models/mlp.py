@@ -372,6 +372,20 @@ class FusedMLPTrainer:
             return
         self._step_eager()
 
+    def steps(self, n: int) -> None:
+        """Run ``n`` full training steps.  With a multi-step graph captured
+        (``capture(unroll=k)``) they replay k at a time: the ~8 us gap that every
+        graph launch leaves between the previous step's SGD and the next rows
+        kernel is paid once per k steps (every step still runs all three kernels
+        on its own batch; the device cursor advances inside the graph)."""
+        g, k = getattr(self, "graph_unrolled", None), getattr(self, "unroll", 1)
+        if self.graph is not None and g is not None and k > 1:  # self.graph=None invalidates both
+            while n >= k:
+                g.replay()
+                n -= k
+        for _ in range(n):
+            self.step()
+
     def _step_eager(self) -> None:
         self._rows(True)
         self._wgrad()
@@ -382,8 +396,9 @@ class FusedMLPTrainer:
             self.allreduce(self.grad)
             self._sgd(2, from_grad=True, grad_out=False)
 
-    def capture(self, warmup: int = 2) -> None:
-        """Capture one step into a hipGraph (kernels only, or kernels + RCCL)."""
+    def capture(self, warmup: int = 2, unroll: int = 1) -> None:
+        """Capture one step into a hipGraph (kernels only, or kernels + RCCL);
+        ``unroll > 1`` also captures a k-step graph used by :meth:`steps`."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -394,6 +409,13 @@ class FusedMLPTrainer:
         with torch.cuda.graph(g):
             self._step_eager()
         self.graph = g
+        self.graph_unrolled, self.unroll = None, max(1, int(unroll))
+        if self.unroll > 1:
+            gk = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gk):
+                for _ in range(self.unroll):
+                    self._step_eager()
+            self.graph_unrolled = gk
 
     # ---- eval / state ----
     def stats(self) -> StepStats:

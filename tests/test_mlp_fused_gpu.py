@@ -115,6 +115,24 @@ def test_graph_replay_equals_eager():
     assert torch.equal(a.get_flat(), b.get_flat())
 
 
+def test_unrolled_graph_runs_every_step():
+    """steps(n) with a 4-step graph == n eager steps (incl. a remainder and the cursor walk)."""
+    batch = 1024
+    x, y = _data(batch * 3, seed=12)
+    flat = M.init_params(10)
+    a = M.FusedMLPTrainer(batch=batch, flat=flat)
+    b = M.FusedMLPTrainer(batch=batch, flat=flat)
+    a.load_shard(x, y)
+    b.load_shard(x, y)
+    b.capture(warmup=0, unroll=4)
+    for _ in range(11):
+        a.step()
+    b.steps(11)
+    torch.cuda.synchronize()
+    assert int(a.cursor.item()) == int(b.cursor.item()) == 11
+    assert torch.equal(a.get_flat(), b.get_flat())
+
+
 def test_allreduce_hook_path_matches_single_rank():
     """The eager data-parallel step (reduce -> all-reduce hook -> update) with a
     simulated 2-rank all-reduce of identical replicas equals one rank's step."""
