@@ -8,26 +8,31 @@
 //           per CU (67.5 KB LDS): L1 -> ReLU -> L2 -> ReLU -> L3 -> softmax-CE
 //           -> dZ -> dH2 -> dH1, all row-local.  The u8 input streams through
 //           a 2-slot LDS ring in 64-wide K chunks (normalised to bf16 on the
-//           way in, two chunks of register prefetch); weights are stored in
+//           way in, 4 chunks of register prefetch); weights are stored in
 //           MFMA-fragment order (each wave-load is one contiguous 1 KB block)
 //           and stream from L2 through a 4-deep per-wave register ring; ReLU
-//           masks stay as bits in registers.  Every operand the weight
-//           gradient needs (normalised X, H1, H2, dZ, dH2, dH1) is written
-//           row-major with coalesced 16-B stores.
+//           masks are re-derived from the activations kept in LDS.  H1, dH2
+//           and dH1 are written row-major with coalesced 16-B stores for the
+//           weight gradient; [dW3 | db3] (10 x 257) is computed here from the
+//           LDS images as one fp32 partial per 64 rows, so H2 and dZ never
+//           reach HBM.
 //   K_wgrad (mlp_wgrad_kernel) grouped split-K GEMM dW = dH^T . A over the
-//           batch: 128x128 tiles; both operands stream global -> LDS by
-//           LDS-DMA (global_load_lds_dwordx4, no VGPR staging) into a 4-slot
-//           ring of XOR-swizzled [64 batch rows][128] images (three stages in
-//           flight, counted vmcnt + raw s_barrier), read transposed with
-//           ds_read_b64_tr_b16; bias gradients come from an extra MFMA
-//           against a ones fragment.  Deterministic fp32 slabs.
+//           batch for dW1 (A = raw u8 X) and dW2 (A = H1): 128x128 tiles; both
+//           operands stream global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//           no VGPR staging) into a 4-slot ring of XOR-swizzled [64 batch
+//           rows][128] images (three stages in flight, counted vmcnt + raw
+//           s_barrier), read transposed with ds_read_b64_tr_b16/_b8; bias
+//           gradients come from an extra MFMA against a ones fragment.
+//           Deterministic fp32 slabs.  The spare CUs of its grid sum the rows
+//           kernel's dW3 partials into the slab.
 //   K_sgd   (mlp_sgd_kernel)   slab reduction (+ optional all-reduce
 //           hand-off) + momentum SGD on fp32 master weights, refreshing the
-//           bf16 shadow weights (and the transposed copies the backward
-//           pass reads) in the same pass; bumps the device batch cursor so
-//           the whole step replays from a hipGraph without host work.
+//           bf16 shadow weights (and the transposed copies the backward pass
+//           reads) in the same pass; bumps the device batch cursor so the
+//           whole step replays from a hipGraph without host work.
 #include "common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 using namespace sl;
@@ -38,6 +43,12 @@ using namespace sl;
 #ifndef SL_MLP_RING2
 #define SL_MLP_RING2 4
 #endif
+#ifndef SL_MLP_SLICES
+#define SL_MLP_SLICES 14  // weight-gradient K slices: 18 tiles x 14 = 252 GEMM workgroups
+#endif
+#ifndef SL_W3_UNROLL
+#define SL_W3_UNROLL 16
+#endif
 #ifndef SL_MLP_XQ
 #define SL_MLP_XQ 4  // X prefetch distance in 64-column chunks (4 measured +1% over 2)
 #endif
@@ -47,7 +58,6 @@ constexpr int D_INP = 832;  // layer-1 K padded to 13 chunks of 64 (w1h row stri
 constexpr int NCHUNK = D_INP / 64;
 constexpr int HID = 256;
 constexpr int NC = 10;
-constexpr int DZ_COLS = 16;  // dZ row stride in global memory
 constexpr int BM = 64;       // batch rows granularity (the rows kernel runs 64 or 128 per workgroup)
 constexpr int HS_LD = 264;   // [64][256] bf16 LDS images: 528-B rows
 constexpr int XC_LD = 72;    // X chunk image rows: 64 k + 8 pad = 144 B (ds_read_b128 conflict-free)
@@ -62,6 +72,9 @@ constexpr long P_B2 = P_W2 + (long)HID * HID;
 constexpr long P_W3 = P_B2 + HID;
 constexpr long P_B3 = P_W3 + (long)NC * HID;
 constexpr long P_N = P_B3 + NC;  // 269322
+// Per-64-row partials of [dW3 | db3] (2570 values, flat order from P_W3), padded rows.
+constexpr int W3P_N = NC * HID + NC;
+constexpr int W3P_LD = 2576;
 }  // namespace
 
 // Weights are kept in MFMA B-fragment order: for a [N][K] matrix (K
@@ -96,14 +109,13 @@ struct MlpRowArgs {
   const uint16_t *w1h, *w2h, *w3h, *w2th, *w3th;
   const float *b1, *b2, *b3;
   float xa, xb, grad_scale;
-  uint16_t *h1, *h2, *dz, *dh2, *dh1;  // row-major [batch][256] ([batch][16] for dz)
+  uint16_t* h1;                        // row-major [batch][256]
+  float* w3p;                          // [batch / 64][W3P_LD] partial [dW3 | db3]
+  uint16_t *dh2, *dh1;                 // row-major [batch][256]
   float *loss, *correct, *logits;
   unsigned long long* stamps;  // diagnostics: per-workgroup phase timestamps (nullptr in production)
 };
 
-// Fully unrolled K loop with a 4-deep register ring for the per-wave B
-// operand (weights, streamed from L2).  `after(s)` runs after step s's MFMAs
-// and its ring refill (chunk hand-offs / barriers of the A operand ring).
 // Fully unrolled K loop with a D-deep register ring for the per-wave B operand
 // (weights, streamed from L2).  `after(s)` runs after step s's MFMAs and its
 // ring refill (chunk hand-offs / barriers / spread-out stores).
@@ -363,10 +375,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     floatx4_t z = zero4();
     const uint16_t* ha = R0 + (wave * 16 + lr) * HS_LD + 8 * lg;
 #pragma unroll
-    for (int ks = 0; ks < KS2; ++ks) {
-      z = mfma16(lds8(ha + ks * 32), w3f[ks], z);
-      if (TRAIN) copy_part<BM, NT, HID>(R0, HS_LD, a.h2 + (long)row0 * HID, HID, tid, ks);
-    }
+    for (int ks = 0; ks < KS2; ++ks) z = mfma16(lds8(ha + ks * 32), w3f[ks], z);
     const int c = lr;
     const float bias3 = c < NC ? a.b3[c] : 0.f;
 #pragma unroll
@@ -396,7 +405,37 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   if (!TRAIN) return;
   __syncthreads();
   stamp(5);
-  copy_out<BM, NT, DZ_COLS>(RZ, DZ_LD, a.dz + (long)row0 * DZ_COLS, DZ_COLS, tid);
+
+  // ---- [dW3 | db3] partial over this wave's 64 rows: dZ^T (RZ) . H2 (R0), both read
+  // transposed (ds_read_b64_tr_b16).  The weight-gradient kernel would otherwise need
+  // H2 and dZ in HBM (a [batch][256] write here + a re-read there) and spend 2 of its
+  // 20 tiles on a 10-row GEMM.  mlp_sgd_kernel sums the partials in a fixed order. ----
+  {
+    floatx4_t d3[NF], db3 = zero4();
+#pragma unroll
+    for (int n = 0; n < NF; ++n) d3[n] = zero4();
+    short8_t ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int k0 = rw + 32 * ks;
+      const short8_t af = lds_tr8(RZ + k0 * DZ_LD, DZ_LD, lane);  // A[c][row] = dZ[row][c]
+#pragma unroll
+      for (int n = 0; n < NF; ++n) d3[n] = mfma16(af, lds_tr8(R0 + k0 * HS_LD + cw + n * 16, HS_LD, lane), d3[n]);
+      if (wng == 0) db3 = mfma16(af, ones, db3);
+    }
+    float* part = a.w3p + (long)((row0 + rw) >> 6) * W3P_LD;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 4 * lg + r;
+      if (c < NC) {
+#pragma unroll
+        for (int n = 0; n < NF; ++n) part[c * HID + cw + n * 16 + lr] = d3[n][r];
+        if (wng == 0 && lr == 0) part[NC * HID + c] = db3[r];
+      }
+    }
+  }
 
   // ---- dH2 = (dZ W3) * 1[H2 > 0], K = 32 (10 classes, zero padded); out -> R0 ----
   zero_acc();
@@ -457,13 +496,16 @@ struct WgProblem {
   long w_off, b_off;  // flat destinations of dW ([m_real][n_real]) and db
 };
 struct WgArgs {
-  WgProblem p[3];
+  WgProblem p[2];  // dW1 (u8 X), dW2 (H1); dW3 comes from the rows kernel's partials
   int total_tiles;
   int steps_per_slice, total_steps;  // 64-row stages
   float* slab;
   long slab_stride;
   const int* cursor;  // X is the resident shard: rows start at batch_base(cursor)
   int n_batches, batch;
+  int gemm_wgs, slices;  // blocks >= gemm_wgs reduce the rows kernel's [dW3 | db3] partials
+  const float* w3p;      // [n_w3p][W3P_LD]
+  int n_w3p;
 };
 
 constexpr int WG_NSLOT = 4;               // LDS ring slots (128 KB): three stages in flight (5 measured no better)
@@ -559,16 +601,66 @@ __device__ __forceinline__ void wg_vmcnt(int younger) {
 // let one wave's LDS reads / barrier wait run under the other's MFMAs (at one
 // wave per SIMD the pipe was busy 25 % of the time, profiles/r01_v6).
 constexpr int WG_NT = 512;
+
+// [dW3 | db3] = sum over the rows kernel's per-64-row partials, computed by the
+// few workgroups the GEMM grid leaves over (18 tiles x 14 slices = 252 of 256
+// CUs), so it costs no time on the critical path.  Reducer r takes a band of
+// float4 columns; G row groups per column, 16 loads in flight per thread, then a
+// fixed-order sum through LDS (deterministic).  The result goes to slab slice
+// 0 and zeros to the other slices, so mlp_sgd_kernel needs no special case.
+__device__ __forceinline__ void w3_reduce(const WgArgs& A, float4* red, int r, int nr) {
+  constexpr int NCOL = W3P_LD / 4;
+  const int cpw = (NCOL + nr - 1) / nr;  // <= 322 columns: G >= 1
+  const int G = WG_NT / cpw;
+  const int t = threadIdx.x, col = t % cpw, g = t / cpw;
+  const int c = r * cpw + col;
+  const bool act = g < G && c < NCOL;
+  if (act) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* src = reinterpret_cast<const float4*>(A.w3p) + c;
+#pragma unroll SL_W3_UNROLL
+    for (int b = g; b < A.n_w3p; b += G) {
+      const float4 v = src[(long)b * NCOL];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    red[g * cpw + col] = s;
+  }
+  __syncthreads();
+  if (act && g == 0) {
+    float4 tot = red[col];
+    for (int i = 1; i < G; ++i) {
+      const float4 v = red[i * cpw + col];
+      tot.x += v.x; tot.y += v.y; tot.z += v.z; tot.w += v.w;
+    }
+    const float tv[4] = {tot.x, tot.y, tot.z, tot.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = 4 * c + j;
+      if (q < W3P_N) {
+        A.slab[P_W3 + q] = tv[j];
+        for (int sl = 1; sl < A.slices; ++sl) A.slab[(long)sl * A.slab_stride + P_W3 + q] = 0.f;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_NSLOT * WG_SLOT];
+  if ((int)blockIdx.x >= A.gemm_wgs) {  // block-uniform
+#ifdef SL_W3_SKIP  // timing experiments only
+    return;
+#endif
+    w3_reduce(A, reinterpret_cast<float4*>(smem), (int)blockIdx.x - A.gemm_wgs, (int)gridDim.x - A.gemm_wgs);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
   const int kg = wave >> 2, w4 = wave & 3;
   const int lr = lane & 15, lg = lane >> 4;
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int logical = xcd_remap(blockIdx.x, A.gemm_wgs);
   const int s = logical / A.total_tiles;
   const int t = logical - s * A.total_tiles;
-  const int pi = t >= A.p[2].tile_base ? 2 : (t >= A.p[1].tile_base ? 1 : 0);
+  const int pi = t >= A.p[1].tile_base ? 1 : 0;
   const WgProblem& P = A.p[pi];
   const int lt = t - P.tile_base;
   const int tm = lt / P.tiles_n, tn = lt - tm * P.tiles_n;
@@ -577,7 +669,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int st0 = s * A.steps_per_slice;
   const int nst = min(A.steps_per_slice, A.total_steps - st0);
   const bool do_bias = tn == 0 && wn == 0;
-  const bool m_live = m0 + wm * 64 < P.m_real;  // wave-uniform: skip MFMAs on all-padding rows
   const bool u8b = pi == 0;
 
   // LDS-DMA map (bf16 images): wave w, piece j (0..1) covers image rows 4 (2w + j) .. +3;
@@ -592,8 +683,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   for (int j = 0; j < 2; ++j) {
     const int row = 4 * (2 * wave + j) + prow;
     const int c = wg_swz(lane & 15, row);
-    const int acol = min(m0 + c * 8, P.lda - 8);  // columns past dZ's 16 are don't-care rows of dW3
-    asrc[j] = static_cast<const uint16_t*>(P.a) + (long)(st0 * 64 + row) * P.lda + acol;
+    asrc[j] = static_cast<const uint16_t*>(P.a) + (long)(st0 * 64 + row) * P.lda + m0 + c * 8;
     bsrc[j] = static_cast<const uint16_t*>(P.b) + (long)(st0 * 64 + row) * P.ldb + n0 + c * 8;
   }
   const uint8_t* bsrc8;
@@ -641,18 +731,18 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   for (int j = 0; j < 4; ++j)
     b_addr[j] = u8b ? wg_tr8_addr(wn * 64 + j * 16, lane) + kg * (32 * 128) : wg_tr_addr(wn * 64 + j * 16, lane) + kg * (32 * 128 * 2);
 
-  // The main loop is instantiated per (u8, live, bias) combination and selected
+  // The main loop is instantiated per (u8, bias) combination and selected
   // by a scalar branch OUTSIDE it: with the conditions inside, hipcc treated
   // them as divergent and copied all 64 accumulators AGPR<->VGPR on every stage.
-  auto mainloop = [&](auto u8_c, auto live_c, auto bias_c) {
-    constexpr bool U8 = decltype(u8_c)::value, LIVE = decltype(live_c)::value, BIAS = decltype(bias_c)::value;
+  auto mainloop = [&](auto u8_c, auto bias_c) {
+    constexpr bool U8 = decltype(u8_c)::value, BIAS = decltype(bias_c)::value;
     constexpr int PPS = U8 ? 3 : 4;  // LDS-DMA pieces per wave per stage
     for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, u8_c);
     for (int st = 0; st < nst; ++st) {
       wg_vmcnt<PPS>(min(WG_NSLOT - 2, nst - 1 - st));  // this wave's pieces of stage st have landed
       __builtin_amdgcn_s_barrier();  // ... everyone's have; the slot of stage st-1 is free
       if (st + WG_NSLOT - 1 < nst) issue(st + WG_NSLOT - 1, u8_c);
-      if constexpr (LIVE) {
+      {
         const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
         short8_t af[4], bf[4];
 #pragma unroll
@@ -689,14 +779,12 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   using T_ = std::true_type;
   using F_ = std::false_type;
   if (u8b) {
-    if (do_bias) mainloop(T_{}, T_{}, T_{});
-    else mainloop(T_{}, T_{}, F_{});
-  } else if (!m_live) {
-    mainloop(F_{}, F_{}, F_{});
+    if (do_bias) mainloop(T_{}, T_{});
+    else mainloop(T_{}, F_{});
   } else if (do_bias) {
-    mainloop(F_{}, T_{}, T_{});
+    mainloop(F_{}, T_{});
   } else {
-    mainloop(F_{}, T_{}, F_{});
+    mainloop(F_{}, F_{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -793,6 +881,20 @@ __device__ __forceinline__ float quad_sum(float v) {
   return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
 }
 
+__device__ __forceinline__ void sgd_apply(const SgdArgs& a, long p, float gme) {
+  if (a.grad_out) a.grad_out[p] = gme;
+  if (a.mode == 1) return;
+  float w = a.w[p];
+  float d = gme + a.wd * w;
+  if (a.mom) {
+    d = a.mu * a.mom[p] + d;
+    a.mom[p] = d;
+  }
+  w -= a.lr * d;
+  a.w[p] = w;
+  write_shadow(a, p, w);
+}
+
 __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -835,17 +937,7 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
     gme = mine ? a.grad_in[p] : 0.f;
   }
   if (!mine) return;
-  if (a.grad_out) a.grad_out[p] = gme;
-  if (a.mode == 1) return;
-  float w = a.w[p];
-  float d = gme + a.wd * w;
-  if (a.mom) {
-    d = a.mu * a.mom[p] + d;
-    a.mom[p] = d;
-  }
-  w -= a.lr * d;
-  a.w[p] = w;
-  write_shadow(a, p, w);
+  sgd_apply(a, p, gme);
 }
 
 // ---------------------------------------------------------------------------
@@ -878,7 +970,7 @@ int sl_mlp_rows_bm(int batch) {
 int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_batches, int batch,
                 const uint16_t* w1h, const uint16_t* w2h, const uint16_t* w3h, const uint16_t* w2th,
                 const uint16_t* w3th, const float* params, float xa, float xb, float grad_scale,
-                uint16_t* h1, uint16_t* h2, uint16_t* dz, uint16_t* dh2, uint16_t* dh1,
+                uint16_t* h1, float* w3p, uint16_t* dh2, uint16_t* dh1,
                 float* loss, float* correct, float* logits, int train, hipStream_t stream) {
   if (batch <= 0 || batch % BM != 0) return -1;
   MlpRowArgs a;
@@ -886,10 +978,10 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th;
   a.b1 = params + P_B1; a.b2 = params + P_B2; a.b3 = params + P_B3;
   a.xa = xa; a.xb = xb; a.grad_scale = grad_scale;
-  a.h1 = h1; a.h2 = h2; a.dz = dz; a.dh2 = dh2; a.dh1 = dh1;
+  a.h1 = h1; a.w3p = w3p; a.dh2 = dh2; a.dh1 = dh1;
   a.loss = loss; a.correct = correct; a.logits = logits;
   a.stamps = g_stamps;
-  if (train && (!h1 || !h2 || !dz || !dh2 || !dh1)) return -2;
+  if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
   const int bm = sl_mlp_rows_bm(batch);
   if (bm == 128) {
     if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 2>), dim3(batch / 128), dim3(512), 0, stream, a);
@@ -907,7 +999,7 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
 int sl_mlp_wgrad_slices(int batch, int requested) {
   if (batch <= 0 || batch % 64 != 0) return -1;
   const int total = batch / 64;
-  int req = requested > 0 ? requested : 12;  // 20 tiles x 12 slices = 240 WGs: one per CU (128 KB LDS each)
+  int req = requested > 0 ? requested : SL_MLP_SLICES;  // one GEMM WG per CU (128 KB LDS each)
   if (req > total) req = total;
   const int spp = (total + req - 1) / req;
   return (total + spp - 1) / spp;
@@ -916,19 +1008,18 @@ int sl_mlp_wgrad_slices(int batch, int requested) {
 // x: the resident u8 shard [n_batches * batch][784]; the batch rows are the
 // ones the rows kernel used (cursor not yet bumped: mlp_sgd_kernel bumps it).
 int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, const uint16_t* h1,
-                 const uint16_t* h2, const uint16_t* dz, const uint16_t* dh2, const uint16_t* dh1, float* slab,
-                 int slices, long slab_stride, hipStream_t stream) {
+                 const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
+                 long slab_stride, hipStream_t stream) {
+  if (!w3p || n_w3p != batch / 64) return -1;
   const int s_eff = sl_mlp_wgrad_slices(batch, slices);
   if (s_eff <= 0 || s_eff != slices) return -1;
   WgArgs a;
-  // dW1, db1 = dH1^T [256 x B] . Xn
+  // dW1, db1 = dH1^T [256 x B] . X (raw u8; normalised in mlp_sgd_kernel)
   a.p[0] = WgProblem{dh1, HID, x, D_IN, HID, D_IN, HID / 128, (D_IN + 127) / 128, 0, P_W1, P_B1};
   // dW2, db2 = dH2^T . H1
   a.p[1] = WgProblem{dh2, HID, h1, HID, HID, HID, HID / 128, HID / 128, 0, P_W2, P_B2};
-  // dW3, db3 = dZ^T . H2
-  a.p[2] = WgProblem{dz, DZ_COLS, h2, HID, NC, HID, 1, HID / 128, 0, P_W3, P_B3};
   int base = 0;
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 2; ++i) {
     a.p[i].tile_base = base;
     base += a.p[i].tiles_m * a.p[i].tiles_n;
   }
@@ -937,8 +1028,12 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
   a.steps_per_slice = (a.total_steps + slices - 1) / slices;
   a.slab = slab; a.slab_stride = slab_stride;
   a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
-  if (((uintptr_t)x & 15) != 0) return -2;  // LDS-DMA pieces are 16-B
-  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(WG_NT), 0, stream, a);
+  a.gemm_wgs = base * slices; a.slices = slices;
+  a.w3p = w3p; a.n_w3p = n_w3p;
+  // reducers on the CUs the GEMM grid leaves idle (at least 2, at most 8)
+  const int reducers = std::min(8, std::max(2, 256 - a.gemm_wgs));
+  if (((uintptr_t)x & 15) != 0 || ((uintptr_t)w3p & 15) != 0) return -2;  // 16-B pieces / float4 reads
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(a.gemm_wgs + reducers), dim3(WG_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -34,6 +34,7 @@ CLASSES = 10
 MNIST_MEAN = 0.1307
 MNIST_STD = 0.3081
 BLOCK_ROWS = 64  # batch rows per workgroup of the fused row kernel
+W3P_LD = 2576  # row stride of the rows kernel's [dW3 | db3] partials (2,570 used)
 
 LAYOUT = (
     ("fc1.weight", (HIDDEN, D_IN)),
@@ -267,10 +268,10 @@ class FusedMLPTrainer:
         self.w3th = torch.zeros(HIDDEN, 32, dtype=bf, device=dev)
         # row-major activations for the weight-gradient kernel ([batch][256], dZ [batch][16])
         self.h1t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
-        self.h2t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
         self.dh1t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
         self.dh2t = torch.empty(batch, HIDDEN, dtype=bf, device=dev)
-        self.dzt = torch.empty(batch, 16, dtype=bf, device=dev)
+        # per-64-row partials of [dW3 | db3] from the rows kernel (H2 / dZ never reach HBM)
+        self.w3p = torch.empty(batch // 64, W3P_LD, dtype=torch.float32, device=dev)
         self.loss = torch.zeros(batch, dtype=torch.float32, device=dev)
         self.correct = torch.zeros(batch, dtype=torch.float32, device=dev)
         self.slab = torch.empty(self.slices, self.n_pad, dtype=torch.float32, device=dev)
@@ -324,10 +325,10 @@ class FusedMLPTrainer:
             "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
                              p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
                              p(self.params), self.xa, self.xb, self.grad_scale,
-                             p(self.h1t), p(self.h2t), p(self.dzt), p(self.dh2t), p(self.dh1t),
+                             p(self.h1t), p(self.w3p), p(self.dh2t), p(self.dh1t),
                              p(self.loss), p(self.correct), None, 1),
             "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
-                              p(self.h1t), p(self.h2t), p(self.dzt), p(self.dh2t), p(self.dh1t), p(self.slab),
+                              p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
                               self.slices, self.n_pad),
         }
         for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
@@ -348,7 +349,7 @@ class FusedMLPTrainer:
         n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, self.grad_scale,
-               n.ptr(self.h1t), n.ptr(self.h2t), n.ptr(self.dzt), n.ptr(self.dh2t), n.ptr(self.dh1t),
+               n.ptr(self.h1t), n.ptr(self.w3p), n.ptr(self.dh2t), n.ptr(self.dh1t),
                n.ptr(self.loss), n.ptr(self.correct), None, 0, n.stream_ptr())
 
     def _wgrad(self):
@@ -432,7 +433,7 @@ class FusedMLPTrainer:
         corr = torch.zeros(rows, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None,
                n.ptr(loss), n.ptr(corr), None, 0, n.stream_ptr())
         return StepStats(float(loss.mean()), float(corr.mean()), rows)
 
@@ -445,7 +446,7 @@ class FusedMLPTrainer:
         out = torch.empty(rows, CLASSES, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None,
                None, None, n.ptr(out), 0, n.stream_ptr())
         return out
 
