@@ -46,6 +46,9 @@ using namespace sl;
 #ifndef SL_MLP_SLICES
 #define SL_MLP_SLICES 14  // weight-gradient K slices: 18 tiles x 14 = 252 GEMM workgroups
 #endif
+#ifndef SL_L1_KO
+#define SL_L1_KO 0  // timing knockouts of mlp_l1_kernel (1 X loads, 2 X conversion, 3 MFMAs, 4 W1 loads)
+#endif
 #ifndef SL_W3_UNROLL
 #define SL_W3_UNROLL 16
 #endif
@@ -203,7 +206,9 @@ __device__ __forceinline__ void copy_part(const uint16_t* src, int ld, uint16_t*
 // WMG > 1 splits the waves into WMG row groups (each 16 * MF rows) so that the
 // NF weight fragments a wave streams feed MF m-fragments while halving the
 // LDS A-fragment traffic of the 1 x 8 layout at BM = 128.
-template <bool TRAIN, int BM, int WMG>
+// L1 = false: H1 was already computed by mlp_l1_kernel (train path); the tile is
+// staged from global into R1 and layer 1 / its H1 write are skipped.
+template <bool TRAIN, int BM, int WMG, bool L1 = true>
 __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpRowArgs a) {
   constexpr int NWV = BM / 16;       // waves per workgroup
   constexpr int MF = BM / 16 / WMG;  // m-fragments per wave
@@ -310,6 +315,14 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   // labels of this lane's 4 softmax rows (wave * 16 + 4 lg + r), fetched long before use
   const uint32_t lab4 = a.y ? *reinterpret_cast<const uint32_t*>(a.y + srow0 + wave * 16 + 4 * lg) : 0u;
 
+  if constexpr (!L1) {
+#pragma unroll
+    for (int q = tid; q < BM * (HID / 8); q += NT) {
+      const int r = q >> 5, c8 = (q & 31) * 8;
+      *reinterpret_cast<short8_t*>(R1 + r * HS_LD + c8) = ld8(a.h1 + (long)(row0 + r) * HID + c8);
+    }
+    stamp(1);
+  } else {
   zero_acc();
   {
     // X chunks c+1 .. c+XQ wait in registers (slot chunk % XQ): the u8 input
@@ -342,6 +355,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   }
   stamp(1);
   relu_out(a.b1, R1);
+  }
   __syncthreads();
   stamp(2);
 
@@ -356,7 +370,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
         },
         [&](int st, short8_t (&b)[NF]) { mfma_step(ha + st * 32, HS_LD, b); },
         [&](int st) {
-          if (TRAIN) copy_part<BM, NT, HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid, st);
+          if (TRAIN && L1) copy_part<BM, NT, HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid, st);
         });
   }
   stamp(3);
@@ -467,6 +481,178 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   __syncthreads();
   copy_out<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid);
   stamp(9);
+}
+
+
+// ---------------------------------------------------------------------------
+// Layer-1 forward of the train step as a weight-efficient GEMM:
+//   H1 = relu(Xn W1^T + b1)   (bf16 [batch][256] for the rows kernel and wgrad)
+// 128 x 128 tiles, 4 waves of 64 x 64, two workgroups per CU.  Inside the row-fused kernel every
+// 64-row workgroup streams all of W1 (426 KB) from L2 -- 32 KB per 64-wide K
+// chunk per 64 rows, more than L2 can feed the MFMAs (layer 1 was 47 % of that
+// kernel's cycles, profiles/r01_v11).  Here one staging of a W1 chunk in LDS
+// serves 128 rows (2x less L2 traffic per row) and every X element is
+// normalised once.  Two workgroups per CU: with one 8-wave 256-row workgroup
+// the per-chunk barrier kept both waves of a SIMD in phase (MFMA bursts, then
+// conversion bursts) and the MFMA pipe was busy 22 % of the time.  The two
+// column tiles of a row block are adjacent in the XCD remap, so they read
+// their X rows through one L2.  Register-staged double buffer: the W1 pieces of chunk c+1
+// and the X pieces of chunk c+2 (HBM) are in flight during chunk c's MFMAs.
+// ---------------------------------------------------------------------------
+constexpr int L1_BM = 128, L1_BN = 128, L1_NT = 256;
+constexpr int L1_A_LD = 72;                  // [128][72] bf16 A image (144-B rows, conflict-free b128 reads)
+constexpr int L1_A = L1_BM * L1_A_LD;        // elements
+constexpr int L1_B = 16 * 512;               // 8 n-tiles x 2 k-steps of fragment-ordered W1 (16 KB)
+constexpr int L1_SLOT = L1_A + L1_B;
+constexpr int L1_KSTEPS = (D_IN + 31) / 32;  // 25: the last holds 16 real columns
+constexpr int L1_NCH = (L1_KSTEPS + 1) / 2;  // 13 chunks of 64
+constexpr int L1_O_LD = L1_BN + 8;          // epilogue image row stride
+static_assert(L1_BM * L1_O_LD <= 2 * L1_SLOT, "epilogue image must fit the ring");
+
+struct L1Args {
+  const uint8_t* x;
+  const int* cursor;
+  int n_batches, batch;
+  const uint16_t* w1h;
+  const float* b1;
+  float xa, xb;
+  uint16_t* h1;
+};
+
+__global__ __launch_bounds__(L1_NT, 2) void mlp_l1_kernel(L1Args a) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * L1_SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const long row0 = (long)(tile >> 1) * L1_BM;
+  const int col0 = (tile & 1) * L1_BN, nt0 = col0 >> 4;
+  const long srow0 = batch_base(a.cursor, a.n_batches, a.batch) + row0;
+  const int wr = (wave & 1) * 64, wc = (wave >> 1) * 64;
+  const float nxa = a.xa + 0.f * (float)lane, nxb = a.xb + 0.f * (float)lane;  // VGPRs (constant-bus limit)
+
+  // X: 512 16-B pieces per chunk, rows tid/4 and tid/4 + 64
+  const int xr = tid >> 2, xc = (tid & 3) * 16;
+  const uint8_t* xg = a.x + (srow0 + xr) * D_IN + xc;
+  auto xload = [&](int c, uint4 (&v)[2]) {
+    const bool ok = c * 64 + xc < D_IN;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#if SL_L1_KO == 1
+      v[j] = make_uint4(c, j, 0, 0);
+#else
+      v[j] = ok ? *reinterpret_cast<const uint4*>(xg + (long)j * 64 * D_IN + c * 64) : make_uint4(0, 0, 0, 0);
+#endif
+  };
+  auto xstore = [&](int slot, int c, const uint4 (&v)[2]) {
+    const bool ok = c * 64 + xc < D_IN;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint16_t* d = smem + slot * L1_SLOT + (xr + 64 * j) * L1_A_LD + xc;
+#if SL_L1_KO == 2
+      *reinterpret_cast<uint4*>(d) = v[j];
+      *reinterpret_cast<uint4*>(d + 8) = v[j];
+#else
+      *reinterpret_cast<short8_t*>(d) = ok ? u8x8_to_bf16(make_uint2(v[j].x, v[j].y), nxa, nxb) : zero8();
+      *reinterpret_cast<short8_t*>(d + 8) = ok ? u8x8_to_bf16(make_uint2(v[j].z, v[j].w), nxa, nxb) : zero8();
+#endif
+    }
+  };
+  // W1: 16 fragments of 1 KB per chunk, 4 x 16 B per thread, copied in fragment order
+  auto wload = [&](int c, short8_t (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = tid + L1_NT * i, blk = p >> 6, l = p & 63;
+#if SL_L1_KO == 4
+      v[i] = zero8(); v[i][0] = (short)(c + blk + l);
+#else
+      v[i] = ld8(a.w1h + (long)((nt0 + (blk >> 1)) * KS1 + 2 * c + (blk & 1)) * 512 + l * 8);
+#endif
+    }
+  };
+  auto wstore = [&](int slot, const short8_t (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = tid + L1_NT * i;
+      *reinterpret_cast<short8_t*>(smem + slot * L1_SLOT + L1_A + p * 8) = v[i];
+    }
+  };
+
+  floatx4_t acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
+  auto compute = [&](int slot, int nks) {
+    const uint16_t* A = smem + slot * L1_SLOT;
+    const uint16_t* B = A + L1_A;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (kk < nks) {
+        short8_t af[4], bf[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) af[m] = lds8(A + (wr + m * 16 + lr) * L1_A_LD + kk * 32 + 8 * lg);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bf[n] = lds8(B + (((wc >> 4) + n) * 2 + kk) * 512 + lane * 8);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+#if SL_L1_KO == 3
+            acc[m][n][0] += (float)af[m][0] * (float)bf[n][1];
+#else
+            acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
+#endif
+          }
+      }
+    }
+  };
+
+  // prefetch distances (chunks): X from HBM L1_XD ahead, W1 (L2-resident) L1_WD ahead;
+  // one chunk of MFMAs is ~0.5 us, HBM latency under load ~2 us
+  constexpr int XD = 4, WD = 2;
+  uint4 xq[XD][2];
+  short8_t wq[WD][4];
+#pragma unroll
+  for (int i = 0; i < XD; ++i) xload(i, xq[i]);
+#pragma unroll
+  for (int i = 0; i < WD; ++i) wload(i, wq[i]);
+  xstore(0, 0, xq[0]);
+  wstore(0, wq[0]);
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < L1_NCH; ++c) {
+    if (c + XD < L1_NCH) xload(c + XD, xq[c % XD]);
+    if (c + WD < L1_NCH) wload(c + WD, wq[c % WD]);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(c & 1, L1_KSTEPS - 2 * c);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < L1_NCH) {
+      xstore((c + 1) & 1, c + 1, xq[(c + 1) % XD]);
+      wstore((c + 1) & 1, wq[(c + 1) % WD]);
+    }
+    __syncthreads();
+  }
+
+  // bias + ReLU -> bf16 image over the ring, then coalesced 16-B row stores
+  uint16_t* img = smem;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = wc + n * 16 + lr;
+    const float bias = a.b1[col0 + col];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        img[(wr + m * 16 + 4 * lg + r) * L1_O_LD + col] = f2bf(fmaxf(acc[m][n][r] + bias, 0.f));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = tid; q < L1_BM * (L1_BN / 8); q += L1_NT) {
+    const int r = q >> 4, c8 = (q & 15) * 8;
+    *reinterpret_cast<short8_t*>(a.h1 + (row0 + r) * HID + col0 + c8) =
+        *reinterpret_cast<const short8_t*>(img + r * L1_O_LD + c8);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -982,14 +1168,31 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.loss = loss; a.correct = correct; a.logits = logits;
   a.stamps = g_stamps;
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
+  // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_l1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);
   if (bm == 128) {
-    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 2>), dim3(batch / 128), dim3(512), 0, stream, a);
+    if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 2, false>), dim3(batch / 128), dim3(512), 0, stream, a);
+    else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 2>), dim3(batch / 128), dim3(512), 0, stream, a);
     else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, 2>), dim3(batch / 128), dim3(512), 0, stream, a);
   } else {
-    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
+    if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1, false>), dim3(batch / 64), dim3(256), 0, stream, a);
+    else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL((mlp_rows_kernel<false, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
   }
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+// Layer-1 forward GEMM of the train step (batch % 256 == 0): H1 for the rows
+// kernel's train == 2 mode and for the weight gradient.
+int sl_mlp_l1(const uint8_t* x, const int* cursor, int n_batches, int batch, const uint16_t* w1h,
+              const float* params, float xa, float xb, uint16_t* h1, hipStream_t stream) {
+  if (batch <= 0 || batch % L1_BM != 0 || !x || !h1 || !w1h || !params) return -1;
+  if (((uintptr_t)x & 15) != 0 || ((uintptr_t)h1 & 15) != 0) return -2;
+  L1Args a;
+  a.x = x; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
+  a.w1h = w1h; a.b1 = params + P_B1; a.xa = xa; a.xb = xb; a.h1 = h1;
+  hipLaunchKernelGGL(mlp_l1_kernel, dim3(batch / L1_BM * (HID / L1_BN)), dim3(L1_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }

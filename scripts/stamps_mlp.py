@@ -26,7 +26,7 @@ torch.cuda.synchronize()
 _native.call("sl_mlp_set_stamps", None)
 s = st.view(-1, 16)[:, :10].cpu().double()
 d = s[:, 1:] - s[:, :-1]
-names = ["layer1", "relu1+h1", "layer2", "relu2+h2", "layer3+ce+dz", "dH2 mfma", "mask+dh2", "dH1 mfma", "mask+dh1"]
+names = ["layer1", "relu1", "layer2+h1", "relu2", "layer3+ce", "dW3 part+dH2", "mask2", "dH1+dh2", "mask1+dh1"]
 print(f"B={B} BM={bm} workgroups={s.shape[0]}  total median cycles {float((s[:, 9] - s[:, 0]).median()):.0f}")
 for i, n in enumerate(names):
     print(f"  {n:14s} median {float(d[:, i].median()):8.0f}  mean {float(d[:, i].mean()):8.0f}")

@@ -277,6 +277,10 @@ class FusedMLPTrainer:
         self.slab = torch.empty(self.slices, self.n_pad, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        # layer 1 of the train step as a separate 128-row-tile GEMM (mlp_l1_kernel) when SL_MLP_L1=1.
+        # Off by default: it takes 49 us against the ~32 us that layer 1 costs inside the row-fused
+        # kernel (22 % MFMA busy, latency-bound; profiles/r01_v10)
+        self.l1_gemm = batch % 128 == 0 and os.environ.get("SL_MLP_L1", "0") == "1"
         self.allreduce = None  # callable(grad_tensor) -> None, sums in place (RCCL)
         self.x = self.y = None
         self.n_batches = 1
@@ -322,11 +326,13 @@ class FusedMLPTrainer:
         n, p = self._n, self._n.ptr
         ws = (p(self.w1h), p(self.w2h), p(self.w2th), p(self.w3h), p(self.w3th))
         lc = {
+            "l1": n.Launch("sl_mlp_l1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1h),
+                           p(self.params), self.xa, self.xb, p(self.h1t)),
             "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
                              p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
                              p(self.params), self.xa, self.xb, self.grad_scale,
                              p(self.h1t), p(self.w3p), p(self.dh2t), p(self.dh1t),
-                             p(self.loss), p(self.correct), None, 1),
+                             p(self.loss), p(self.correct), None, 2 if self.l1_gemm else 1),
             "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
                               self.slices, self.n_pad),
@@ -344,7 +350,10 @@ class FusedMLPTrainer:
 
     def _rows(self, train: bool = True):
         if train:
-            return self._launches()["rows"]()
+            lc = self._launches()
+            if self.l1_gemm:
+                lc["l1"]()
+            return lc["rows"]()
         n = self._n
         n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),

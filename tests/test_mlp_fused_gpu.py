@@ -37,8 +37,9 @@ def rows_bm():
     _native.call("sl_mlp_set_rows_bm", 0)
 
 
-@pytest.mark.parametrize("batch,bm", [(64, 64), (512, 64), (2048, 64), (512, 128), (2048, 128)])
-def test_gradients_match_reference(batch, bm, rows_bm):
+@pytest.mark.parametrize("batch,bm,l1", [(64, 64, True), (512, 64, True), (2048, 64, True), (512, 128, True),
+                                         (2048, 128, True), (2048, 64, False), (512, 128, False)])
+def test_gradients_match_reference(batch, bm, l1, rows_bm):
     from serverless_learn_amd.ops import _native
 
     rows_bm(bm)
@@ -46,6 +47,7 @@ def test_gradients_match_reference(batch, bm, rows_bm):
     x, y = _data(batch, seed=3)
     flat = M.init_params(2)
     tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
+    tr.l1_gemm = l1 and batch % 128 == 0  # layer 1 as the separate GEMM or inside the rows kernel
     tr.load_shard(x, y)
     g = tr.compute_grads().cpu()
     torch.cuda.synchronize()
@@ -63,6 +65,22 @@ def test_gradients_match_reference(batch, bm, rows_bm):
     st = tr.stats()
     assert abs(st.loss - float(loss) / batch) < 2e-2
     assert abs(st.accuracy - float(correct) / batch) < 0.05
+
+
+def test_layer1_gemm_matches_row_fused_layer1():
+    """mlp_l1_kernel's H1 is bit-identical to the rows kernel's own layer 1 (same k order)."""
+    batch = 1024
+    x, y = _data(batch, seed=7)
+    flat = M.init_params(4)
+    h = []
+    for l1 in (True, False):
+        tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
+        tr.l1_gemm = l1
+        tr.load_shard(x, y)
+        tr.compute_grads()
+        torch.cuda.synchronize()
+        h.append(tr.h1t.clone())
+    assert torch.equal(h[0], h[1]), float((h[0].float() - h[1].float()).abs().max())
 
 
 def test_sgd_step_matches_reference():
