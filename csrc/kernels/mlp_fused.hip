@@ -13,18 +13,17 @@
 //           and stream from L2 through a 4-deep per-wave register ring; ReLU
 //           masks are re-derived from the activations kept in LDS.  H1, dH2
 //           and dH1 are written row-major with coalesced 16-B stores for the
-//           weight gradient; [dW3 | db3] (10 x 257) is computed here from the
-//           LDS images as one fp32 partial per 64 rows, so H2 and dZ never
-//           reach HBM.
+//           weight gradient; [dW3 | db3] (10 x 257) and the bias gradients
+//           db1 / db2 are computed here from the LDS images as one fp32
+//           partial row per 64 rows, so H2 and dZ never reach HBM.
 //   K_wgrad (mlp_wgrad_kernel) grouped split-K GEMM dW = dH^T . A over the
-//           batch for dW1 (A = raw u8 X) and dW2 (A = H1): 128x128 tiles; both
+//           batch for dW1 (A = raw u8 X) and dW2 (A = H1): 256x128 tiles; both
 //           operands stream global -> LDS by LDS-DMA (global_load_lds_dwordx4,
-//           no VGPR staging) into a 4-slot ring of XOR-swizzled [64 batch
-//           rows][128] images (three stages in flight, counted vmcnt + raw
-//           s_barrier), read transposed with ds_read_b64_tr_b16/_b8; bias
-//           gradients come from an extra MFMA against a ones fragment.
-//           Deterministic fp32 slabs.  The spare CUs of its grid sum the rows
-//           kernel's dW3 partials into the slab.
+//           no VGPR staging) into a 3-slot ring of XOR-swizzled [64 batch
+//           rows][128] images (two stages in flight, counted vmcnt + raw
+//           s_barrier), read transposed with ds_read_b64_tr_b16/_b8.
+//           Deterministic fp32 slabs; each workgroup also sums a band of the
+//           rows kernel's partial rows ([dW3 | db3 | db1 | db2]) over its slice.
 //   K_sgd   (mlp_sgd_kernel)   slab reduction (+ optional all-reduce
 //           hand-off) + momentum SGD on fp32 master weights, refreshing the
 //           bf16 shadow weights (and the transposed copies the backward pass
@@ -44,13 +43,16 @@ using namespace sl;
 #define SL_MLP_RING2 4
 #endif
 #ifndef SL_MLP_SLICES
-#define SL_MLP_SLICES 14  // weight-gradient K slices: 18 tiles x 14 = 252 GEMM workgroups
+#define SL_MLP_SLICES 28  // weight-gradient K slices: 9 tiles x 28 = 252 GEMM workgroups
 #endif
 #ifndef SL_L1_KO
 #define SL_L1_KO 0  // timing knockouts of mlp_l1_kernel (1 X loads, 2 X conversion, 3 MFMAs, 4 W1 loads)
 #endif
-#ifndef SL_W3_UNROLL
-#define SL_W3_UNROLL 16
+#ifndef SL_WG_PRIO
+#define SL_WG_PRIO 0  // s_setprio(1) around the wgrad MFMA bursts
+#endif
+#ifndef SL_WG_KO
+#define SL_WG_KO 0  // timing knockouts of mlp_wgrad_kernel (1 no MFMAs, 2 no LDS-DMA after stage 0)
 #endif
 #ifndef SL_MLP_XQ
 #define SL_MLP_XQ 4  // X prefetch distance in 64-column chunks (4 measured +1% over 2)
@@ -75,9 +77,12 @@ constexpr long P_B2 = P_W2 + (long)HID * HID;
 constexpr long P_W3 = P_B2 + HID;
 constexpr long P_B3 = P_W3 + (long)NC * HID;
 constexpr long P_N = P_B3 + NC;  // 269322
-// Per-64-row partials of [dW3 | db3] (2570 values, flat order from P_W3), padded rows.
+// Per-64-row partial rows of the rows kernel: [dW3 | db3] (2570 values, flat order
+// from P_W3), then the column sums of dH1 and dH2 (db1 / db2 partials).
 constexpr int W3P_N = NC * HID + NC;
-constexpr int W3P_LD = 2576;
+constexpr int W3P_DB1 = 2576;
+constexpr int W3P_DB2 = W3P_DB1 + HID;
+constexpr int W3P_LD = W3P_DB2 + HID;  // 3088
 }  // namespace
 
 // Weights are kept in MFMA B-fragment order: for a [N][K] matrix (K
@@ -113,7 +118,7 @@ struct MlpRowArgs {
   const float *b1, *b2, *b3;
   float xa, xb, grad_scale;
   uint16_t* h1;                        // row-major [batch][256]
-  float* w3p;                          // [batch / 64][W3P_LD] partial [dW3 | db3]
+  float* w3p;                          // [batch / 64][W3P_LD] partial [dW3 | db3 | db1 | db2]
   uint16_t *dh2, *dh1;                 // row-major [batch][256]
   float *loss, *correct, *logits;
   unsigned long long* stamps;  // diagnostics: per-workgroup phase timestamps (nullptr in production)
@@ -463,6 +468,26 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   masked_out(R0);
   __syncthreads();
   stamp(7);
+  // column sums of the masked dH2 over this wave's 64 rows: the db2 partial (ones-row MFMA)
+  auto col_sums = [&](const uint16_t* img, int off) {
+    short8_t ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
+    floatx4_t cs[NF];
+#pragma unroll
+    for (int n = 0; n < NF; ++n) cs[n] = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int n = 0; n < NF; ++n)
+        cs[n] = mfma16(ones, lds_tr8(img + (rw + 32 * ks) * HS_LD + cw + n * 16, HS_LD, lane), cs[n]);
+    if (lg == 0) {
+      float* part = a.w3p + (long)((row0 + rw) >> 6) * W3P_LD + off;
+#pragma unroll
+      for (int n = 0; n < NF; ++n) part[cw + n * 16 + lr] = cs[n][0];
+    }
+  };
+  col_sums(R0, W3P_DB2);
 
   // ---- dH1 = (dH2 W2) * 1[H1 > 0], K = 256; A = R0, out -> R1 ----
   zero_acc();
@@ -480,6 +505,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   masked_out(R1);
   __syncthreads();
   copy_out<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid);
+  col_sums(R1, W3P_DB1);
   stamp(9);
 }
 
@@ -656,12 +682,18 @@ __global__ __launch_bounds__(L1_NT, 2) void mlp_l1_kernel(L1Args a) {
 }
 
 // ---------------------------------------------------------------------------
-// Weight-gradient grouped split-K GEMM:  G[m][n] = sum_b A[b][m] * Bop[b][n]
-// (+ db[m] = sum_b A[b][m]), A and Bop row-major over the batch index b.
+// Weight-gradient grouped split-K GEMM:  G[m][n] = sum_b A[b][m] * Bop[b][n],
+// A = dH1 / dH2 ([batch][256] bf16), Bop = raw u8 X / bf16 H1, row-major over b.
 //
-// Workgroup tile 128 (m) x 128 (n), 4 waves of 64 x 64.  One K slice of the
-// batch per workgroup; grid order is slice-major after the XCD remap, so all
-// tiles of one slice -- which read the same batch rows -- share an L2.
+// Workgroup tile 256 (m: all of dH) x 128 (n); 8 waves as 4 (m) x 2 (n) of
+// 64 x 64, every wave over the whole 64-row stage: 32 MFMAs per wave per
+// barrier.  (The previous 128 x 128 tile, two k-halves of 16 MFMAs per
+// barrier, ran at 22 % MFMA busy: profiles/r01_v10.)  One K slice of the
+// batch per workgroup; grid order is slice-major after the XCD remap, so the
+// 9 tiles of one slice -- which read the same batch rows -- share an L2.
+// 3-slot LDS ring of 48 KB stages (A as two swizzled [64][128] halves, then B)
+// fed by LDS-DMA, counted vmcnt + raw s_barrier; k-step 1's fragment reads are
+// in flight under k-step 0's MFMAs.
 //
 // dW1's B operand is the RAW u8 input, not a normalised bf16 copy: pixels
 // 0..255 are exact in bf16, so the kernel computes S = dH1^T X exactly and
@@ -671,15 +703,21 @@ __global__ __launch_bounds__(L1_NT, 2) void mlp_l1_kernel(L1Args a) {
 // per 65,536-row step.  The u8 image is read with ds_read_b64_tr_b8 (probed
 // lane map, scripts/probes/tr8_probe.hip: per 16-lane group, lane 2q+p
 // addresses row q bytes 8p..8p+7; lane i receives column i of the 8 rows).
+// dW1 has 784 columns: its 7th tile holds 16 real ones, and the waves past
+// them skip their MFMAs (the tile count per slice stays 9).
+//
+// The rows kernel writes per-64-row partial rows: [dW3 | db3] and the column
+// sums of dH1 / dH2 (db1 / db2).  Before its main loop each workgroup sums a
+// band of those columns over its slice's stages into the slice's slab, so the
+// slab carries every gradient and mlp_sgd_kernel needs no special case.
 // ---------------------------------------------------------------------------
 struct WgProblem {
-  const void* a;  // [batch][lda] bf16: dH1 / dH2 / dZ
-  int lda;
-  const void* b;  // [batch][ldb]: u8 X (problem 0) / bf16 H1 / H2
+  const void* a;  // [batch][256] bf16: dH1 / dH2
+  const void* b;  // [batch][ldb]: u8 X (problem 0) / bf16 H1
   int ldb;
-  int m_real, n_real;
-  int tiles_m, tiles_n, tile_base;
-  long w_off, b_off;  // flat destinations of dW ([m_real][n_real]) and db
+  int n_real, tiles_n, tile_base;
+  long w_off, b_off;  // flat destinations of dW ([256][n_real]) and db
+  int bias_part;      // this problem's db partial inside the rows kernel's partial rows
 };
 struct WgArgs {
   WgProblem p[2];  // dW1 (u8 X), dW2 (H1); dW3 comes from the rows kernel's partials
@@ -689,16 +727,15 @@ struct WgArgs {
   long slab_stride;
   const int* cursor;  // X is the resident shard: rows start at batch_base(cursor)
   int n_batches, batch;
-  int gemm_wgs, slices;  // blocks >= gemm_wgs reduce the rows kernel's [dW3 | db3] partials
-  const float* w3p;      // [n_w3p][W3P_LD]
+  const float* w3p;      // [n_w3p][W3P_LD] partial rows of the rows kernel
   int n_w3p;
 };
 
-constexpr int WG_NSLOT = 4;               // LDS ring slots (128 KB): three stages in flight (5 measured no better)
+constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages in flight
 constexpr int WG_IMG = 64 * 128;          // one [64 k][128] bf16 image, unpadded (swizzled)
-constexpr int WG_SLOT = 2 * WG_IMG;       // A image + B image = 32 KB
+constexpr int WG_SLOT = 3 * WG_IMG;       // A half 0, A half 1, B = 48 KB
 constexpr int WG_OUT_LD = 128 + 4;        // fp32 epilogue tile
-static_assert((128 * WG_OUT_LD + 128) * 4 <= WG_NSLOT * WG_SLOT * 2, "epilogue tile must fit the ring");
+static_assert(256 * WG_OUT_LD * 4 <= WG_NSLOT * WG_SLOT * 2, "epilogue tile must fit the ring");
 
 // 16-B chunk position inside a 256-B image row.  XOR on chunk-pair bits with
 // f(r) = (r & 3) | ((r >> 3) & 1) << 2 makes every ds_read_b64_tr_b16 of the
@@ -781,86 +818,31 @@ __device__ __forceinline__ void wg_vmcnt(int younger) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// 8 waves: waves 0-3 take k-step 0 (batch rows 0-31) of every 64-row stage,
-// waves 4-7 k-step 1 (rows 32-63), each as a 2 x 2 grid of 64 x 64 sub-tiles;
-// the two k-halves are summed through LDS in the epilogue.  Two waves per SIMD
-// let one wave's LDS reads / barrier wait run under the other's MFMAs (at one
-// wave per SIMD the pipe was busy 25 % of the time, profiles/r01_v6).
 constexpr int WG_NT = 512;
-
-// [dW3 | db3] = sum over the rows kernel's per-64-row partials, computed by the
-// few workgroups the GEMM grid leaves over (18 tiles x 14 slices = 252 of 256
-// CUs), so it costs no time on the critical path.  Reducer r takes a band of
-// float4 columns; G row groups per column, 16 loads in flight per thread, then a
-// fixed-order sum through LDS (deterministic).  The result goes to slab slice
-// 0 and zeros to the other slices, so mlp_sgd_kernel needs no special case.
-__device__ __forceinline__ void w3_reduce(const WgArgs& A, float4* red, int r, int nr) {
-  constexpr int NCOL = W3P_LD / 4;
-  const int cpw = (NCOL + nr - 1) / nr;  // <= 322 columns: G >= 1
-  const int G = WG_NT / cpw;
-  const int t = threadIdx.x, col = t % cpw, g = t / cpw;
-  const int c = r * cpw + col;
-  const bool act = g < G && c < NCOL;
-  if (act) {
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4* src = reinterpret_cast<const float4*>(A.w3p) + c;
-#pragma unroll SL_W3_UNROLL
-    for (int b = g; b < A.n_w3p; b += G) {
-      const float4 v = src[(long)b * NCOL];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    red[g * cpw + col] = s;
-  }
-  __syncthreads();
-  if (act && g == 0) {
-    float4 tot = red[col];
-    for (int i = 1; i < G; ++i) {
-      const float4 v = red[i * cpw + col];
-      tot.x += v.x; tot.y += v.y; tot.z += v.z; tot.w += v.w;
-    }
-    const float tv[4] = {tot.x, tot.y, tot.z, tot.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = 4 * c + j;
-      if (q < W3P_N) {
-        A.slab[P_W3 + q] = tv[j];
-        for (int sl = 1; sl < A.slices; ++sl) A.slab[(long)sl * A.slab_stride + P_W3 + q] = 0.f;
-      }
-    }
-  }
-}
 
 __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_NSLOT * WG_SLOT];
-  if ((int)blockIdx.x >= A.gemm_wgs) {  // block-uniform
-#ifdef SL_W3_SKIP  // timing experiments only
-    return;
-#endif
-    w3_reduce(A, reinterpret_cast<float4*>(smem), (int)blockIdx.x - A.gemm_wgs, (int)gridDim.x - A.gemm_wgs);
-    return;
-  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
-  const int kg = wave >> 2, w4 = wave & 3;
+  const int wm = wave & 3, wn = wave >> 2;
   const int lr = lane & 15, lg = lane >> 4;
-  const int logical = xcd_remap(blockIdx.x, A.gemm_wgs);
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int s = logical / A.total_tiles;
   const int t = logical - s * A.total_tiles;
   const int pi = t >= A.p[1].tile_base ? 1 : 0;
   const WgProblem& P = A.p[pi];
-  const int lt = t - P.tile_base;
-  const int tm = lt / P.tiles_n, tn = lt - tm * P.tiles_n;
-  const int m0 = tm * 128, n0 = tn * 128;
-  const int wm = w4 >> 1, wn = w4 & 1;
+  const int tn = t - P.tile_base;
+  const int n0 = tn * 128;
   const int st0 = s * A.steps_per_slice;
   const int nst = min(A.steps_per_slice, A.total_steps - st0);
-  const bool do_bias = tn == 0 && wn == 0;
   const bool u8b = pi == 0;
+  // n-blocks of this wave that hold real columns (dW1's last tile: 16 columns)
+  const int nvalid = __builtin_amdgcn_readfirstlane(min(4, max(0, (P.n_real - n0 - wn * 64 + 15) / 16)));
 
-  // LDS-DMA map (bf16 images): wave w, piece j (0..1) covers image rows 4 (2w + j) .. +3;
-  // lane -> row 4 (2w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row).
-  // u8 image: wave w covers rows 8w .. 8w+7; lane -> row + lane / 8,
-  // LDS chunk lane % 8 <- global chunk swz8(lane % 8, row).
+  // LDS-DMA map: bf16 [64][128] images -- wave w, piece j (0..1) covers rows 4 (2w + j) .. +3,
+  // lane -> row 4 (2w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row);
+  // A is two such images (m 0..127, 128..255).  u8 image: wave w covers rows 8w .. 8w+7,
+  // lane -> row + lane / 8, LDS chunk lane % 8 <- global chunk swz8(lane % 8, row).
   const int prow = lane >> 4;
   const uint16_t* asrc[2];
   const uint16_t* bsrc[2];
@@ -869,7 +851,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   for (int j = 0; j < 2; ++j) {
     const int row = 4 * (2 * wave + j) + prow;
     const int c = wg_swz(lane & 15, row);
-    asrc[j] = static_cast<const uint16_t*>(P.a) + (long)(st0 * 64 + row) * P.lda + m0 + c * 8;
+    asrc[j] = static_cast<const uint16_t*>(P.a) + (long)(st0 * 64 + row) * HID + c * 8;
     bsrc[j] = static_cast<const uint16_t*>(P.b) + (long)(st0 * 64 + row) * P.ldb + n0 + c * 8;
   }
   const uint8_t* bsrc8;
@@ -879,147 +861,187 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     const int col = min(n0 + c * 16, P.ldb - 16);  // columns >= 784 are don't-care columns of dW1
     bsrc8 = static_cast<const uint8_t*>(P.b) + (xrow0 + st0 * 64 + row) * P.ldb + col;
   }
-  auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % 4
+  auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % 3
     constexpr bool U8 = decltype(u8_c)::value;
+#if SL_WG_KO == 2  // timing knockout: no operand movement (stage 0 only)
+    if (st > 0) return;
+#endif
     uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
-    uint16_t* Bi = Ai + WG_IMG;
+    uint16_t* Bi = Ai + 2 * WG_IMG;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int rbase = 4 * (2 * wave + j) * 128;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(asrc[j] + (long)st * 64 * P.lda),
-                                       (SL_LDS void*)(Ai + rbase), 16, 0, 0);
-      if constexpr (!U8)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[j] + (long)st * 64 * P.ldb),
-                                         (SL_LDS void*)(Bi + rbase), 16, 0, 0);
-    }
-    if constexpr (U8)
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(asrc[j] + (long)st * 64 * HID + h * 128),
+            (SL_LDS void*)(Ai + h * WG_IMG + 4 * (2 * wave + j) * 128), 16, 0, 0);
+    if constexpr (U8) {
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc8 + (long)st * 64 * P.ldb),
                                        (SL_LDS void*)(reinterpret_cast<uint8_t*>(Bi) + 8 * wave * 128), 16, 0, 0);
-  };
-
-  floatx4_t acc[4][4], accb[4];
+    } else {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    accb[i] = zero4();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
-  }
-  short8_t ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
-
-  // per-lane tr-read addresses, computed once; this wave's k-half is a constant byte offset
-  const uint32_t lds_base = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
-  uint32_t a_addr[4], b_addr[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) a_addr[i] = wg_tr_addr(wm * 64 + i * 16, lane) + kg * (32 * 128 * 2);
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    b_addr[j] = u8b ? wg_tr8_addr(wn * 64 + j * 16, lane) + kg * (32 * 128) : wg_tr_addr(wn * 64 + j * 16, lane) + kg * (32 * 128 * 2);
-
-  // The main loop is instantiated per (u8, bias) combination and selected
-  // by a scalar branch OUTSIDE it: with the conditions inside, hipcc treated
-  // them as divergent and copied all 64 accumulators AGPR<->VGPR on every stage.
-  auto mainloop = [&](auto u8_c, auto bias_c) {
-    constexpr bool U8 = decltype(u8_c)::value, BIAS = decltype(bias_c)::value;
-    constexpr int PPS = U8 ? 3 : 4;  // LDS-DMA pieces per wave per stage
-    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, u8_c);
-    for (int st = 0; st < nst; ++st) {
-      wg_vmcnt<PPS>(min(WG_NSLOT - 2, nst - 1 - st));  // this wave's pieces of stage st have landed
-      __builtin_amdgcn_s_barrier();  // ... everyone's have; the slot of stage st-1 is free
-      if (st + WG_NSLOT - 1 < nst) issue(st + WG_NSLOT - 1, u8_c);
-      {
-        const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
-        short8_t af[4], bf[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = wg_tr8<0>(sb + a_addr[i]);
-        if constexpr (U8) {
-          uint2v_t raw[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) raw[j] = ds_tr8_off<WG_IMG * 2>(sb + b_addr[j]);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            bf[j] = u8x8_exact_bf16(raw[j]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) bf[j] = wg_tr8<WG_IMG * 2>(sb + b_addr[j]);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-        }
-        if constexpr (BIAS) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) accb[i] = mfma16(af[i], ones, accb[i]);
-        }
-      }
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[j] + (long)st * 64 * P.ldb),
+                                         (SL_LDS void*)(Bi + 4 * (2 * wave + j) * 128), 16, 0, 0);
     }
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
   if (u8b) {
-    if (do_bias) mainloop(T_{}, T_{});
-    else mainloop(T_{}, F_{});
-  } else if (do_bias) {
-    mainloop(F_{}, T_{});
+    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, T_{});
   } else {
-    mainloop(F_{}, F_{});
+    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, F_{});
   }
+
+  // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
+  // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
+  // a fixed-order sum through LDS (deterministic).  Scratch in ring slot 2, whose first
+  // LDS-DMA (stage 2) is issued after the main loop's first barrier. ----
+  {
+    constexpr int NC4 = W3P_LD / 4;
+    const int per = (NC4 + A.total_tiles - 1) / A.total_tiles;
+    const int c0 = t * per, nc = min(NC4, c0 + per) - c0;
+    float4* red = reinterpret_cast<float4*>(smem + 2 * WG_SLOT);
+    const int G = WG_NT / nc, col = tid % nc, g = tid / nc;
+    if (g < G) {
+      const float4* src = reinterpret_cast<const float4*>(A.w3p + (long)st0 * W3P_LD) + c0 + col;
+      float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+      for (int k = g; k < nst; k += G) {
+        const float4 v = src[(long)k * NC4];
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+      }
+      red[g * nc + col] = sum;
+    }
+    __syncthreads();
+    if (g == 0) {
+      float4 tot = red[col];
+      for (int i = 1; i < G; ++i) {
+        const float4 v = red[i * nc + col];
+        tot.x += v.x; tot.y += v.y; tot.z += v.z; tot.w += v.w;
+      }
+      const float tv[4] = {tot.x, tot.y, tot.z, tot.w};
+      float* out = A.slab + (long)s * A.slab_stride;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = 4 * (c0 + col) + j;
+        if (q < W3P_N) out[P_W3 + q] = tv[j];
+        else if (q >= W3P_DB1 && q < W3P_DB2) out[P_B1 + q - W3P_DB1] = tv[j];
+        else if (q >= W3P_DB2) out[P_B2 + q - W3P_DB2] = tv[j];
+      }
+    }
+  }
+
+  floatx4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+
+  // per-lane tr-read byte addresses within a slot; k-step 1 is a constant offset
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
+  uint32_t a_addr[4], b_addr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a_addr[i] = (wm >> 1) * WG_IMG * 2 + wg_tr_addr((wm & 1) * 64 + i * 16, lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    b_addr[j] = 2 * WG_IMG * 2 + (u8b ? wg_tr8_addr(wn * 64 + j * 16, lane) : wg_tr_addr(wn * 64 + j * 16, lane));
+
+  // Instantiated per (u8, live n-blocks) and selected by a scalar branch OUTSIDE
+  // the loop (conditions inside made hipcc copy every accumulator AGPR<->VGPR).
+  auto mainloop = [&](auto u8_c, auto nb_c) {
+    constexpr bool U8 = decltype(u8_c)::value;
+    constexpr int NB = decltype(nb_c)::value;
+    constexpr int PPS = U8 ? 5 : 6;  // LDS-DMA pieces per wave per stage
+    constexpr int KB = U8 ? 4096 : 8192;  // byte offset of k-step 1 in the B image
+    for (int st = 0; st < nst; ++st) {
+      wg_vmcnt<PPS>(min(WG_NSLOT - 2, nst - 1 - st));  // this wave's pieces of stage st have landed
+      __builtin_amdgcn_s_barrier();  // ... everyone's have; the slot of stage st-1 is free
+      if (st + WG_NSLOT - 1 < nst) issue(st + WG_NSLOT - 1, u8_c);
+      if constexpr (NB > 0) {
+        const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
+        short8_t a0[4], a1[4], b0[NB], b1[NB];
+        uint2v_t r0[NB], r1[NB];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a0[i] = wg_tr8<0>(sb + a_addr[i]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (U8) r0[j] = ds_tr8_off<0>(sb + b_addr[j]);
+          else b0[j] = wg_tr8<0>(sb + b_addr[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a1[i] = wg_tr8<8192>(sb + a_addr[i]);
+        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // k-step 0's reads (a1's 8 still in flight)
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (U8) {
+#pragma unroll
+          for (int j = 0; j < NB; ++j) b0[j] = u8x8_exact_bf16(r0[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (U8) r1[j] = ds_tr8_off<KB>(sb + b_addr[j]);
+          else b1[j] = wg_tr8<KB>(sb + b_addr[j]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#if SL_WG_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (U8) {
+#pragma unroll
+          for (int j = 0; j < NB; ++j) b1[j] = u8x8_exact_bf16(r1[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+#if SL_WG_PRIO
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(0);
+#endif
+      }
+    }
+  };
+  using I4 = std::integral_constant<int, 4>;
+  using I1 = std::integral_constant<int, 1>;
+  using I0 = std::integral_constant<int, 0>;
+#if SL_WG_KO == 1  // timing knockout: no fragment reads / MFMAs
+  if (u8b) mainloop(T_{}, I0{});
+  else mainloop(F_{}, I0{});
+#else
+  if (u8b) {
+    if (nvalid >= 4) mainloop(T_{}, I4{});
+    else if (nvalid >= 1) mainloop(T_{}, I1{});
+    else mainloop(T_{}, I0{});
+  } else {
+    mainloop(F_{}, I4{});
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---- epilogue: k-half 1 parks its tile in LDS, k-half 0 adds and stores fp32 rows to the slab ----
+  // ---- epilogue: the fp32 tile through LDS, then float4 rows into slab slice s ----
   float* Os = reinterpret_cast<float*>(smem);
-  float* Ob = Os + 128 * WG_OUT_LD;  // bias partials of k-half 1
-  if (kg == 1) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Os[(wm * 64 + i * 16 + 4 * lg + r) * WG_OUT_LD + wn * 64 + j * 16 + lr] = acc[i][j][r];
-    if (do_bias && lr == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Ob[wm * 64 + i * 16 + 4 * lg + r] = accb[i][r];
-    }
-  }
+      for (int r = 0; r < 4; ++r)
+        Os[(wm * 64 + i * 16 + 4 * lg + r) * WG_OUT_LD + wn * 64 + j * 16 + lr] = acc[i][j][r];
   __syncthreads();
-  float* out = A.slab + (long)s * A.slab_stride;
-  if (kg == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Os[(wm * 64 + i * 16 + 4 * lg + r) * WG_OUT_LD + wn * 64 + j * 16 + lr] += acc[i][j][r];
-    if (do_bias && lr == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ml = wm * 64 + i * 16 + 4 * lg + r;
-          if (m0 + ml < P.m_real) out[P.b_off + m0 + ml] = accb[i][r] + Ob[ml];
-        }
-    }
-  }
-  __syncthreads();
-  for (int q = tid; q < 128 * 32; q += WG_NT) {
+  float* out = A.slab + (long)s * A.slab_stride + P.w_off;
+  for (int q = tid; q < 256 * 32; q += WG_NT) {
     const int rl = q >> 5, c4 = (q & 31) * 4;
-    const int m = m0 + rl, n = n0 + c4;
-    if (m < P.m_real && n < P.n_real)
-      *reinterpret_cast<float4*>(out + P.w_off + (long)m * P.n_real + n) =
-          *reinterpret_cast<const float4*>(Os + rl * WG_OUT_LD + c4);
+    const int n = n0 + c4;
+    if (n < P.n_real)
+      *reinterpret_cast<float4*>(out + (long)rl * P.n_real + n) = *reinterpret_cast<const float4*>(Os + rl * WG_OUT_LD + c4);
   }
 }
 
@@ -1081,14 +1103,27 @@ __device__ __forceinline__ void sgd_apply(const SgdArgs& a, long p, float gme) {
   write_shadow(a, p, w);
 }
 
+// SGD_TPG threads per float4 group of parameters: each sums every SGD_TPG-th
+// slab slice, the group combines by DPP (quad perms, then row_half_mirror for 8).
+#ifndef SL_SGD_TPG
+#define SL_SGD_TPG 4
+#endif
+constexpr int SGD_TPG = SL_SGD_TPG;
+static_assert(SGD_TPG == 4 || SGD_TPG == 8, "4 or 8 threads per group");
+__device__ __forceinline__ float group_sum(float v) {
+  v = quad_sum(v);
+  if constexpr (SGD_TPG == 8) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  return v;
+}
+
 __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int part = (int)(t & 3);
-  const long p0 = (t >> 2) * 4;
-  if (p0 >= a.n) return;  // whole quads exit together (n groups are quad-aligned in t)
+  const int part = (int)(t % SGD_TPG);
+  const long p0 = (t / SGD_TPG) * 4;
+  if (p0 >= a.n) return;  // whole groups exit together (n groups are group-aligned in t)
   const long p = p0 + part;
-  const bool mine = p < a.n;
+  const bool mine = part < 4 && p < a.n;
   if (a.mode == 0) {
     // shadow refresh only (after init / checkpoint load / gossip mixing)
     if (mine) write_shadow(a, p, a.w[p]);
@@ -1100,18 +1135,18 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
   if (a.slab) {
     if (full) {
       const float* src = a.slab + p0;
-      for (int sidx = part; sidx < a.slices; sidx += 4) {
+      for (int sidx = part; sidx < a.slices; sidx += SGD_TPG) {
         const float4 v = *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride);
         g[0] += v.x; g[1] += v.y; g[2] += v.z; g[3] += v.w;
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) g[j] = quad_sum(g[j]);
-      gme = g[part];
-      if (p0 < P_B1) {  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per quad
+      for (int j = 0; j < 4; ++j) g[j] = group_sum(g[j]);
+      gme = g[part & 3];
+      if (p0 < P_B1) {  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per group
         const float* dbs = a.slab + P_B1 + p0 / D_IN;
         float db = 0.f;
-        for (int sidx = part; sidx < a.slices; sidx += 4) db += dbs[(long)sidx * a.slab_stride];
-        db = quad_sum(db);
+        for (int sidx = part; sidx < a.slices; sidx += SGD_TPG) db += dbs[(long)sidx * a.slab_stride];
+        db = group_sum(db);
         gme = a.xa * gme + a.xb * db;
       }
     } else {
@@ -1218,25 +1253,22 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
   if (s_eff <= 0 || s_eff != slices) return -1;
   WgArgs a;
   // dW1, db1 = dH1^T [256 x B] . X (raw u8; normalised in mlp_sgd_kernel)
-  a.p[0] = WgProblem{dh1, HID, x, D_IN, HID, D_IN, HID / 128, (D_IN + 127) / 128, 0, P_W1, P_B1};
+  a.p[0] = WgProblem{dh1, x, D_IN, D_IN, (D_IN + 127) / 128, 0, P_W1, P_B1, W3P_DB1};
   // dW2, db2 = dH2^T . H1
-  a.p[1] = WgProblem{dh2, HID, h1, HID, HID, HID, HID / 128, HID / 128, 0, P_W2, P_B2};
+  a.p[1] = WgProblem{dh2, h1, HID, HID, HID / 128, 0, P_W2, P_B2, W3P_DB2};
   int base = 0;
   for (int i = 0; i < 2; ++i) {
     a.p[i].tile_base = base;
-    base += a.p[i].tiles_m * a.p[i].tiles_n;
+    base += a.p[i].tiles_n;
   }
   a.total_tiles = base;
   a.total_steps = batch / 64;
   a.steps_per_slice = (a.total_steps + slices - 1) / slices;
   a.slab = slab; a.slab_stride = slab_stride;
   a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
-  a.gemm_wgs = base * slices; a.slices = slices;
   a.w3p = w3p; a.n_w3p = n_w3p;
-  // reducers on the CUs the GEMM grid leaves idle (at least 2, at most 8)
-  const int reducers = std::min(8, std::max(2, 256 - a.gemm_wgs));
   if (((uintptr_t)x & 15) != 0 || ((uintptr_t)w3p & 15) != 0) return -2;  // 16-B pieces / float4 reads
-  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(a.gemm_wgs + reducers), dim3(WG_NT), 0, stream, a);
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(WG_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
@@ -1254,7 +1286,7 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   if (mode == 1 && !grad_out) return -1;
   if (slab && (slab_stride & 3)) return -1;
   const long groups = (P_N + 3) / 4;
-  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * 4 + 255) / 256), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + 255) / 256), dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }

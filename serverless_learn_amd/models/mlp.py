@@ -34,7 +34,7 @@ CLASSES = 10
 MNIST_MEAN = 0.1307
 MNIST_STD = 0.3081
 BLOCK_ROWS = 64  # batch rows per workgroup of the fused row kernel
-W3P_LD = 2576  # row stride of the rows kernel's [dW3 | db3] partials (2,570 used)
+W3P_LD = 3088  # row stride of the rows kernel's partial rows: [dW3 | db3 | pad | db1 | db2]
 
 LAYOUT = (
     ("fc1.weight", (HIDDEN, D_IN)),
@@ -326,8 +326,6 @@ class FusedMLPTrainer:
         n, p = self._n, self._n.ptr
         ws = (p(self.w1h), p(self.w2h), p(self.w2th), p(self.w3h), p(self.w3th))
         lc = {
-            "l1": n.Launch("sl_mlp_l1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1h),
-                           p(self.params), self.xa, self.xb, p(self.h1t)),
             "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
                              p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
                              p(self.params), self.xa, self.xb, self.grad_scale,
@@ -337,6 +335,9 @@ class FusedMLPTrainer:
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
                               self.slices, self.n_pad),
         }
+        if self.l1_gemm:
+            lc["l1"] = n.Launch("sl_mlp_l1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1h),
+                                p(self.params), self.xa, self.xb, p(self.h1t))
         for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
                                                         "reduce": (1, False, True, False),
                                                         "update": (2, True, False, True)}.items():

@@ -77,6 +77,8 @@ def lib():
                 build_kernels()
             handle = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
             for name in _SIGS:
+                if path != KERNELS_SO and not hasattr(handle, name):
+                    continue  # an A/B build of older kernels: only what it exports
                 _bind(handle, name)
             _lib = handle
     return _lib
