@@ -48,6 +48,9 @@ using namespace sl;
 #ifndef SL_L1_KO
 #define SL_L1_KO 0  // timing knockouts of mlp_l1_kernel (1 X loads, 2 X conversion, 3 MFMAs, 4 W1 loads)
 #endif
+#ifndef SL_WG_PIPE
+#define SL_WG_PIPE 1  // software-pipelined wgrad main loop (0: the plain loop)
+#endif
 #ifndef SL_WG_PRIO
 #define SL_WG_PRIO 0  // s_setprio(1) around the wgrad MFMA bursts
 #endif
@@ -863,7 +866,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   }
   auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % 3
     constexpr bool U8 = decltype(u8_c)::value;
-#if SL_WG_KO == 2  // timing knockout: no operand movement (stage 0 only)
+#if SL_WG_KO == 2 || SL_WG_KO == 4  // timing knockout: no operand movement (stage 0 only)
     if (st > 0) return;
 #endif
     uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
@@ -1008,12 +1011,145 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       }
     }
   };
+  // Software-pipelined form: the fragment reads of stage st+1 are issued right
+  // after the barrier that publishes it and run under stage st's MFMAs (two
+  // register sets).  Without it the 8 waves of the workgroup read LDS in
+  // lockstep and then ran their MFMAs: ~1,000 LDS cycles + 1,024 MFMA cycles
+  // per stage back to back (knockout "reads + MFMAs only": 45.7 us).
+  // The slot of stage st is refilled (stage st+3) after the barrier of step st,
+  // when every wave has waited for its own reads of stage st.
+  auto mainloop_pipe = [&](auto u8_c, auto nb_c) {
+    constexpr bool U8 = decltype(u8_c)::value;
+    constexpr int NB = decltype(nb_c)::value;
+    constexpr int NBR = NB > 0 ? NB : 1;
+    constexpr int PPS = U8 ? 5 : 6;
+    constexpr int KB = U8 ? 4096 : 8192;
+    short8_t fa[2][2][4];     // [set][k-step][m-block]
+    short8_t fb[2][2][NBR];   // bf16 B fragments
+    uint2v_t fr[2][2][NBR];   // raw u8 B fragments (converted next to their MFMAs)
+    auto read_stage = [&](int st, auto set_c) {
+      constexpr int S = decltype(set_c)::value;
+      if constexpr (NB > 0) {
+        const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[S][0][i] = wg_tr8<0>(sb + a_addr[i]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (U8) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
+          else fb[S][0][j] = wg_tr8<0>(sb + b_addr[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[S][1][i] = wg_tr8<8192>(sb + a_addr[i]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (U8) fr[S][1][j] = ds_tr8_off<KB>(sb + b_addr[j]);
+          else fb[S][1][j] = wg_tr8<KB>(sb + b_addr[j]);
+        }
+      }
+    };
+    auto mfmas = [&](auto set_c) {
+      constexpr int S = decltype(set_c)::value;
+      if constexpr (NB > 0) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          short8_t b[NBR];
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            if constexpr (U8) b[j] = u8x8_exact_bf16(fr[S][k][j]);
+            else b[j] = fb[S][k][j];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(fa[S][k][i], b[j], acc[i][j]);
+        }
+      }
+    };
+    // one fragment of the next stage (f: A k0 i0..3, B k0, A k1, B k1), for the interleave
+    auto read_frag = [&](uint32_t sb, int f, auto set_c) {
+      constexpr int S = decltype(set_c)::value;
+      const int k = f >> 3, w = f & 7;
+      if (w < 4) {
+        if (k == 0) fa[S][0][w] = wg_tr8<0>(sb + a_addr[w]);
+        else fa[S][1][w] = wg_tr8<8192>(sb + a_addr[w]);
+      } else if (w - 4 < NB) {
+        const int j = w - 4;
+        if constexpr (U8) {
+          if (k == 0) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
+          else fr[S][1][j] = ds_tr8_off<KB>(sb + b_addr[j]);
+        } else {
+          if (k == 0) fb[S][0][j] = wg_tr8<0>(sb + b_addr[j]);
+          else fb[S][1][j] = wg_tr8<KB>(sb + b_addr[j]);
+        }
+      }
+    };
+    // The next stage's 16 fragment reads are interleaved one per two MFMAs: issued
+    // as one burst after the barrier, the 8 waves' reads queued behind each other
+    // and the MFMAs waited for the queue (reads and MFMAs did not overlap).  The
+    // last step reads its own slot again (harmless) rather than branching.
+    auto step = [&](int st, auto cur_c, auto nxt_c) {
+      constexpr int C = decltype(cur_c)::value;
+      if (st + 1 < nst) {
+        wg_vmcnt<PPS>(min(1, nst - 2 - st));  // stage st+1 has landed (stage st+2 may be in flight)
+        __builtin_amdgcn_s_barrier();          // ... for everyone; every wave is done reading stage st
+        if (st + 3 < nst) issue(st + 3, u8_c);  // into stage st's slot
+      }
+      const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % WG_NSLOT) * WG_SLOT * 2);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NB > 0) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          short8_t b[NBR];
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            if constexpr (U8) b[j] = u8x8_exact_bf16(fr[C][k][j]);
+            else b[j] = fb[C][k][j];
+          }
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int i = q >> 2, j = q & 3;
+#if SL_WG_KO != 4  // 4: no DMA and no MFMAs (reads + barriers only)
+            if (j < NB) acc[i][j] = mfma16(fa[C][k][i], b[j], acc[i][j]);
+#endif
+            if (q & 1) {
+              read_frag(sbn, k * 8 + (q >> 1), nxt_c);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    wg_vmcnt<PPS>(min(1, nst - 1));  // stage 0 has landed (stage 1 may be in flight)
+    __builtin_amdgcn_s_barrier();
+    if (2 < nst) issue(2, u8_c);
+    read_stage(0, S0{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    for (int st = 0; st < nst; st += 2) {
+      step(st, S0{}, S1{});
+      if (st + 1 < nst) step(st + 1, S1{}, S0{});
+    }
+  };
   using I4 = std::integral_constant<int, 4>;
   using I1 = std::integral_constant<int, 1>;
   using I0 = std::integral_constant<int, 0>;
 #if SL_WG_KO == 1  // timing knockout: no fragment reads / MFMAs
   if (u8b) mainloop(T_{}, I0{});
   else mainloop(F_{}, I0{});
+#elif SL_WG_KO == 3  // timing knockout: no main loop (prologue sums + epilogue only)
+#elif SL_WG_PIPE
+  if (u8b) {
+    if (nvalid >= 4) mainloop_pipe(T_{}, I4{});
+    else if (nvalid >= 1) mainloop_pipe(T_{}, I1{});
+    else mainloop_pipe(T_{}, I0{});
+  } else {
+    mainloop_pipe(F_{}, I4{});
+  }
 #else
   if (u8b) {
     if (nvalid >= 4) mainloop(T_{}, I4{});
