@@ -71,6 +71,8 @@ constexpr int HS_LD = 264;   // [64][256] bf16 LDS images: 528-B rows
 constexpr int XC_LD = 72;    // X chunk image rows: 64 k + 8 pad = 144 B (ds_read_b128 conflict-free)
 constexpr int DZ_LD = 40;
 constexpr int KS1 = D_INP / 32, KS2 = HID / 32;  // 32-deep k-steps of layer 1 / of 256-wide layers
+// k-steps layer 1 actually runs: 25 (784 = 24.5 x 32; the 26th step of the padded K is all zeros)
+constexpr int L1_KSTEPS_ROWS = (D_IN + 31) / 32;
 
 // Flat parameter layout (torch nn.Linear order): W1 b1 W2 b2 W3 b3.
 constexpr long P_W1 = 0;
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     for (int i = 1; i <= SL_MLP_XQ; ++i) xq[i % SL_MLP_XQ] = i < NCHUNK ? xload(i) : make_uint4(0, 0, 0, 0);
     xstore(0, xload(0));
     __syncthreads();
-    kloop_ring<KS1, NF, RING>(
+    kloop_ring<L1_KSTEPS_ROWS, NF, RING>(
         [&](short8_t (&r)[NF], int st) {
 #pragma unroll
           for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
