@@ -278,7 +278,11 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
 #pragma unroll
       for (int n = 0; n < NF; ++n) acc[m][n] = zero4();
   };
-  // MFMAs of one 32-deep k-step: A fragments from an LDS image, B from the ring
+  // MFMAs of one 32-deep k-step: A fragments from an LDS image, B from the ring.
+  // The operands go in swapped (weights first), so the accumulator is the
+  // TRANSPOSED tile: lane (lg, lr) holds output features 4 lg .. 4 lg + 3 of batch
+  // row lr -- four consecutive bf16 of one image row, written by one ds_write_b64
+  // (with rows in the lane's registers the epilogues needed 64 ds_write_b16 each).
   auto mfma_step = [&](const uint16_t* abase, int ld, const short8_t* b) {
     short8_t af[MF];
 #pragma unroll
@@ -286,33 +290,37 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
 #pragma unroll
     for (int m = 0; m < MF; ++m)
 #pragma unroll
-      for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(af[m], b[n], acc[m][n]);
+      for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(b[n], af[m], acc[m][n]);
   };
   // bias + ReLU epilogue into a [BM][HS_LD] image
   auto relu_out = [&](const float* bias_v, uint16_t* img) {
 #pragma unroll
     for (int n = 0; n < NF; ++n) {
-      const int col = cw + n * 16 + lr;
-      const float bias = bias_v[col];
+      const int col = cw + n * 16 + 4 * lg;
+      const float4 bias = *reinterpret_cast<const float4*>(bias_v + col);
 #pragma unroll
-      for (int m = 0; m < MF; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          img[(rw + m * 16 + 4 * lg + r) * HS_LD + col] = f2bf(fmaxf(acc[m][n][r] + bias, 0.f));
+      for (int m = 0; m < MF; ++m) {
+        uint2 v;
+        v.x = pack2(fmaxf(acc[m][n][0] + bias.x, 0.f), fmaxf(acc[m][n][1] + bias.y, 0.f));
+        v.y = pack2(fmaxf(acc[m][n][2] + bias.z, 0.f), fmaxf(acc[m][n][3] + bias.w, 0.f));
+        *reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col) = v;
+      }
     }
   };
   // in place: img holds the forward activation H (>= 0); write acc * 1[H > 0]
   auto masked_out = [&](uint16_t* img) {
 #pragma unroll
     for (int n = 0; n < NF; ++n) {
-      const int col = cw + n * 16 + lr;
+      const int col = cw + n * 16 + 4 * lg;
 #pragma unroll
-      for (int m = 0; m < MF; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          uint16_t* e = img + (rw + m * 16 + 4 * lg + r) * HS_LD + col;
-          *e = f2bf(*e != 0 ? acc[m][n][r] : 0.f);
-        }
+      for (int m = 0; m < MF; ++m) {
+        uint2* e = reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col);
+        const uint2 h = *e;
+        uint2 v;
+        v.x = pack2((h.x & 0xffffu) ? acc[m][n][0] : 0.f, (h.x >> 16) ? acc[m][n][1] : 0.f);
+        v.y = pack2((h.y & 0xffffu) ? acc[m][n][2] : 0.f, (h.y >> 16) ? acc[m][n][3] : 0.f);
+        *e = v;
+      }
     }
   };
 
