@@ -42,6 +42,9 @@ using namespace sl;
 #ifndef SL_MLP_RING2
 #define SL_MLP_RING2 4
 #endif
+#ifndef SL_ROWS128_WMG
+#define SL_ROWS128_WMG 2  // row groups of the 128-row rows-kernel tile (1: each wave 128 rows x 32 features)
+#endif
 #ifndef SL_MLP_SLICES
 #define SL_MLP_SLICES 28  // weight-gradient K slices: 9 tiles x 28 = 252 GEMM workgroups
 #endif
@@ -441,8 +444,10 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   // ---- [dW3 | db3] partial over this wave's 64 rows: dZ^T (RZ) . H2 (R0), both read
   // transposed (ds_read_b64_tr_b16).  The weight-gradient kernel would otherwise need
   // H2 and dZ in HBM (a [batch][256] write here + a re-read there) and spend 2 of its
-  // 20 tiles on a 10-row GEMM.  mlp_sgd_kernel sums the partials in a fixed order. ----
-  {
+  // 20 tiles on a 10-row GEMM.  The wgrad kernel sums the partials in a fixed order. ----
+#pragma unroll
+  for (int hr = 0; hr < MF / 4; ++hr) {  // one partial row per 64 of this wave's rows
+    const int rh = rw + 64 * hr;
     floatx4_t d3[NF], db3 = zero4();
 #pragma unroll
     for (int n = 0; n < NF; ++n) d3[n] = zero4();
@@ -451,13 +456,13 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int k0 = rw + 32 * ks;
+      const int k0 = rh + 32 * ks;
       const short8_t af = lds_tr8(RZ + k0 * DZ_LD, DZ_LD, lane);  // A[c][row] = dZ[row][c]
 #pragma unroll
       for (int n = 0; n < NF; ++n) d3[n] = mfma16(af, lds_tr8(R0 + k0 * HS_LD + cw + n * 16, HS_LD, lane), d3[n]);
       if (wng == 0) db3 = mfma16(af, ones, db3);
     }
-    float* part = a.w3p + (long)((row0 + rw) >> 6) * W3P_LD;
+    float* part = a.w3p + (long)((row0 + rh) >> 6) * W3P_LD;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int c = 4 * lg + r;
@@ -486,18 +491,22 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     short8_t ones;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
-    floatx4_t cs[NF];
 #pragma unroll
-    for (int n = 0; n < NF; ++n) cs[n] = zero4();
+    for (int hr = 0; hr < MF / 4; ++hr) {
+      const int rh = rw + 64 * hr;
+      floatx4_t cs[NF];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int n = 0; n < NF; ++n) cs[n] = zero4();
 #pragma unroll
-      for (int n = 0; n < NF; ++n)
-        cs[n] = mfma16(ones, lds_tr8(img + (rw + 32 * ks) * HS_LD + cw + n * 16, HS_LD, lane), cs[n]);
-    if (lg == 0) {
-      float* part = a.w3p + (long)((row0 + rw) >> 6) * W3P_LD + off;
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int n = 0; n < NF; ++n) part[cw + n * 16 + lr] = cs[n][0];
+        for (int n = 0; n < NF; ++n)
+          cs[n] = mfma16(ones, lds_tr8(img + (rh + 32 * ks) * HS_LD + cw + n * 16, HS_LD, lane), cs[n]);
+      if (lg == 0) {
+        float* part = a.w3p + (long)((row0 + rh) >> 6) * W3P_LD + off;
+#pragma unroll
+        for (int n = 0; n < NF; ++n) part[cw + n * 16 + lr] = cs[n][0];
+      }
     }
   };
   col_sums(R0, W3P_DB2);
@@ -1352,9 +1361,9 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_l1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);
   if (bm == 128) {
-    if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 2, false>), dim3(batch / 128), dim3(512), 0, stream, a);
-    else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 2>), dim3(batch / 128), dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, 2>), dim3(batch / 128), dim3(512), 0, stream, a);
+    if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, SL_ROWS128_WMG, false>), dim3(batch / 128), dim3(512), 0, stream, a);
+    else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, SL_ROWS128_WMG>), dim3(batch / 128), dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, SL_ROWS128_WMG>), dim3(batch / 128), dim3(512), 0, stream, a);
   } else {
     if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1, false>), dim3(batch / 64), dim3(256), 0, stream, a);
     else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
