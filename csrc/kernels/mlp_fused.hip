@@ -756,8 +756,6 @@ struct WgArgs {
 constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages in flight
 constexpr int WG_IMG = 64 * 128;          // one [64 k][128] bf16 image, unpadded (swizzled)
 constexpr int WG_SLOT = 3 * WG_IMG;       // A half 0, A half 1, B = 48 KB
-constexpr int WG_OUT_LD = 128 + 4;        // fp32 epilogue tile
-static_assert(256 * WG_OUT_LD * 4 <= WG_NSLOT * WG_SLOT * 2, "epilogue tile must fit the ring");
 
 // 16-B chunk position inside a 256-B image row.  XOR on chunk-pair bits with
 // f(r) = (r & 3) | ((r >> 3) & 1) << 2 makes every ds_read_b64_tr_b16 of the
@@ -1011,7 +1009,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
+          for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(b0[j], a0[i], acc[i][j]);
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
@@ -1022,7 +1020,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+          for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
 #if SL_WG_PRIO
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(0);
@@ -1080,7 +1078,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(fa[S][k][i], b[j], acc[i][j]);
+            for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(b[j], fa[S][k][i], acc[i][j]);
         }
       }
     };
@@ -1128,7 +1126,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
           for (int q = 0; q < 16; ++q) {
             const int i = q >> 2, j = q & 3;
 #if SL_WG_KO != 4  // 4: no DMA and no MFMAs (reads + barriers only)
-            if (j < NB) acc[i][j] = mfma16(fa[C][k][i], b[j], acc[i][j]);
+            if (j < NB) acc[i][j] = mfma16(b[j], fa[C][k][i], acc[i][j]);
 #endif
             if (q & 1) {
               read_frag(sbn, k * 8 + (q >> 1), nxt_c);
@@ -1179,25 +1177,19 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   }
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  // ---- epilogue: the fp32 tile through LDS, then float4 rows into slab slice s ----
-  float* Os = reinterpret_cast<float*>(smem);
+  // ---- epilogue: the MFMAs took their operands swapped (B first), so each lane holds
+  // 4 consecutive n of one m row: float4 stores straight from registers into slab slice
+  // s (no LDS staging, no barriers) ----
+  float* out = A.slab + (long)s * A.slab_stride + P.w_off;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Os[(wm * 64 + i * 16 + 4 * lg + r) * WG_OUT_LD + wn * 64 + j * 16 + lr] = acc[i][j][r];
-  __syncthreads();
-  float* out = A.slab + (long)s * A.slab_stride + P.w_off;
-  for (int q = tid; q < 256 * 32; q += WG_NT) {
-    const int rl = q >> 5, c4 = (q & 31) * 4;
-    const int n = n0 + c4;
-    if (n < P.n_real)
-      *reinterpret_cast<float4*>(out + (long)rl * P.n_real + n) = *reinterpret_cast<const float4*>(Os + rl * WG_OUT_LD + c4);
-  }
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * lg;
+      if (n < P.n_real)
+        *reinterpret_cast<floatx4_t*>(out + (long)(wm * 64 + i * 16 + lr) * P.n_real + n) = acc[i][j];
+    }
 }
 
 // ---------------------------------------------------------------------------
