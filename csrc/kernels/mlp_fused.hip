@@ -60,6 +60,9 @@ using namespace sl;
 #ifndef SL_WG_KO
 #define SL_WG_KO 0  // timing knockouts of mlp_wgrad_kernel (1 no MFMAs, 2 no LDS-DMA after stage 0)
 #endif
+#ifndef SL_MLP_APF
+#define SL_MLP_APF 1  // rows kernel: prefetch the next k-step's A fragments (3-slot X ring)
+#endif
 #ifndef SL_MLP_XQ
 #define SL_MLP_XQ 4  // X prefetch distance in 64-column chunks (4 measured +1% over 2)
 #endif
@@ -157,6 +160,30 @@ __device__ __forceinline__ void kloop_ring(LoadB&& loadb, Step&& step, After&& a
   }
 }
 
+// kloop_ring with the A fragments (LDS) of step s+1 read during step s: issued
+// right before the step's MFMAs, their latency hides under them instead of
+// stalling every k-step (the sched_barriers that pin the weight ring kept the
+// compiler from hoisting them).  loada(af, s) reads step s's MF fragments;
+// mfma(af, b) runs the step.
+template <int NSTEPS, int NF, int MF, int D, class LoadB, class LoadA, class Mfma, class After>
+__device__ __forceinline__ void kloop_ring_a(LoadB&& loadb, LoadA&& loada, Mfma&& mfma, After&& after) {
+  short8_t r[D][NF];
+  short8_t af[2][MF];
+#pragma unroll
+  for (int i = 0; i < D && i < NSTEPS; ++i) loadb(r[i], i);
+  loada(af[0], 0);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < NSTEPS; ++s) {
+    if (s + 1 < NSTEPS) loada(af[(s + 1) & 1], s + 1);
+    mfma(af[s & 1], r[s % D]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + D < NSTEPS) loadb(r[s % D], s + D);
+    __builtin_amdgcn_sched_barrier(0);
+    after(s);
+  }
+}
+
 __device__ __forceinline__ long batch_base(const int* cursor, int n_batches, int batch) {
   const long b = cursor ? (long)(*cursor % n_batches) : 0;
   return b * batch;
@@ -229,7 +256,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   constexpr int NF = 16 * WMG / NWV; // n-fragments per wave
   constexpr int RING = NF >= 4 ? SL_MLP_RING4 : SL_MLP_RING2;  // weight ring depth (k-steps)
   constexpr int REGB = BM * HS_LD;   // one LDS region (elements)
-  static_assert(2 * BM * XC_LD <= REGB, "X ring must fit region 0");
+  static_assert(3 * BM * XC_LD <= REGB, "X ring must fit region 0");
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * REGB + BM * DZ_LD];
   uint16_t* R0 = smem;             // X ring -> H2 image -> dH2 image
   uint16_t* R1 = smem + REGB;      // H1 image -> dH1 image
@@ -266,7 +293,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     return (c * 64 + xcol < D_IN) ? *reinterpret_cast<const uint4*>(xg + c * 64) : make_uint4(0, 0, 0, 0);
   };
   auto xstore = [&](int c, uint4 v) {
-    uint16_t* d = R0 + (c & 1) * BM * XC_LD + xrow * XC_LD + xcol;
+    uint16_t* d = R0 + (SL_MLP_APF ? c % 3 : c & 1) * BM * XC_LD + xrow * XC_LD + xcol;
     short8_t lo = zero8(), hi = zero8();
     if (c * 64 + xcol < D_IN) {
       lo = u8x8_to_bf16(make_uint2(v.x, v.y), nxa, nxb);
@@ -290,6 +317,12 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     short8_t af[MF];
 #pragma unroll
     for (int m = 0; m < MF; ++m) af[m] = lds8(abase + (rw + m * 16) * ld);
+#pragma unroll
+    for (int m = 0; m < MF; ++m)
+#pragma unroll
+      for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(b[n], af[m], acc[m][n]);
+  };
+  auto mfma_ab = [&](const short8_t (&af)[MF], const short8_t (&b)[NF]) {
 #pragma unroll
     for (int m = 0; m < MF; ++m)
 #pragma unroll
@@ -353,6 +386,31 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
     for (int i = 1; i <= SL_MLP_XQ; ++i) xq[i % SL_MLP_XQ] = i < NCHUNK ? xload(i) : make_uint4(0, 0, 0, 0);
     xstore(0, xload(0));
     __syncthreads();
+#if SL_MLP_APF
+    // 3-slot X ring: chunk c+1 is converted after the first k-step of chunk c and
+    // published by the barrier right after it, so step 2c+1 can prefetch step
+    // 2c+2's fragments; its slot last held chunk c-2, read before the barrier of
+    // step 2c-2
+    kloop_ring_a<L1_KSTEPS_ROWS, NF, MF, RING>(
+        [&](short8_t (&r)[NF], int st) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
+        },
+        [&](short8_t (&af)[MF], int st) {
+          const uint16_t* ab = R0 + ((st >> 1) % 3) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg;
+#pragma unroll
+          for (int m = 0; m < MF; ++m) af[m] = lds8(ab + (rw + m * 16) * XC_LD);
+        },
+        mfma_ab,
+        [&](int st) {
+          const int c = st >> 1;
+          if (!(st & 1)) {
+            if (c + 1 < NCHUNK) xstore(c + 1, xq[(c + 1) % SL_MLP_XQ]);
+            if (c + 1 + SL_MLP_XQ < NCHUNK) xq[(c + 1) % SL_MLP_XQ] = xload(c + 1 + SL_MLP_XQ);
+            __syncthreads();
+          }
+        });
+#else
     kloop_ring<L1_KSTEPS_ROWS, NF, RING>(
         [&](short8_t (&r)[NF], int st) {
 #pragma unroll
@@ -373,6 +431,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
             __syncthreads();
           }
         });
+#endif
   }
   stamp(1);
   relu_out(a.b1, R1);
@@ -384,12 +443,25 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   zero_acc();
   {
     const uint16_t* ha = R1 + lr * HS_LD + 8 * lg;
+#if SL_MLP_APF
+    kloop_ring_a<KS2, NF, MF, RING>(
+        [&](short8_t (&r)[NF], int st) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) r[n] = f_w2(n, st, KS2);
+        },
+        [&](short8_t (&af)[MF], int st) {
+#pragma unroll
+          for (int m = 0; m < MF; ++m) af[m] = lds8(ha + st * 32 + (rw + m * 16) * HS_LD);
+        },
+        mfma_ab,
+#else
     kloop_ring<KS2, NF, RING>(
         [&](short8_t (&r)[NF], int st) {
 #pragma unroll
           for (int n = 0; n < NF; ++n) r[n] = f_w2(n, st, KS2);
         },
         [&](int st, short8_t (&b)[NF]) { mfma_step(ha + st * 32, HS_LD, b); },
+#endif
         [&](int st) {
           if (TRAIN && L1) copy_part<BM, NT, HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid, st);
         });
@@ -515,12 +587,25 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   zero_acc();
   {
     const uint16_t* ha = R0 + lr * HS_LD + 8 * lg;
+#if SL_MLP_APF
+    kloop_ring_a<KS2, NF, MF, RING>(
+        [&](short8_t (&r)[NF], int st) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) r[n] = f_w2t(n, st, KS2);
+        },
+        [&](short8_t (&af)[MF], int st) {
+#pragma unroll
+          for (int m = 0; m < MF; ++m) af[m] = lds8(ha + st * 32 + (rw + m * 16) * HS_LD);
+        },
+        mfma_ab,
+#else
     kloop_ring<KS2, NF, RING>(
         [&](short8_t (&r)[NF], int st) {
 #pragma unroll
           for (int n = 0; n < NF; ++n) r[n] = f_w2t(n, st, KS2);
         },
         [&](int st, short8_t (&b)[NF]) { mfma_step(ha + st * 32, HS_LD, b); },
+#endif
         [&](int st) { copy_part<BM, NT, HID>(R0, HS_LD, a.dh2 + (long)row0 * HID, HID, tid, st); });
   }
   stamp(8);
