@@ -60,6 +60,12 @@ using namespace sl;
 #ifndef SL_WG_KO
 #define SL_WG_KO 0  // timing knockouts of mlp_wgrad_kernel (1 no MFMAs, 2 no LDS-DMA after stage 0)
 #endif
+#ifndef SL_MLP_ONEIMG
+#define SL_MLP_ONEIMG 0  // rows kernel: one activation image (3 workgroups per CU)
+#endif
+#ifndef SL_MLP_RING_ONE
+#define SL_MLP_RING_ONE 3  // weight ring depth of the one-image kernel (register budget 168)
+#endif
 #ifndef SL_MLP_APF
 #define SL_MLP_APF 1  // rows kernel: prefetch the next k-step's A fragments (3-slot X ring)
 #endif
@@ -248,19 +254,26 @@ __device__ __forceinline__ void copy_part(const uint16_t* src, int ld, uint16_t*
 // LDS A-fragment traffic of the 1 x 8 layout at BM = 128.
 // L1 = false: H1 was already computed by mlp_l1_kernel (train path); the tile is
 // staged from global into R1 and layer 1 / its H1 write are skipped.
+// ONE (SL_MLP_ONEIMG, 64-row tiles): a single activation image instead of two --
+// H2 overwrites H1 after layer 2 (the H1 ReLU mask survives as 4-bit bytes) and
+// dH1 overwrites dH2 -- so the LDS footprint drops from 72.7 KB to 42.8 KB and
+// three workgroups fit on a CU.
 template <bool TRAIN, int BM, int WMG, bool L1 = true>
-__global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpRowArgs a) {
+__global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) void mlp_rows_kernel(MlpRowArgs a) {
   constexpr int NWV = BM / 16;       // waves per workgroup
   constexpr int MF = BM / 16 / WMG;  // m-fragments per wave
   constexpr int NT = BM * 4;         // threads
   constexpr int NF = 16 * WMG / NWV; // n-fragments per wave
-  constexpr int RING = NF >= 4 ? SL_MLP_RING4 : SL_MLP_RING2;  // weight ring depth (k-steps)
+  constexpr bool ONE = SL_MLP_ONEIMG && BM == 64 && L1;
+  constexpr int RING = ONE ? SL_MLP_RING_ONE : (NF >= 4 ? SL_MLP_RING4 : SL_MLP_RING2);  // weight ring depth (k-steps)
   constexpr int REGB = BM * HS_LD;   // one LDS region (elements)
   static_assert(3 * BM * XC_LD <= REGB, "X ring must fit region 0");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * REGB + BM * DZ_LD];
-  uint16_t* R0 = smem;             // X ring -> H2 image -> dH2 image
-  uint16_t* R1 = smem + REGB;      // H1 image -> dH1 image
-  uint16_t* RZ = smem + 2 * REGB;  // dZ image
+  constexpr int SMEM = ONE ? REGB + BM * DZ_LD + BM * 32 : 2 * REGB + BM * DZ_LD;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
+  uint16_t* R0 = smem;                          // X ring -> H2 image -> dH2 image
+  uint16_t* R1 = ONE ? smem : smem + REGB;      // H1 image -> dH1 image
+  uint16_t* RZ = smem + (ONE ? REGB : 2 * REGB);  // dZ image
+  uint8_t* M1 = reinterpret_cast<uint8_t*>(smem + REGB + BM * DZ_LD);  // ONE: [BM][64] H1 mask nibbles
   // ReLU masks are NOT kept in registers: H1/H2 stay in LDS until the masked
   // backward products overwrite them in place (hipcc held 64 compare masks per
   // layer in SGPR pairs and spilled ~200 SGPRs).
@@ -328,8 +341,8 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
 #pragma unroll
       for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(b[n], af[m], acc[m][n]);
   };
-  // bias + ReLU epilogue into a [BM][HS_LD] image
-  auto relu_out = [&](const float* bias_v, uint16_t* img) {
+  // bias + ReLU epilogue into a [BM][HS_LD] image (+ the nibble mask of H > 0)
+  auto relu_out = [&](const float* bias_v, uint16_t* img, bool with_mask) {
 #pragma unroll
     for (int n = 0; n < NF; ++n) {
       const int col = cw + n * 16 + 4 * lg;
@@ -339,6 +352,25 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
         uint2 v;
         v.x = pack2(fmaxf(acc[m][n][0] + bias.x, 0.f), fmaxf(acc[m][n][1] + bias.y, 0.f));
         v.y = pack2(fmaxf(acc[m][n][2] + bias.z, 0.f), fmaxf(acc[m][n][3] + bias.w, 0.f));
+        *reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col) = v;
+        if (ONE && with_mask)
+          M1[(rw + m * 16 + lr) * 64 + (col >> 2)] =
+              (uint8_t)(((v.x & 0xffffu) != 0) | (((v.x >> 16) != 0) << 1) | (((v.y & 0xffffu) != 0) << 2) |
+                        (((v.y >> 16) != 0) << 3));
+      }
+    }
+  };
+  // ONE: write acc * 1[H1 > 0] from the nibble mask
+  auto masked_bits_out = [&](uint16_t* img) {
+#pragma unroll
+    for (int n = 0; n < NF; ++n) {
+      const int col = cw + n * 16 + 4 * lg;
+#pragma unroll
+      for (int m = 0; m < MF; ++m) {
+        const uint32_t b = M1[(rw + m * 16 + lr) * 64 + (col >> 2)];
+        uint2 v;
+        v.x = pack2((b & 1u) ? acc[m][n][0] : 0.f, (b & 2u) ? acc[m][n][1] : 0.f);
+        v.y = pack2((b & 4u) ? acc[m][n][2] : 0.f, (b & 8u) ? acc[m][n][3] : 0.f);
         *reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col) = v;
       }
     }
@@ -434,7 +466,8 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
 #endif
   }
   stamp(1);
-  relu_out(a.b1, R1);
+  if constexpr (ONE) __syncthreads();  // the X ring shares the image H1 goes to
+  relu_out(a.b1, R1, true);
   }
   __syncthreads();
   stamp(2);
@@ -468,9 +501,16 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
   }
   stamp(3);
   short8_t w3f[KS2];  // layer-3 weights, prefetched under the ReLU-2 epilogue
+  if constexpr (!ONE) {
 #pragma unroll
-  for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
-  relu_out(a.b2, R0);
+    for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
+  }
+  if constexpr (ONE) __syncthreads();  // every wave is done reading H1: H2 replaces it
+  relu_out(a.b2, R0, false);
+  if constexpr (ONE) {  // after the epilogue: the 32 registers would push past the 168 budget
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
+  }
   __syncthreads();
   stamp(4);
 
@@ -609,7 +649,12 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpR
         [&](int st) { copy_part<BM, NT, HID>(R0, HS_LD, a.dh2 + (long)row0 * HID, HID, tid, st); });
   }
   stamp(8);
-  masked_out(R1);
+  if constexpr (ONE) {
+    __syncthreads();  // every wave is done reading dH2: dH1 replaces it
+    masked_bits_out(R1);
+  } else {
+    masked_out(R1);
+  }
   __syncthreads();
   copy_out<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid);
   col_sums(R1, W3P_DB1);
