@@ -51,6 +51,12 @@ using namespace sl;
 #ifndef SL_L1_KO
 #define SL_L1_KO 0  // timing knockouts of mlp_l1_kernel (1 X loads, 2 X conversion, 3 MFMAs, 4 W1 loads)
 #endif
+#ifndef SL_WG_W128
+#define SL_WG_W128 1  // wgrad waves cover 128 m x 32 n (2 x 4 waves; half the u8 conversions) instead of 64 x 64
+#endif
+#ifndef SL_WG_CVT
+#define SL_WG_CVT 1  // wgrad u8 B-fragment conversions scheduled under the MFMAs of the previous k-step
+#endif
 #ifndef SL_WG_PIPE
 #define SL_WG_PIPE 1  // software-pipelined wgrad main loop (0: the plain loop)
 #endif
@@ -969,12 +975,18 @@ __device__ __forceinline__ void wg_vmcnt(int younger) {
 }
 
 constexpr int WG_NT = 512;
+constexpr int WG_MI = SL_WG_W128 ? 8 : 4;  // 16-row A (dZ) fragments per wave
+constexpr int WG_NJ = SL_WG_W128 ? 2 : 4;  // 16-column B fragments per wave
+constexpr int WG_NF = WG_MI + WG_NJ;       // fragments per wave per k-step
+#if SL_WG_W128 && !SL_WG_PIPE
+#error "SL_WG_W128 needs the pipelined main loop"
+#endif
 
 __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_NSLOT * WG_SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
-  const int wm = wave & 3, wn = wave >> 2;
+  const int wm = SL_WG_W128 ? (wave & 1) : (wave & 3), wn = SL_WG_W128 ? (wave >> 1) : (wave >> 2);
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int s = logical / A.total_tiles;
@@ -987,7 +999,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int nst = min(A.steps_per_slice, A.total_steps - st0);
   const bool u8b = pi == 0;
   // n-blocks of this wave that hold real columns (dW1's last tile: 16 columns)
-  const int nvalid = __builtin_amdgcn_readfirstlane(min(4, max(0, (P.n_real - n0 - wn * 64 + 15) / 16)));
+  const int nvalid = __builtin_amdgcn_readfirstlane(min(WG_NJ, max(0, (P.n_real - n0 - wn * 16 * WG_NJ + 15) / 16)));
 
   // LDS-DMA map: bf16 [64][128] images -- wave w, piece j (0..1) covers rows 4 (2w + j) .. +3,
   // lane -> row 4 (2w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row);
@@ -1082,20 +1094,25 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     }
   }
 
-  floatx4_t acc[4][4];
+  floatx4_t acc[WG_MI][WG_NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+    for (int j = 0; j < WG_NJ; ++j) acc[i][j] = zero4();
 
   // per-lane tr-read byte addresses within a slot; k-step 1 is a constant offset
   const uint32_t lds_base = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
-  uint32_t a_addr[4], b_addr[4];
+  uint32_t a_addr[WG_MI], b_addr[WG_NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) a_addr[i] = (wm >> 1) * WG_IMG * 2 + wg_tr_addr((wm & 1) * 64 + i * 16, lane);
+  for (int i = 0; i < WG_MI; ++i) {
+    const int r = wm * 16 * WG_MI + i * 16;  // A row (m) 0..255: image r / 128
+    a_addr[i] = (r >> 7) * WG_IMG * 2 + wg_tr_addr(r & 127, lane);
+  }
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    b_addr[j] = 2 * WG_IMG * 2 + (u8b ? wg_tr8_addr(wn * 64 + j * 16, lane) : wg_tr_addr(wn * 64 + j * 16, lane));
+  for (int j = 0; j < WG_NJ; ++j) {
+    const int c = wn * 16 * WG_NJ + j * 16;
+    b_addr[j] = 2 * WG_IMG * 2 + (u8b ? wg_tr8_addr(c, lane) : wg_tr_addr(c, lane));
+  }
 
   // Instantiated per (u8, live n-blocks) and selected by a scalar branch OUTSIDE
   // the loop (conditions inside made hipcc copy every accumulator AGPR<->VGPR).
@@ -1171,22 +1188,25 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     constexpr int NBR = NB > 0 ? NB : 1;
     constexpr int PPS = U8 ? 5 : 6;
     constexpr int KB = U8 ? 4096 : 8192;
-    short8_t fa[2][2][4];     // [set][k-step][m-block]
+    short8_t fa[2][2][WG_MI]; // [set][k-step][m-block]
     short8_t fb[2][2][NBR];   // bf16 B fragments
     uint2v_t fr[2][2][NBR];   // raw u8 B fragments (converted next to their MFMAs)
+#if SL_WG_CVT
+    short8_t fc[2][2][NBR];   // converted u8 B fragments (SL_WG_CVT schedule)
+#endif
     auto read_stage = [&](int st, auto set_c) {
       constexpr int S = decltype(set_c)::value;
       if constexpr (NB > 0) {
         const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[S][0][i] = wg_tr8<0>(sb + a_addr[i]);
+        for (int i = 0; i < WG_MI; ++i) fa[S][0][i] = wg_tr8<0>(sb + a_addr[i]);
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           if constexpr (U8) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
           else fb[S][0][j] = wg_tr8<0>(sb + b_addr[j]);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[S][1][i] = wg_tr8<8192>(sb + a_addr[i]);
+        for (int i = 0; i < WG_MI; ++i) fa[S][1][i] = wg_tr8<8192>(sb + a_addr[i]);
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           if constexpr (U8) fr[S][1][j] = ds_tr8_off<KB>(sb + b_addr[j]);
@@ -1206,21 +1226,21 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
             else b[j] = fb[S][k][j];
           }
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
             for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(b[j], fa[S][k][i], acc[i][j]);
         }
       }
     };
-    // one fragment of the next stage (f: A k0 i0..3, B k0, A k1, B k1), for the interleave
+    // one fragment of the next stage (f: A k0 i0..MI-1, B k0, A k1, B k1), for the interleave
     auto read_frag = [&](uint32_t sb, int f, auto set_c) {
       constexpr int S = decltype(set_c)::value;
-      const int k = f >> 3, w = f & 7;
-      if (w < 4) {
+      const int k = f / WG_NF, w = f % WG_NF;
+      if (w < WG_MI) {
         if (k == 0) fa[S][0][w] = wg_tr8<0>(sb + a_addr[w]);
         else fa[S][1][w] = wg_tr8<8192>(sb + a_addr[w]);
-      } else if (w - 4 < NB) {
-        const int j = w - 4;
+      } else if (w - WG_MI < NB) {
+        const int j = w - WG_MI;
         if constexpr (U8) {
           if (k == 0) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
           else fr[S][1][j] = ds_tr8_off<KB>(sb + b_addr[j]);
@@ -1230,7 +1250,16 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
         }
       }
     };
-    // The next stage's 16 fragment reads are interleaved one per two MFMAs: issued
+    // the k-step's NF fragment reads of the next stage, spread over its 16 MFMAs
+    auto reads_after = [&](uint32_t sb, int k, int q, auto set_c) {
+      const int f0 = k * WG_NF + q * WG_NF / 16, f1 = k * WG_NF + (q + 1) * WG_NF / 16;
+      if (f1 > f0) {
+#pragma unroll
+        for (int f = f0; f < f1; ++f) read_frag(sb, f, set_c);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // The next stage's fragment reads are interleaved one per ~two MFMAs: issued
     // as one burst after the barrier, the 8 waves' reads queued behind each other
     // and the MFMAs waited for the queue (reads and MFMAs did not overlap).  The
     // last step reads its own slot again (harmless) rather than branching.
@@ -1243,25 +1272,62 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       }
       const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % WG_NSLOT) * WG_SLOT * 2);
       __builtin_amdgcn_sched_barrier(0);
+#if SL_WG_CVT
+      if constexpr (U8 && NB > 0) {
+        // u8 -> bf16 conversions off the MFMA critical path: k-step 1's fragments
+        // (landed at the end of the previous step) are converted under k-step 0's
+        // MFMAs, the next stage's k-step-0 fragments under k-step 1's second half.
+        // MFMAs run j-major, so fragment j is needed only from MFMA 4j on.
+        constexpr int N = 1 - C;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int j = q / WG_MI, i = q % WG_MI;
+            if (j < NB) acc[i][j] = mfma16(fc[C][k][j], fa[C][k][i], acc[i][j]);
+            if (k == 0 && q % WG_MI == 1 && j < NB) {
+              fc[C][1][j] = u8x8_exact_bf16(fr[C][1][j]);
+              asm volatile("" : "+v"(fc[C][1][j]));
+            }
+            if (k == 1 && q == 8) {
+              // everything but k-step 1's first A fragments (2 LDS ops each) has landed
+              __builtin_amdgcn_sched_barrier(0);
+              asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * (8 * WG_NF / 16)) : "memory");
+              __builtin_amdgcn_sched_barrier(0);
+            }
+            if (k == 1 && q >= 8 && (q & 1) == 0 && ((q - 8) >> 1) < NB) {
+              short8_t& d = fc[N][0][(q - 8) >> 1];
+              d = u8x8_exact_bf16(fr[N][0][(q - 8) >> 1]);
+              asm volatile("" : "+v"(d));  // keep it here (LLVM sinks it past the back edge otherwise)
+            }
+            reads_after(sbn, k, q, nxt_c);
+          }
+        }
+      } else
+#endif
       if constexpr (NB > 0) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           short8_t b[NBR];
 #pragma unroll
           for (int j = 0; j < NB; ++j) {
+#if SL_WG_KO == 5  // timing knockout: no u8 -> bf16 conversion (wrong numerics)
+            if constexpr (U8) {
+              typedef uint32_t u32x4k __attribute__((ext_vector_type(4)));
+              b[j] = __builtin_bit_cast(short8_t, u32x4k{fr[C][k][j][0], fr[C][k][j][1], fr[C][k][j][0], fr[C][k][j][1]});
+            }
+#else
             if constexpr (U8) b[j] = u8x8_exact_bf16(fr[C][k][j]);
+#endif
             else b[j] = fb[C][k][j];
           }
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
-            const int i = q >> 2, j = q & 3;
+            const int i = q / WG_NJ, j = q % WG_NJ;
 #if SL_WG_KO != 4  // 4: no DMA and no MFMAs (reads + barriers only)
             if (j < NB) acc[i][j] = mfma16(b[j], fa[C][k][i], acc[i][j]);
 #endif
-            if (q & 1) {
-              read_frag(sbn, k * 8 + (q >> 1), nxt_c);
-              __builtin_amdgcn_sched_barrier(0);
-            }
+            reads_after(sbn, k, q, nxt_c);
           }
         }
       }
@@ -1277,12 +1343,18 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     read_stage(0, S0{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#if SL_WG_CVT
+    if constexpr (U8) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) fc[0][0][j] = u8x8_exact_bf16(fr[0][0][j]);
+    }
+#endif
     for (int st = 0; st < nst; st += 2) {
       step(st, S0{}, S1{});
       if (st + 1 < nst) step(st + 1, S1{}, S0{});
     }
   };
-  using I4 = std::integral_constant<int, 4>;
+  using I4 = std::integral_constant<int, WG_NJ>;  // all n-blocks live
   using I1 = std::integral_constant<int, 1>;
   using I0 = std::integral_constant<int, 0>;
 #if SL_WG_KO == 1  // timing knockout: no fragment reads / MFMAs
@@ -1291,7 +1363,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #elif SL_WG_KO == 3  // timing knockout: no main loop (prologue sums + epilogue only)
 #elif SL_WG_PIPE
   if (u8b) {
-    if (nvalid >= 4) mainloop_pipe(T_{}, I4{});
+    if (nvalid >= WG_NJ) mainloop_pipe(T_{}, I4{});
     else if (nvalid >= 1) mainloop_pipe(T_{}, I1{});
     else mainloop_pipe(T_{}, I0{});
   } else {
@@ -1313,12 +1385,12 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // s (no LDS staging, no barriers) ----
   float* out = A.slab + (long)s * A.slab_stride + P.w_off;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * lg;
+    for (int j = 0; j < WG_NJ; ++j) {
+      const int n = n0 + wn * 16 * WG_NJ + j * 16 + 4 * lg;
       if (n < P.n_real)
-        *reinterpret_cast<floatx4_t*>(out + (long)(wm * 64 + i * 16 + lr) * P.n_real + n) = acc[i][j];
+        *reinterpret_cast<floatx4_t*>(out + (long)(wm * 16 * WG_MI + i * 16 + lr) * P.n_real + n) = acc[i][j];
     }
 }
 
