@@ -1438,13 +1438,14 @@ __device__ __forceinline__ float quad_sum(float v) {
   return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
 }
 
-__device__ __forceinline__ void sgd_apply(const SgdArgs& a, long p, float gme) {
+// w0 / m0: the parameter and momentum, loaded by the caller ahead of the slab sums
+__device__ __forceinline__ void sgd_apply(const SgdArgs& a, long p, float gme, float w0, float m0) {
   if (a.grad_out) a.grad_out[p] = gme;
   if (a.mode == 1) return;
-  float w = a.w[p];
+  float w = w0;
   float d = gme + a.wd * w;
   if (a.mom) {
-    d = a.mu * a.mom[p] + d;
+    d = a.mu * m0 + d;
     a.mom[p] = d;
   }
   w -= a.lr * d;
@@ -1479,22 +1480,42 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
     return;
   }
   const bool full = p0 + 4 <= a.n;
+  // the update's own operands, in flight together with the slab loads
+  const bool upd = mine && a.mode != 1;
+  const float w0 = upd ? a.w[p] : 0.f;
+  const float m0 = upd && a.mom ? a.mom[p] : 0.f;
   float g[4] = {0.f, 0.f, 0.f, 0.f};
   float gme;
   if (a.slab) {
     if (full) {
+      // All of a thread's slab loads (and dW1's db1 loads) are issued before the first
+      // wait: the plain loop waited vmcnt(0) per slice, two chains of 7 dependent
+      // ~1 us loads (12.4 us per call).
       const float* src = a.slab + p0;
-      for (int sidx = part; sidx < a.slices; sidx += SGD_TPG) {
-        const float4 v = *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride);
-        g[0] += v.x; g[1] += v.y; g[2] += v.z; g[3] += v.w;
+      const bool w1row = p0 < P_B1;  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per group
+      const float* dbs = a.slab + P_B1 + (w1row ? p0 / D_IN : 0);
+      float db = 0.f;
+      constexpr int U = 8;  // slices per thread per batch of loads (28 slices / 4 threads = 7)
+      for (int s0 = part; s0 < a.slices; s0 += SGD_TPG * U) {
+        float4 v[U];
+        float d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int sidx = s0 + u * SGD_TPG;
+          v[u] = sidx < a.slices ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+          d[u] = (w1row && sidx < a.slices) ? dbs[(long)sidx * a.slab_stride] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          g[0] += v[u].x; g[1] += v[u].y; g[2] += v[u].z; g[3] += v[u].w;
+          db += d[u];
+        }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) g[j] = group_sum(g[j]);
       gme = g[part & 3];
-      if (p0 < P_B1) {  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per group
-        const float* dbs = a.slab + P_B1 + p0 / D_IN;
-        float db = 0.f;
-        for (int sidx = part; sidx < a.slices; sidx += SGD_TPG) db += dbs[(long)sidx * a.slab_stride];
+      if (w1row) {
         db = group_sum(db);
         gme = a.xa * gme + a.xb * db;
       }
@@ -1507,7 +1528,7 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
     gme = mine ? a.grad_in[p] : 0.f;
   }
   if (!mine) return;
-  sgd_apply(a, p, gme);
+  sgd_apply(a, p, gme, w0, m0);
 }
 
 // ---------------------------------------------------------------------------
