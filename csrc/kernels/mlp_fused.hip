@@ -1450,11 +1450,16 @@ __device__ __forceinline__ void sgd_apply(const SgdArgs& a, long p, float gme, f
   }
   w -= a.lr * d;
   a.w[p] = w;
+#if SL_SGD_KO != 1  // timing knockout 1: no bf16 shadow writes
   write_shadow(a, p, w);
+#endif
 }
 
 // SGD_TPG threads per float4 group of parameters: each sums every SGD_TPG-th
 // slab slice, the group combines by DPP (quad perms, then row_half_mirror for 8).
+#ifndef SL_SGD_KO
+#define SL_SGD_KO 0  // timing knockouts of mlp_sgd_kernel (1: no shadow writes, 2: no slab reads)
+#endif
 #ifndef SL_SGD_TPG
 #define SL_SGD_TPG 4
 #endif
@@ -1502,6 +1507,11 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int sidx = s0 + u * SGD_TPG;
+#if SL_SGD_KO == 2  // timing knockout 2: no slab reads
+          v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          d[u] = 0.f;
+          continue;
+#endif
           v[u] = sidx < a.slices ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
                                  : make_float4(0.f, 0.f, 0.f, 0.f);
           d[u] = (w1row && sidx < a.slices) ? dbs[(long)sidx * a.slab_stride] : 0.f;
