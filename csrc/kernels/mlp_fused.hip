@@ -892,6 +892,18 @@ struct WgArgs {
 constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages in flight
 constexpr int WG_IMG = 64 * 128;          // one [64 k][128] bf16 image, unpadded (swizzled)
 constexpr int WG_SLOT = 3 * WG_IMG;       // A half 0, A half 1, B = 48 KB
+#ifndef SL_WG_RING4
+#define SL_WG_RING4 0  // u8 (dW1) tiles: 4 slots of 40 KB (three stages in flight) instead of 3 of 48 KB; A/B neutral (profiles/r01_v15)
+#endif
+// u8 tiles need only 8 KB of B per slot: 4 x 40 KB fill the 160 KB of LDS exactly
+constexpr int WG_NSLOT8 = SL_WG_RING4 ? 4 : WG_NSLOT;
+constexpr int WG_SLOT8 = SL_WG_RING4 ? 2 * WG_IMG + WG_IMG / 2 : WG_SLOT;
+constexpr int WG_LDS = WG_NSLOT8 * WG_SLOT8 > WG_NSLOT * WG_SLOT ? WG_NSLOT8 * WG_SLOT8 : WG_NSLOT * WG_SLOT;
+template <bool U8> constexpr int wg_ns() { return U8 ? WG_NSLOT8 : WG_NSLOT; }
+template <bool U8> constexpr int wg_slot() { return U8 ? WG_SLOT8 : WG_SLOT; }
+#if SL_WG_RING4 && !SL_WG_PIPE
+#error "SL_WG_RING4 needs the pipelined main loop"
+#endif
 
 // 16-B chunk position inside a 256-B image row.  XOR on chunk-pair bits with
 // f(r) = (r & 3) | ((r >> 3) & 1) << 2 makes every ds_read_b64_tr_b16 of the
@@ -983,7 +995,7 @@ constexpr int WG_NF = WG_MI + WG_NJ;       // fragments per wave per k-step
 #endif
 
 __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[WG_NSLOT * WG_SLOT];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WG_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
   const int wm = SL_WG_W128 ? (wave & 1) : (wave & 3), wn = SL_WG_W128 ? (wave >> 1) : (wave >> 2);
@@ -1023,12 +1035,12 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     const int col = min(n0 + c * 16, P.ldb - 16);  // columns >= 784 are don't-care columns of dW1
     bsrc8 = static_cast<const uint8_t*>(P.b) + (xrow0 + st0 * 64 + row) * P.ldb + col;
   }
-  auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % 3
+  auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % NS
     constexpr bool U8 = decltype(u8_c)::value;
 #if SL_WG_KO == 2 || SL_WG_KO == 4  // timing knockout: no operand movement (stage 0 only)
     if (st > 0) return;
 #endif
-    uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
+    uint16_t* Ai = smem + (st % wg_ns<U8>()) * wg_slot<U8>();
     uint16_t* Bi = Ai + 2 * WG_IMG;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -1050,20 +1062,20 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   using T_ = std::true_type;
   using F_ = std::false_type;
   if (u8b) {
-    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, T_{});
+    for (int st = 0; st < wg_ns<true>() - 1 && st < nst; ++st) issue(st, T_{});
   } else {
-    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, F_{});
+    for (int st = 0; st < wg_ns<false>() - 1 && st < nst; ++st) issue(st, F_{});
   }
 
   // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
   // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
-  // a fixed-order sum through LDS (deterministic).  Scratch in ring slot 2, whose first
-  // LDS-DMA (stage 2) is issued after the main loop's first barrier. ----
+  // a fixed-order sum through LDS (deterministic).  Scratch in the last ring slot, whose
+  // first LDS-DMA (stage NS-1) is issued after the main loop's first barrier. ----
   {
     constexpr int NC4 = W3P_LD / 4;
     const int per = (NC4 + A.total_tiles - 1) / A.total_tiles;
     const int c0 = t * per, nc = min(NC4, c0 + per) - c0;
-    float4* red = reinterpret_cast<float4*>(smem + 2 * WG_SLOT);
+    float4* red = reinterpret_cast<float4*>(smem + (u8b ? (WG_NSLOT8 - 1) * WG_SLOT8 : (WG_NSLOT - 1) * WG_SLOT));
     const int G = WG_NT / nc, col = tid % nc, g = tid / nc;
     if (g < G) {
       const float4* src = reinterpret_cast<const float4*>(A.w3p + (long)st0 * W3P_LD) + c0 + col;
@@ -1188,6 +1200,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     constexpr int NBR = NB > 0 ? NB : 1;
     constexpr int PPS = U8 ? 5 : 6;
     constexpr int KB = U8 ? 4096 : 8192;
+    constexpr int NS = wg_ns<U8>(), SLOT = wg_slot<U8>();  // ring depth / slot stride (uint16)
     short8_t fa[2][2][WG_MI]; // [set][k-step][m-block]
     short8_t fb[2][2][NBR];   // bf16 B fragments
     uint2v_t fr[2][2][NBR];   // raw u8 B fragments (converted next to their MFMAs)
@@ -1197,7 +1210,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     auto read_stage = [&](int st, auto set_c) {
       constexpr int S = decltype(set_c)::value;
       if constexpr (NB > 0) {
-        const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
+        const uint32_t sb = lds_base + (uint32_t)((st % NS) * SLOT * 2);
 #pragma unroll
         for (int i = 0; i < WG_MI; ++i) fa[S][0][i] = wg_tr8<0>(sb + a_addr[i]);
 #pragma unroll
@@ -1266,11 +1279,11 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     auto step = [&](int st, auto cur_c, auto nxt_c) {
       constexpr int C = decltype(cur_c)::value;
       if (st + 1 < nst) {
-        wg_vmcnt<PPS>(min(1, nst - 2 - st));  // stage st+1 has landed (stage st+2 may be in flight)
+        wg_vmcnt<PPS>(min(NS - 2, nst - 2 - st));  // stage st+1 has landed (st+2 .. st+NS-1 may be in flight)
         __builtin_amdgcn_s_barrier();          // ... for everyone; every wave is done reading stage st
-        if (st + 3 < nst) issue(st + 3, u8_c);  // into stage st's slot
+        if (st + NS < nst) issue(st + NS, u8_c);  // into stage st's slot
       }
-      const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % WG_NSLOT) * WG_SLOT * 2);
+      const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % NS) * SLOT * 2);
       __builtin_amdgcn_sched_barrier(0);
 #if SL_WG_CVT
       if constexpr (U8 && NB > 0) {
@@ -1337,9 +1350,9 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
-    wg_vmcnt<PPS>(min(1, nst - 1));  // stage 0 has landed (stage 1 may be in flight)
+    wg_vmcnt<PPS>(min(NS - 2, nst - 1));  // stage 0 has landed (stages 1 .. NS-2 may be in flight)
     __builtin_amdgcn_s_barrier();
-    if (2 < nst) issue(2, u8_c);
+    if (NS - 1 < nst) issue(NS - 1, u8_c);  // the last slot: free once the prologue sums are done
     read_stage(0, S0{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
