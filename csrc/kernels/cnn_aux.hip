@@ -106,9 +106,22 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 // Per-channel sums of dz = dy*1[y>0] and dz*x.  Thread layout: TPR = C/8
 // threads per row, 256/TPR rows per pass; partials folded through LDS, then
 // across workgroups through an rsum buffer (result at rsum_result(sums, 2C)).
+// ReLU mask of y = relu(x*scale + shift) re-derived from the BN input x and the
+// forward coefficients (coef rows 0/1 = scale/shift, written by bn_publish), so
+// the backward of a non-residual BN+ReLU never reads y: 2 streams instead of 3.
+__device__ __forceinline__ void relu_mask_coef8(const float* __restrict__ coef, int C, int c0, float (&sc)[8],
+                                                float (&sh)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = coef[c0 + j];
+    sh[j] = coef[C + c0 + j];
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
                                                             const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ x,
+                                                            const float* __restrict__ mcoef,
                                                             uint16_t* __restrict__ dz_out, float* __restrict__ sums,
                                                             long rows, int C) {
   __shared__ float part[256][17];
@@ -116,19 +129,24 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   const int tid = threadIdx.x;
   const int cg = tid % tpr, rsub = tid / tpr;
   float s[8] = {0.f}, d[8] = {0.f};
+  float msc[8], msh[8];
+  if (mcoef) relu_mask_coef8(mcoef, C, cg * 8, msc, msh);
   if (rsub < rpp) {
     for (long r = (long)blockIdx.x * rpp + rsub; r < rows; r += (long)gridDim.x * rpp) {
       const long off = r * C + cg * 8;
       float g[8], xv[8];
       unpack8(ld8(dy + off), g);
+      unpack8(ld8(x + off), xv);
       if (y) {
         float yv[8];
         unpack8(ld8(y + off), yv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      } else if (mcoef) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = xv[j] * msc[j] + msh[j] > 0.f ? g[j] : 0.f;
       }
       if (dz_out) *reinterpret_cast<short8_t*>(dz_out + off) = pack8(g);
-      unpack8(ld8(x + off), xv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s[j] += g[j];
@@ -279,6 +297,7 @@ __global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __r
 __global__ __launch_bounds__(256) void bn_bwd_apply_sums_kernel(const uint16_t* __restrict__ dy,
                                                                 const uint16_t* __restrict__ y,
                                                                 const uint16_t* __restrict__ x,
+                                                                const float* __restrict__ mcoef,
                                                                 const float* __restrict__ sums,
                                                                 const float* __restrict__ coef,
                                                                 float* __restrict__ grad_gamma,
@@ -300,16 +319,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_sums_kernel(const uint16_t* 
     cb[j] = -sc * rstd * sdxh / count;
     cc[j] = -sc * s0 / count - cb[j] * mean;
   }
+  float msc[8], msh[8];
+  if (mcoef) relu_mask_coef8(mcoef, C, c0, msc, msh);
   for (long q = t0; q < total; q += (long)gridDim.x * blockDim.x) {
     float g[8], xv[8];
     unpack8(ld8(dy + q * 8), g);
+    unpack8(ld8(x + q * 8), xv);
     if (y) {
       float yv[8];
       unpack8(ld8(y + q * 8), yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    } else if (mcoef) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = xv[j] * msc[j] + msh[j] > 0.f ? g[j] : 0.f;
     }
-    unpack8(ld8(x + q * 8), xv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = ca[j] * g[j] + cb[j] * xv[j] + cc[j];
     *reinterpret_cast<short8_t*>(dx + q * 8) = pack8(g);
@@ -526,14 +550,15 @@ int sl_bn_apply(const uint16_t* x, const float* coef, const uint16_t* res, const
   return 0;
 }
 
-int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, uint16_t* dz_out, float* sums,
-                     long rows, int C, hipStream_t stream) {
+int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* mcoef,
+                     uint16_t* dz_out, float* sums, long rows, int C, hipStream_t stream) {
   if ((C & 7) || C > 2048 || (C & (C - 1))) return -1;
   const int rpp = 256 / (C / 8);
   long blocks = (rows + rpp * 8 - 1) / (rpp * 8);  // >= 8 rows per thread
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, dz_out, sums, rows, C);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, dz_out, sums, rows,
+                     C);
   SL_CHECK_LAUNCH();
   return 0;
 }
@@ -570,12 +595,12 @@ int sl_bn_apply_stats(const uint16_t* x, const float* stats, const float* gamma,
   return 0;
 }
 
-int sl_bn_bwd_apply_sums(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* sums,
+int sl_bn_bwd_apply_sums(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* mcoef, const float* sums,
                          const float* coef, float* grad_gamma, float* grad_beta, uint16_t* dx, long rows, int C,
                          float count, hipStream_t stream) {
   if ((C & 7) || 256 % (C / 8) != 0) return -1;
-  hipLaunchKernelGGL(bn_bwd_apply_sums_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, dy, y, x, sums,
-                     coef, grad_gamma, grad_beta, dx, rows, C, count);
+  hipLaunchKernelGGL(bn_bwd_apply_sums_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, dy, y, x, mcoef,
+                     sums, coef, grad_gamma, grad_beta, dx, rows, C, count);
   SL_CHECK_LAUNCH();
   return 0;
 }

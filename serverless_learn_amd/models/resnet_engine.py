@@ -260,8 +260,10 @@ class FusedResNetTrainer:
             K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
             K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g)
             K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"])
-            K.bn_bwd_reduce(st["da1"], st["a1"], st["c1"], b1.sums_buf)
-            K.bn_bwd_apply_sums(st["da1"], st["a1"], st["c1"], b1.sums, b1.coef, b1.ggamma, b1.gbeta, st["dc1"])
+            # a1 = relu(bn1(c1)): the mask is re-derived from c1 and bn1's coefficients
+            K.bn_bwd_reduce(st["da1"], None, st["c1"], b1.sums_buf, mask_coef=b1.coef)
+            K.bn_bwd_apply_sums(st["da1"], None, st["c1"], b1.sums, b1.coef, b1.ggamma, b1.gbeta, st["dc1"],
+                                mask_coef=b1.coef)
             K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g)
             K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, st["dx"], add=add)
             dy = st["dx"]
@@ -271,8 +273,9 @@ class FusedResNetTrainer:
         if spec.stem == "imagenet":
             K.maxpool_bwd(dy, self.p0_arg, self.da0)
             dy = self.da0
-        K.bn_bwd_reduce(dy, self.a0, self.c0, sbn.sums_buf)
-        K.bn_bwd_apply_sums(dy, self.a0, self.c0, sbn.sums, sbn.coef, sbn.ggamma, sbn.gbeta, self.dc0)
+        K.bn_bwd_reduce(dy, None, self.c0, sbn.sums_buf, mask_coef=sbn.coef)
+        K.bn_bwd_apply_sums(dy, None, self.c0, sbn.sums, sbn.coef, sbn.ggamma, sbn.gbeta, self.dc0,
+                            mask_coef=sbn.coef)
         sc = spec.stem_conv
         K.conv_wgrad(self.x0, self.dc0, 64, sc.k, sc.stride, sc.pad, self.conv["stem"].g)
         maybe_bucket(0, force=True)

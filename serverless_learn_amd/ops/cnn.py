@@ -24,13 +24,13 @@ N.register("sl_input_norm", [P, P, P, I, I, L, P, P, F, F, F, F, F, F, P])
 N.register("sl_cursor_bump", [P, P])
 N.register("sl_bn_finalize", [P, P, P, P, P, P, I, F, F, F, P])
 N.register("sl_bn_apply", [P, P, P, P, P, L, I, I, I, P])
-N.register("sl_bn_bwd_reduce", [P, P, P, P, P, L, I, P])
+N.register("sl_bn_bwd_reduce", [P, P, P, P, P, P, L, I, P])
 N.register("sl_bn_bwd_finalize", [P, P, P, P, P, I, F, P])
 N.register("sl_bn_bwd_apply", [P, P, P, P, P, L, I, P])
 N.register("sl_rsum_floats", [I], ctypes.c_long)
 N.register("sl_rsum_result_offset", [I], ctypes.c_long)
 N.register("sl_bn_apply_stats", [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, F, F, F, P])
-N.register("sl_bn_bwd_apply_sums", [P, P, P, P, P, P, P, P, L, I, F, P])
+N.register("sl_bn_bwd_apply_sums", [P, P, P, P, P, P, P, P, P, L, I, F, P])
 N.register("sl_maxpool_fwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_maxpool_bwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_avgpool_fwd", [P, P, I, I, I, P])
@@ -154,10 +154,16 @@ def bn_apply(x, coef, y, relu=True, res=None, rcoef=None):
            rows, c, 1 if relu else 0, mode, N.stream_ptr())
 
 
-def bn_bwd_reduce(dy, y, x, sums, dz_out=None):
+def bn_bwd_reduce(dy, y, x, sums, dz_out=None, mask_coef=None):
+    """dz = dy * relu'(.) and the per-channel sums for the BN backward.  The ReLU
+    mask comes from ``y`` (block outputs with a residual) or, for a plain
+    ``y = relu(bn(x))``, from ``x`` and the layer's forward ``mask_coef``
+    (scale/shift rows of ``coef``), so ``y`` is never read."""
     c = x.shape[-1]
     rows = x.numel() // c
+    assert y is None or mask_coef is None
     N.call("sl_bn_bwd_reduce", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x),
+           _f32(mask_coef) if mask_coef is not None else None,
            _bf16(dz_out) if dz_out is not None else None, _f32(sums), rows, c, N.stream_ptr())
 
 
@@ -187,11 +193,14 @@ def bn_apply_stats(x, bn, y, count, relu=True, res=None, rbn=None, eps=1e-5, mom
            _bf16(y), rows, c, 1 if relu else 0, mode, float(count), float(eps), float(momentum), N.stream_ptr())
 
 
-def bn_bwd_apply_sums(dy, y, x, sums, coef, grad_gamma, grad_beta, dx):
-    """Fused backward finalize + apply: dx, and dgamma/dbeta accumulated into the flat gradient."""
+def bn_bwd_apply_sums(dy, y, x, sums, coef, grad_gamma, grad_beta, dx, mask_coef=None):
+    """Fused backward finalize + apply: dx, and dgamma/dbeta accumulated into the flat gradient.
+    ``mask_coef`` as in :func:`bn_bwd_reduce`."""
     c = x.shape[-1]
     rows = x.numel() // c
-    N.call("sl_bn_bwd_apply_sums", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x), _f32(sums),
+    assert y is None or mask_coef is None
+    N.call("sl_bn_bwd_apply_sums", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x),
+           _f32(mask_coef) if mask_coef is not None else None, _f32(sums),
            _f32(coef), _f32(grad_gamma), _f32(grad_beta), _bf16(dx), rows, c, float(rows), N.stream_ptr())
 
 

@@ -129,6 +129,51 @@ def test_weight_transposer_matches_permute():
     assert torch.equal(t2.view(512, 16), e2)
 
 
+@pytest.mark.parametrize("c", [64, 256])
+def test_bn_relu_backward_mask_from_coef(c):
+    """y = relu(bn(x)) backward with the ReLU mask re-derived from x and the
+    forward coefficients (no read of y) vs fp32 torch and vs the y-mask path."""
+    from serverless_learn_amd.ops import cnn as K
+
+    torch.manual_seed(3)
+    n, h = 8, 8
+    x = bf(torch.randn(n, h, h, c, device=DEV) * 1.5 - 0.3)
+    xf = x.float().reshape(-1, c)
+
+    class _B:
+        pass
+    b = _B()
+    b.stats = torch.stack([xf.sum(0), (xf * xf).sum(0)]).reshape(-1).contiguous()
+    b.gamma, b.beta = torch.rand(c, device=DEV) + 0.5, torch.randn(c, device=DEV)
+    b.coef, b.run_mean, b.run_var = torch.zeros(4 * c, device=DEV), torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+    y = torch.empty_like(x)
+    K.bn_apply_stats(x, b, y, xf.shape[0])
+
+    xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    g_ = b.gamma.clone().requires_grad_(True)
+    b_ = b.beta.clone().requires_grad_(True)
+    ref = F.relu(F.batch_norm(xr, None, None, g_, b_, training=True))
+    dy = bf(torch.randn_like(ref).permute(0, 2, 3, 1).contiguous())
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+
+    outs = {}
+    for mode in ("y", "coef"):
+        sbuf = torch.zeros(K.rsum_floats(2 * c), device=DEV)
+        yy, mc = (y, None) if mode == "y" else (None, b.coef)
+        K.bn_bwd_reduce(dy, yy, x, sbuf, mask_coef=mc)
+        sums = K.rsum_result(sbuf, 2 * c)
+        gg, gb = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
+        dx = torch.empty_like(x)
+        K.bn_bwd_apply_sums(dy, yy, x, sums, b.coef, gg, gb, dx, mask_coef=mc)
+        torch.cuda.synchronize()
+        outs[mode] = (dx.float(), gg, gb)
+    dx, gg, gb = outs["coef"]
+    assert rel(dx.permute(0, 3, 1, 2), xr.grad) < 2e-2
+    assert rel(gg, g_.grad) < 1e-2 and rel(gb, b_.grad) < 1e-2
+    dxy, ggy, gby = outs["y"]
+    assert rel(dx, dxy) < 1e-3 and rel(gg, ggy) < 1e-4 and rel(gb, gby) < 1e-4
+
+
 def test_bn_forward_backward_matches_torch():
     from serverless_learn_amd.ops import cnn as K
 
