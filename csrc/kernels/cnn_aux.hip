@@ -554,8 +554,14 @@ int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
                      uint16_t* dz_out, float* sums, long rows, int C, hipStream_t stream) {
   if ((C & 7) || C > 2048 || (C & (C - 1))) return -1;
   const int rpp = 256 / (C / 8);
+  static int cap = -1;  // grid cap; SL_BNRED_BLOCKS overrides it for A/B runs
+  if (cap < 0) {
+    const char* e = getenv("SL_BNRED_BLOCKS");
+    cap = e ? atoi(e) : 512;  // measured: 128/256/384/512/768/1024/2048/4096 -> profiles/r01_v16
+    if (cap < 1) cap = 512;
+  }
   long blocks = (rows + rpp * 8 - 1) / (rpp * 8);  // >= 8 rows per thread
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, dz_out, sums, rows,
                      C);
