@@ -28,6 +28,17 @@ __device__ __forceinline__ short8_t pack8(const float (&f)[8]) {
   return v;
 }
 
+// Grid cap of the streaming BN apply kernels; SL_BN_APPLY_BLOCKS overrides it for A/B runs.
+static int bn_apply_cap() {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("SL_BN_APPLY_BLOCKS");
+    cap = e ? atoi(e) : 4096;
+    if (cap < 1) cap = 4096;
+  }
+  return cap;
+}
+
 static int blocks_for(long items, int cap = 4096) {
   long b = (items + 255) / 256;
   if (b > cap) b = cap;
@@ -595,7 +606,7 @@ int sl_bn_apply_stats(const uint16_t* x, const float* stats, const float* gamma,
   if (mode == 2 && !rstats) return -2;
   BnStats b{stats, gamma, beta, coef, run_mean, run_var};
   BnStats rb{rstats, rgamma, rbeta, rcoef, rrun_mean, rrun_var};
-  hipLaunchKernelGGL(bn_apply_stats_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, x, b, res, rb, y,
+  hipLaunchKernelGGL(bn_apply_stats_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0, stream, x, b, res, rb, y,
                      rows, C, relu, mode, count, eps, momentum);
   SL_CHECK_LAUNCH();
   return 0;
@@ -605,7 +616,7 @@ int sl_bn_bwd_apply_sums(const uint16_t* dy, const uint16_t* y, const uint16_t* 
                          const float* coef, float* grad_gamma, float* grad_beta, uint16_t* dx, long rows, int C,
                          float count, hipStream_t stream) {
   if ((C & 7) || 256 % (C / 8) != 0) return -1;
-  hipLaunchKernelGGL(bn_bwd_apply_sums_kernel, dim3(blocks_for(rows * (C / 8))), dim3(256), 0, stream, dy, y, x, mcoef,
+  hipLaunchKernelGGL(bn_bwd_apply_sums_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0, stream, dy, y, x, mcoef,
                      sums, coef, grad_gamma, grad_beta, dx, rows, C, count);
   SL_CHECK_LAUNCH();
   return 0;
