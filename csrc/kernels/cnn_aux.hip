@@ -133,6 +133,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ x,
                                                             const float* __restrict__ mcoef,
+                                                            const uint8_t* __restrict__ ymask,
                                                             uint16_t* __restrict__ dz_out, float* __restrict__ sums,
                                                             long rows, int C) {
   __shared__ float part[256][17];
@@ -153,6 +154,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
         unpack8(ld8(y + off), yv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      } else if (ymask) {
+        const unsigned m = ymask[off >> 3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = (m >> j) & 1u ? g[j] : 0.f;
       } else if (mcoef) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = xv[j] * msc[j] + msh[j] > 0.f ? g[j] : 0.f;
@@ -271,8 +276,9 @@ __device__ __forceinline__ void bn_publish(const BnStats& b, int C, float count,
 // y = relu?(bn(x) + r), r = 0 | res | bn_r(res); grid stride is a multiple of C/8.
 __global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __restrict__ x, BnStats b,
                                                              const uint16_t* __restrict__ res, BnStats rb,
-                                                             uint16_t* __restrict__ y, long rows, int C, int relu,
-                                                             int mode, float count, float eps, float momentum) {
+                                                             uint16_t* __restrict__ y, uint8_t* __restrict__ mask_out,
+                                                             long rows, int C, int relu, int mode, float count,
+                                                             float eps, float momentum) {
   const int cpr = C >> 3;
   const long total = rows * cpr;
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -295,7 +301,14 @@ __global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __r
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
     }
-    *reinterpret_cast<short8_t*>(y + q * 8) = pack8(f);
+    const short8_t yv = pack8(f);
+    *reinterpret_cast<short8_t*>(y + q * 8) = yv;
+    if (mask_out) {  // bit j = (stored bf16 y > 0), 1 B per 8 channels
+      unsigned m = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m |= (unsigned)(yv[j] > 0) << j;
+      mask_out[q] = (uint8_t)m;
+    }
   }
   if (blockIdx.x == 0) {
     bn_publish(b, C, count, eps, momentum);
@@ -562,7 +575,7 @@ int sl_bn_apply(const uint16_t* x, const float* coef, const uint16_t* res, const
 }
 
 int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* mcoef,
-                     uint16_t* dz_out, float* sums, long rows, int C, hipStream_t stream) {
+                     const uint8_t* ymask, uint16_t* dz_out, float* sums, long rows, int C, hipStream_t stream) {
   if ((C & 7) || C > 2048 || (C & (C - 1))) return -1;
   const int rpp = 256 / (C / 8);
   static int cap = -1;  // grid cap; SL_BNRED_BLOCKS overrides it for A/B runs
@@ -574,7 +587,7 @@ int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
   long blocks = (rows + rpp * 8 - 1) / (rpp * 8);  // >= 8 rows per thread
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, dz_out, sums, rows,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, ymask, dz_out, sums, rows,
                      C);
   SL_CHECK_LAUNCH();
   return 0;
@@ -599,15 +612,16 @@ int sl_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, co
 
 int sl_bn_apply_stats(const uint16_t* x, const float* stats, const float* gamma, const float* beta, float* coef,
                       float* run_mean, float* run_var, const uint16_t* res, const float* rstats, const float* rgamma,
-                      const float* rbeta, float* rcoef, float* rrun_mean, float* rrun_var, uint16_t* y, long rows,
-                      int C, int relu, int mode, float count, float eps, float momentum, hipStream_t stream) {
+                      const float* rbeta, float* rcoef, float* rrun_mean, float* rrun_var, uint16_t* y,
+                      uint8_t* mask_out, long rows, int C, int relu, int mode, float count, float eps, float momentum,
+                      hipStream_t stream) {
   if ((C & 7) || 256 % (C / 8) != 0) return -1;
   if (mode && !res) return -2;
   if (mode == 2 && !rstats) return -2;
   BnStats b{stats, gamma, beta, coef, run_mean, run_var};
   BnStats rb{rstats, rgamma, rbeta, rcoef, rrun_mean, rrun_var};
   hipLaunchKernelGGL(bn_apply_stats_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0, stream, x, b, res, rb, y,
-                     rows, C, relu, mode, count, eps, momentum);
+                     mask_out, rows, C, relu, mode, count, eps, momentum);
   SL_CHECK_LAUNCH();
   return 0;
 }

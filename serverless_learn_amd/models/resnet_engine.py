@@ -131,6 +131,8 @@ class FusedResNetTrainer:
             shp = (B, oh, oh, blk.conv1.cout)
             for name in ("c1", "a1", "c2", "y", "dz", "dc2", "da1", "dc1"):
                 st[name] = torch.empty(shp, **bf)
+            # 1-bit ReLU mask of y (bit j of byte q = y[8q+j] > 0) for the backward
+            st["ym"] = torch.empty(B * oh * oh * blk.conv1.cout // 8, dtype=torch.uint8, device=dev)
             if blk.down is not None:
                 st["cs"] = torch.empty(shp, **bf)
                 st["dcs"] = torch.empty(shp, **bf)
@@ -217,9 +219,11 @@ class FusedResNetTrainer:
             if blk.down is not None:
                 bd = self.bn[blk.dbn.name]
                 self._conv_bn(st["x"], self.conv[blk.down.name], bd, st["cs"])
-                K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=st["cs"], rbn=bd, momentum=self.bn_momentum)
+                K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=st["cs"], rbn=bd, momentum=self.bn_momentum,
+                                 mask_out=st["ym"])
             else:
-                K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=st["x"], momentum=self.bn_momentum)
+                K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=st["x"], momentum=self.bn_momentum,
+                                 mask_out=st["ym"])
         K.avgpool_fwd(self.feat_in, self.feat)
         K.conv_fwd(self.feat, self.fc_w, spec.classes, 1, 1, 0, yf=self.logits, bias=self.fc_b)
         K.softmax_ce(self.logits, self.labels, self.loss, self.correct, self.dlogits.view(self.batch, LOGIT_LD),
@@ -247,8 +251,9 @@ class FusedResNetTrainer:
             blk: BlockSpec = st["spec"]
             c1, c2 = self.conv[blk.conv1.name], self.conv[blk.conv2.name]
             b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
-            # y = relu(bn2(c2) + sc): dz = dy * 1[y > 0] feeds bn2 and the shortcut
-            K.bn_bwd_reduce(dy, st["y"], st["c2"], b2.sums_buf, dz_out=st["dz"])
+            # y = relu(bn2(c2) + sc): dz = dy * 1[y > 0] feeds bn2 and the shortcut; the
+            # mask comes from the forward's 1-bit image of y, not from y itself
+            K.bn_bwd_reduce(dy, None, st["c2"], b2.sums_buf, dz_out=st["dz"], y_mask=st["ym"])
             add = st["dz"]
             if blk.down is not None:
                 cd, bd = self.conv[blk.down.name], self.bn[blk.dbn.name]

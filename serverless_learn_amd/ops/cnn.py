@@ -24,12 +24,12 @@ N.register("sl_input_norm", [P, P, P, I, I, L, P, P, F, F, F, F, F, F, P])
 N.register("sl_cursor_bump", [P, P])
 N.register("sl_bn_finalize", [P, P, P, P, P, P, I, F, F, F, P])
 N.register("sl_bn_apply", [P, P, P, P, P, L, I, I, I, P])
-N.register("sl_bn_bwd_reduce", [P, P, P, P, P, P, L, I, P])
+N.register("sl_bn_bwd_reduce", [P, P, P, P, P, P, P, L, I, P])
 N.register("sl_bn_bwd_finalize", [P, P, P, P, P, I, F, P])
 N.register("sl_bn_bwd_apply", [P, P, P, P, P, L, I, P])
 N.register("sl_rsum_floats", [I], ctypes.c_long)
 N.register("sl_rsum_result_offset", [I], ctypes.c_long)
-N.register("sl_bn_apply_stats", [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, F, F, F, P])
+N.register("sl_bn_apply_stats", [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, F, F, F, P])
 N.register("sl_bn_bwd_apply_sums", [P, P, P, P, P, P, P, P, P, L, I, F, P])
 N.register("sl_maxpool_fwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_maxpool_bwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
@@ -154,16 +154,20 @@ def bn_apply(x, coef, y, relu=True, res=None, rcoef=None):
            rows, c, 1 if relu else 0, mode, N.stream_ptr())
 
 
-def bn_bwd_reduce(dy, y, x, sums, dz_out=None, mask_coef=None):
+def bn_bwd_reduce(dy, y, x, sums, dz_out=None, mask_coef=None, y_mask=None):
     """dz = dy * relu'(.) and the per-channel sums for the BN backward.  The ReLU
     mask comes from ``y`` (block outputs with a residual) or, for a plain
     ``y = relu(bn(x))``, from ``x`` and the layer's forward ``mask_coef``
-    (scale/shift rows of ``coef``), so ``y`` is never read."""
+    (scale/shift rows of ``coef``), so ``y`` is never read.  ``y_mask`` is the
+    1-bit-per-channel ReLU mask written by :func:`bn_apply_stats` (``mask_out``)
+    for block outputs with a residual: 1/16 of the bytes of ``y``."""
     c = x.shape[-1]
     rows = x.numel() // c
-    assert y is None or mask_coef is None
+    assert (y is not None) + (mask_coef is not None) + (y_mask is not None) <= 1
+    if y_mask is not None:
+        assert y_mask.dtype == torch.uint8 and y_mask.numel() * 8 == x.numel() and y_mask.is_contiguous()
     N.call("sl_bn_bwd_reduce", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x),
-           _f32(mask_coef) if mask_coef is not None else None,
+           _f32(mask_coef) if mask_coef is not None else None, p(y_mask) if y_mask is not None else None,
            _bf16(dz_out) if dz_out is not None else None, _f32(sums), rows, c, N.stream_ptr())
 
 
@@ -180,8 +184,11 @@ def bn_bwd_apply(dy, y, x, dcoef, dx):
            rows, c, N.stream_ptr())
 
 
-def bn_apply_stats(x, bn, y, count, relu=True, res=None, rbn=None, eps=1e-5, momentum=0.1):
-    """Fused finalize + apply; ``bn``/``rbn`` expose stats, gamma, beta, coef, run_mean, run_var."""
+def bn_apply_stats(x, bn, y, count, relu=True, res=None, rbn=None, eps=1e-5, momentum=0.1, mask_out=None):
+    """Fused finalize + apply; ``bn``/``rbn`` expose stats, gamma, beta, coef, run_mean, run_var.
+    ``mask_out`` (u8, numel/8) receives bit j of byte q = ``y[8q+j] > 0``."""
+    if mask_out is not None:
+        assert mask_out.dtype == torch.uint8 and mask_out.numel() * 8 == x.numel() and mask_out.is_contiguous()
     c = x.shape[-1]
     rows = x.numel() // c
     mode = 0 if res is None else (2 if rbn is not None else 1)
@@ -190,7 +197,7 @@ def bn_apply_stats(x, bn, y, count, relu=True, res=None, rbn=None, eps=1e-5, mom
            _f32(bn.run_mean), _f32(bn.run_var), _bf16(res) if res is not None else None,
            _f32(r.stats) if r else None, _f32(r.gamma) if r else None, _f32(r.beta) if r else None,
            _f32(r.coef) if r else None, _f32(r.run_mean) if r else None, _f32(r.run_var) if r else None,
-           _bf16(y), rows, c, 1 if relu else 0, mode, float(count), float(eps), float(momentum), N.stream_ptr())
+           _bf16(y), p(mask_out) if mask_out is not None else None, rows, c, 1 if relu else 0, mode, float(count), float(eps), float(momentum), N.stream_ptr())
 
 
 def bn_bwd_apply_sums(dy, y, x, sums, coef, grad_gamma, grad_beta, dx, mask_coef=None):

@@ -174,6 +174,43 @@ def test_bn_relu_backward_mask_from_coef(c):
     assert rel(dx, dxy) < 1e-3 and rel(gg, ggy) < 1e-4 and rel(gb, gby) < 1e-4
 
 
+def test_bn_residual_relu_bitmask():
+    """bn_apply_stats' 1-bit ReLU mask of y = relu(bn(x) + res) drives
+    bn_bwd_reduce exactly like reading y does."""
+    from serverless_learn_amd.ops import cnn as K
+
+    torch.manual_seed(5)
+    n, h, c = 8, 8, 128
+    x = bf(torch.randn(n, h, h, c, device=DEV))
+    res = bf(torch.randn(n, h, h, c, device=DEV))
+    xf = x.float().reshape(-1, c)
+
+    class _B:
+        pass
+    b = _B()
+    b.stats = torch.stack([xf.sum(0), (xf * xf).sum(0)]).reshape(-1).contiguous()
+    b.gamma, b.beta = torch.rand(c, device=DEV) + 0.5, torch.randn(c, device=DEV)
+    b.coef, b.run_mean, b.run_var = torch.zeros(4 * c, device=DEV), torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+    y = torch.empty_like(x)
+    m = torch.full((x.numel() // 8,), 0xAA, dtype=torch.uint8, device=DEV)
+    K.bn_apply_stats(x, b, y, xf.shape[0], res=res, mask_out=m)
+    torch.cuda.synchronize()
+    bits = (m.view(-1, 1).int() >> torch.arange(8, device=DEV, dtype=torch.int32)) & 1
+    assert torch.equal(bits.reshape(-1).bool(), y.reshape(-1).float() > 0)
+
+    dy = bf(torch.randn_like(x.float()))
+    outs = []
+    for kw in (dict(y=y), dict(y=None, y_mask=m)):
+        sbuf = torch.zeros(K.rsum_floats(2 * c), device=DEV)
+        dz = torch.empty_like(x)
+        yy = kw.pop("y")
+        K.bn_bwd_reduce(dy, yy, x, sbuf, dz_out=dz, **kw)
+        torch.cuda.synchronize()
+        outs.append((dz.clone(), K.rsum_result(sbuf, 2 * c).clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert rel(outs[1][1], outs[0][1]) < 1e-5
+
+
 def test_bn_forward_backward_matches_torch():
     from serverless_learn_amd.ops import cnn as K
 
