@@ -135,12 +135,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const float* __restrict__ mcoef,
                                                             const uint8_t* __restrict__ ymask,
                                                             uint16_t* __restrict__ dz_out, float* __restrict__ sums,
-                                                            long rows, int C) {
-  __shared__ float part[256][17];
+                                                            const uint16_t* __restrict__ x2,
+                                                            float* __restrict__ sums2, long rows, int C) {
+  // x2/sums2: a second BN fed by the same dz (the downsample shortcut's), whose
+  // sums ride along so dz is not read back: sums2 = (sum dz, sum dz*x2).
+  __shared__ float part[256][25];
   const int tpr = C >> 3, rpp = 256 / tpr;
   const int tid = threadIdx.x;
   const int cg = tid % tpr, rsub = tid / tpr;
-  float s[8] = {0.f}, d[8] = {0.f};
+  float s[8] = {0.f}, d[8] = {0.f}, d2[8] = {0.f};
   float msc[8], msh[8];
   if (mcoef) relu_mask_coef8(mcoef, C, cg * 8, msc, msh);
   if (rsub < rpp) {
@@ -168,24 +171,37 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
         s[j] += g[j];
         d[j] += g[j] * xv[j];
       }
+      if (x2) {
+        float x2v[8];
+        unpack8(ld8(x2 + off), x2v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d2[j] += g[j] * x2v[j];
+      }
     }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     part[tid][j] = s[j];
     part[tid][8 + j] = d[j];
+    part[tid][16 + j] = d2[j];
   }
   __syncthreads();
-  // fold the rpp row-groups: thread t < 2*C handles one (quantity, channel)
+  // fold the rpp row-groups: thread t < 2*C (4*C with x2) handles one (quantity, channel);
+  // quantities 0/1 -> sums, 2/3 -> sums2 (2 is sum dz again, 3 is sum dz*x2)
   float* rep = rsum_replica(sums, 2 * C);
-  for (int t = tid; t < 2 * C; t += 256) {
+  float* rep2 = x2 ? rsum_replica(sums2, 2 * C) : nullptr;
+  const int nq = x2 ? 4 * C : 2 * C;
+  for (int t = tid; t < nq; t += 256) {
     const int qsel = t / C, c = t - qsel * C;
     const int g = c >> 3, j = c & 7;
+    const int col = (qsel == 2 ? 0 : qsel == 3 ? 16 : qsel * 8) + j;
     float acc = 0.f;
-    for (int r = 0; r < rpp; ++r) acc += part[r * tpr + g][qsel * 8 + j];
-    atomicAdd(rep + qsel * C + c, acc);
+    for (int r = 0; r < rpp; ++r) acc += part[r * tpr + g][col];
+    if (qsel < 2) atomicAdd(rep + qsel * C + c, acc);
+    else atomicAdd(rep2 + (qsel - 2) * C + c, acc);
   }
-  rsum_finish(sums, 2 * C, reinterpret_cast<int*>(&part[0][16]));
+  rsum_finish(sums, 2 * C, reinterpret_cast<int*>(&part[0][24]));
+  if (x2) rsum_finish(sums2, 2 * C, reinterpret_cast<int*>(&part[1][24]));
 }
 
 // dcoef layout [3][C]: a, b, c with dx = a*dz + b*x + c.  grad_gamma/beta += (flat gradient).
@@ -575,8 +591,10 @@ int sl_bn_apply(const uint16_t* x, const float* coef, const uint16_t* res, const
 }
 
 int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* mcoef,
-                     const uint8_t* ymask, uint16_t* dz_out, float* sums, long rows, int C, hipStream_t stream) {
+                     const uint8_t* ymask, uint16_t* dz_out, float* sums, const uint16_t* x2, float* sums2,
+                     long rows, int C, hipStream_t stream) {
   if ((C & 7) || C > 2048 || (C & (C - 1))) return -1;
+  if ((x2 == nullptr) != (sums2 == nullptr)) return -2;
   const int rpp = 256 / (C / 8);
   static int cap = -1;  // grid cap; SL_BNRED_BLOCKS overrides it for A/B runs
   if (cap < 0) {
@@ -587,7 +605,7 @@ int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
   long blocks = (rows + rpp * 8 - 1) / (rpp * 8);  // >= 8 rows per thread
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, ymask, dz_out, sums, rows,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, ymask, dz_out, sums, x2, sums2, rows,
                      C);
   SL_CHECK_LAUNCH();
   return 0;

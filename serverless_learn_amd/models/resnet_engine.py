@@ -253,11 +253,14 @@ class FusedResNetTrainer:
             b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
             # y = relu(bn2(c2) + sc): dz = dy * 1[y > 0] feeds bn2 and the shortcut; the
             # mask comes from the forward's 1-bit image of y, not from y itself
-            K.bn_bwd_reduce(dy, None, st["c2"], b2.sums_buf, dz_out=st["dz"], y_mask=st["ym"])
+            # with a downsample shortcut its BN sums (same dz, input cs) come from the same pass
+            down = blk.down is not None
+            bd = self.bn[blk.dbn.name] if down else None
+            K.bn_bwd_reduce(dy, None, st["c2"], b2.sums_buf, dz_out=st["dz"], y_mask=st["ym"],
+                            x2=st["cs"] if down else None, sums2=bd.sums_buf if down else None)
             add = st["dz"]
-            if blk.down is not None:
-                cd, bd = self.conv[blk.down.name], self.bn[blk.dbn.name]
-                K.bn_bwd_reduce(st["dz"], None, st["cs"], bd.sums_buf)
+            if down:
+                cd = self.conv[blk.down.name]
                 K.bn_bwd_apply_sums(st["dz"], None, st["cs"], bd.sums, bd.coef, bd.ggamma, bd.gbeta, st["dcs"])
                 K.conv_wgrad(st["x"], st["dcs"], blk.down.cout, 1, blk.down.stride, 0, cd.g)
                 K.conv_dgrad(st["dcs"], cd.wt, blk.down.cin, 1, blk.down.stride, 0, st["dxs"])

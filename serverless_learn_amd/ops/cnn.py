@@ -24,7 +24,7 @@ N.register("sl_input_norm", [P, P, P, I, I, L, P, P, F, F, F, F, F, F, P])
 N.register("sl_cursor_bump", [P, P])
 N.register("sl_bn_finalize", [P, P, P, P, P, P, I, F, F, F, P])
 N.register("sl_bn_apply", [P, P, P, P, P, L, I, I, I, P])
-N.register("sl_bn_bwd_reduce", [P, P, P, P, P, P, P, L, I, P])
+N.register("sl_bn_bwd_reduce", [P, P, P, P, P, P, P, P, P, L, I, P])
 N.register("sl_bn_bwd_finalize", [P, P, P, P, P, I, F, P])
 N.register("sl_bn_bwd_apply", [P, P, P, P, P, L, I, P])
 N.register("sl_rsum_floats", [I], ctypes.c_long)
@@ -154,21 +154,26 @@ def bn_apply(x, coef, y, relu=True, res=None, rcoef=None):
            rows, c, 1 if relu else 0, mode, N.stream_ptr())
 
 
-def bn_bwd_reduce(dy, y, x, sums, dz_out=None, mask_coef=None, y_mask=None):
+def bn_bwd_reduce(dy, y, x, sums, dz_out=None, mask_coef=None, y_mask=None, x2=None, sums2=None):
     """dz = dy * relu'(.) and the per-channel sums for the BN backward.  The ReLU
     mask comes from ``y`` (block outputs with a residual) or, for a plain
     ``y = relu(bn(x))``, from ``x`` and the layer's forward ``mask_coef``
     (scale/shift rows of ``coef``), so ``y`` is never read.  ``y_mask`` is the
     1-bit-per-channel ReLU mask written by :func:`bn_apply_stats` (``mask_out``)
-    for block outputs with a residual: 1/16 of the bytes of ``y``."""
+    for block outputs with a residual: 1/16 of the bytes of ``y``.  ``x2``/``sums2``
+    add the sums of a second BN fed by the same dz (the downsample shortcut's
+    input ``cs``), so dz is not read back for it."""
     c = x.shape[-1]
     rows = x.numel() // c
     assert (y is not None) + (mask_coef is not None) + (y_mask is not None) <= 1
+    assert (x2 is None) == (sums2 is None) and (x2 is None or x2.shape == x.shape)
     if y_mask is not None:
         assert y_mask.dtype == torch.uint8 and y_mask.numel() * 8 == x.numel() and y_mask.is_contiguous()
     N.call("sl_bn_bwd_reduce", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x),
            _f32(mask_coef) if mask_coef is not None else None, p(y_mask) if y_mask is not None else None,
-           _bf16(dz_out) if dz_out is not None else None, _f32(sums), rows, c, N.stream_ptr())
+           _bf16(dz_out) if dz_out is not None else None, _f32(sums),
+           _bf16(x2) if x2 is not None else None, _f32(sums2) if sums2 is not None else None, rows, c,
+           N.stream_ptr())
 
 
 def bn_bwd_finalize(sums, coef, dcoef, grad_gamma, grad_beta, count):

@@ -210,6 +210,20 @@ def test_bn_residual_relu_bitmask():
     assert torch.equal(outs[0][0], outs[1][0])
     assert rel(outs[1][1], outs[0][1]) < 1e-5
 
+    # a second BN fed by the same dz (downsample shortcut) summed in the same pass
+    cs = bf(torch.randn_like(x.float()))
+    sbuf, sbuf2, sbuf_ref = (torch.zeros(K.rsum_floats(2 * c), device=DEV) for _ in range(3))
+    dz = torch.empty_like(x)
+    K.bn_bwd_reduce(dy, None, x, sbuf, dz_out=dz, y_mask=m, x2=cs, sums2=sbuf2)
+    K.bn_bwd_reduce(outs[0][0], None, cs, sbuf_ref)
+    torch.cuda.synchronize()
+    assert torch.equal(dz, outs[0][0])
+    assert rel(K.rsum_result(sbuf, 2 * c), outs[0][1]) < 1e-5
+    assert rel(K.rsum_result(sbuf2, 2 * c), K.rsum_result(sbuf_ref, 2 * c)) < 1e-5
+    dzf = outs[0][0].float().reshape(-1, c)
+    ref2 = torch.cat([dzf.sum(0), (dzf * cs.float().reshape(-1, c)).sum(0)])
+    assert rel(K.rsum_result(sbuf2, 2 * c), ref2) < 1e-4
+
 
 def test_bn_forward_backward_matches_torch():
     from serverless_learn_amd.ops import cnn as K
