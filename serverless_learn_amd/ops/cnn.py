@@ -9,6 +9,8 @@ from __future__ import annotations
 
 import ctypes
 
+import os
+
 import torch
 
 from . import _native as N
@@ -91,13 +93,18 @@ def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None):
            _bf16(add) if add is not None else None, N.stream_ptr())
 
 
-def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: int = 1024):
+# split-K target for the implicit-GEMM weight gradient (workgroups per launch);
+# SL_WGRAD_WGS overrides it for A/B runs
+_WGRAD_WGS = int(os.environ.get("SL_WGRAD_WGS", "768"))  # swept 512..2048, profiles/r01_v16
+
+
+def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: int = 0):
     """dw [cout, k*k*C] fp32 += sum over pixels dy^T im2col(x)."""
     n, h, wd, c = x.shape
     _, oh, ow, ldy = dy.shape
     assert dw.dtype == torch.float32 and dw.numel() >= cout * k * k * c
     N.call("sl_conv_wgrad", _bf16(x), n, h, wd, c, _bf16(dy), ldy, cout, k, k, stride, pad, oh, ow, p(dw),
-           int(target_wgs), N.stream_ptr())
+           int(target_wgs or _WGRAD_WGS), N.stream_ptr())
 
 
 class WtDesc(ctypes.Structure):
