@@ -687,13 +687,25 @@ static int fill_geom(ConvGeom& g, const uint16_t* src, int N, int SH, int SW, in
   return 0;
 }
 
+// 128-row tiles are used while they give at least this many workgroups;
+// SL_GEMM_SMALLM overrides it for A/B runs.
+static int gemm_smallm_tiles() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SL_GEMM_SMALLM");
+    v = e ? atoi(e) : 512;  // swept 256..4096 on MI355X: profiles/r01_v16 (1024 was 4 % slower)
+    if (v < 1) v = 512;
+  }
+  return v;
+}
+
 template <bool T>
 static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) {
   const bool small_n = e.ncols <= 64;
-  // two workgroups per CU: prefer 128-row tiles while they still give >= 2
-  // rounds of workgroups over the 512 slots
+  // prefer 128-row tiles while they still fill the 512 two-per-CU slots once
+  // (ResNet-18 stage 4: 512 128x128 tiles beat 1024 64x128 tiles)
   const int tn128 = (e.ncols + (small_n ? 63 : 127)) / (small_n ? 64 : 128);
-  const bool small_m = (long)((g.M + 127) / 128) * tn128 < 1024;
+  const bool small_m = (long)((g.M + 127) / 128) * tn128 < gemm_smallm_tiles();
   const int BMv = small_m ? 64 : 128, BNv = small_n ? 64 : 128;
   const int tiles_m = (g.M + BMv - 1) / BMv, tiles_n = (e.ncols + BNv - 1) / BNv;
   dim3 grid(tiles_m * tiles_n), block(256);
