@@ -388,6 +388,66 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_sums_kernel(const uint16_t* 
   }
 }
 
+// One BN of a pair fed by the same dz (bn_bwd_apply_dual_kernel).
+struct BnBwdSide {
+  const uint16_t* x;
+  const float* sums;
+  const float* coef;
+  float* grad_gamma;
+  float* grad_beta;
+  uint16_t* dx;
+};
+
+__device__ __forceinline__ void bn_bwd_abc8(const BnBwdSide& b, int C, int c0, float count, float (&ca)[8],
+                                            float (&cb)[8], float (&cc)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const float s0 = b.sums[c], s1 = b.sums[C + c];
+    const float sc = b.coef[c], mean = b.coef[2 * C + c], rstd = b.coef[3 * C + c];
+    const float sdxh = rstd * (s1 - mean * s0);
+    ca[j] = sc;
+    cb[j] = -sc * rstd * sdxh / count;
+    cc[j] = -sc * s0 / count - cb[j] * mean;
+  }
+}
+
+// bn_bwd_apply_sums for the two BNs of a downsample block (bn2 on c2, the
+// shortcut's BN on cs), which share dz: dz is read once for both dx outputs.
+__global__ __launch_bounds__(256) void bn_bwd_apply_dual_kernel(const uint16_t* __restrict__ dz, BnBwdSide a,
+                                                                BnBwdSide b, long rows, int C, float count) {
+  const int cpr = C >> 3;
+  const long total = rows * cpr;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(t0 % cpr) * 8;
+  float aa[8], ab[8], ac[8], ba[8], bb[8], bc[8];
+  bn_bwd_abc8(a, C, c0, count, aa, ab, ac);
+  bn_bwd_abc8(b, C, c0, count, ba, bb, bc);
+  for (long q = t0; q < total; q += (long)gridDim.x * blockDim.x) {
+    float g[8], xa[8], xb[8], oa[8], ob[8];
+    unpack8(ld8(dz + q * 8), g);
+    unpack8(ld8(a.x + q * 8), xa);
+    unpack8(ld8(b.x + q * 8), xb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      oa[j] = aa[j] * g[j] + ab[j] * xa[j] + ac[j];
+      ob[j] = ba[j] * g[j] + bb[j] * xb[j] + bc[j];
+    }
+    *reinterpret_cast<short8_t*>(a.dx + q * 8) = pack8(oa);
+    *reinterpret_cast<short8_t*>(b.dx + q * 8) = pack8(ob);
+  }
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+      const BnBwdSide& s = c < C ? a : b;
+      const int k = c < C ? c : c - C;
+      const float s0 = s.sums[k], s1 = s.sums[C + k];
+      const float mean = s.coef[2 * C + k], rstd = s.coef[3 * C + k];
+      if (s.grad_gamma) s.grad_gamma[k] += rstd * (s1 - mean * s0);
+      if (s.grad_beta) s.grad_beta[k] += s0;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Max pool (KxK, stride s, pad p) with a per-output argmax tap (u8) for backward.
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
@@ -640,6 +700,19 @@ int sl_bn_apply_stats(const uint16_t* x, const float* stats, const float* gamma,
   BnStats rb{rstats, rgamma, rbeta, rcoef, rrun_mean, rrun_var};
   hipLaunchKernelGGL(bn_apply_stats_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0, stream, x, b, res, rb, y,
                      mask_out, rows, C, relu, mode, count, eps, momentum);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_bn_bwd_apply_dual(const uint16_t* dz, const uint16_t* xa, const float* sums_a, const float* coef_a,
+                         float* gg_a, float* gb_a, uint16_t* dx_a, const uint16_t* xb, const float* sums_b,
+                         const float* coef_b, float* gg_b, float* gb_b, uint16_t* dx_b, long rows, int C,
+                         float count, hipStream_t stream) {
+  if ((C & 7) || 256 % (C / 8) != 0) return -1;
+  BnBwdSide a{xa, sums_a, coef_a, gg_a, gb_a, dx_a};
+  BnBwdSide b{xb, sums_b, coef_b, gg_b, gb_b, dx_b};
+  hipLaunchKernelGGL(bn_bwd_apply_dual_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0,
+                     stream, dz, a, b, rows, C, count);
   SL_CHECK_LAUNCH();
   return 0;
 }

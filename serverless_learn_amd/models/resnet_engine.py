@@ -261,11 +261,14 @@ class FusedResNetTrainer:
             add = st["dz"]
             if down:
                 cd = self.conv[blk.down.name]
-                K.bn_bwd_apply_sums(st["dz"], None, st["cs"], bd.sums, bd.coef, bd.ggamma, bd.gbeta, st["dcs"])
+                # dc2 and dcs from one read of dz
+                K.bn_bwd_apply_dual(st["dz"], st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"],
+                                    st["cs"], bd.sums, bd.coef, bd.ggamma, bd.gbeta, st["dcs"])
                 K.conv_wgrad(st["x"], st["dcs"], blk.down.cout, 1, blk.down.stride, 0, cd.g)
                 K.conv_dgrad(st["dcs"], cd.wt, blk.down.cin, 1, blk.down.stride, 0, st["dxs"])
                 add = st["dxs"]
-            K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
+            else:
+                K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
             K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g)
             K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"])
             # a1 = relu(bn1(c1)): the mask is re-derived from c1 and bn1's coefficients

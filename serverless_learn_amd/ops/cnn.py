@@ -33,6 +33,7 @@ N.register("sl_rsum_floats", [I], ctypes.c_long)
 N.register("sl_rsum_result_offset", [I], ctypes.c_long)
 N.register("sl_bn_apply_stats", [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, F, F, F, P])
 N.register("sl_bn_bwd_apply_sums", [P, P, P, P, P, P, P, P, P, L, I, F, P])
+N.register("sl_bn_bwd_apply_dual", [P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, F, P])
 N.register("sl_maxpool_fwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_maxpool_bwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_avgpool_fwd", [P, P, I, I, I, P])
@@ -221,6 +222,17 @@ def bn_bwd_apply_sums(dy, y, x, sums, coef, grad_gamma, grad_beta, dx, mask_coef
     N.call("sl_bn_bwd_apply_sums", _bf16(dy), _bf16(y) if y is not None else None, _bf16(x),
            _f32(mask_coef) if mask_coef is not None else None, _f32(sums),
            _f32(coef), _f32(grad_gamma), _f32(grad_beta), _bf16(dx), rows, c, float(rows), N.stream_ptr())
+
+
+def bn_bwd_apply_dual(dz, xa, sums_a, coef_a, gg_a, gb_a, dx_a, xb, sums_b, coef_b, gg_b, gb_b, dx_b):
+    """:func:`bn_bwd_apply_sums` for two BNs fed by the same ``dz`` (a downsample
+    block's bn2 and shortcut BN), reading ``dz`` once."""
+    c = xa.shape[-1]
+    rows = xa.numel() // c
+    assert xb.shape == xa.shape == dz.shape == dx_a.shape == dx_b.shape
+    N.call("sl_bn_bwd_apply_dual", _bf16(dz), _bf16(xa), _f32(sums_a), _f32(coef_a), _f32(gg_a), _f32(gb_a),
+           _bf16(dx_a), _bf16(xb), _f32(sums_b), _f32(coef_b), _f32(gg_b), _f32(gb_b), _bf16(dx_b), rows, c,
+           float(rows), N.stream_ptr())
 
 
 def maxpool_fwd(x, y, arg, k=3, s=2, pad=1):

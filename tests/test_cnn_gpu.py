@@ -225,6 +225,36 @@ def test_bn_residual_relu_bitmask():
     assert rel(K.rsum_result(sbuf2, 2 * c), ref2) < 1e-4
 
 
+def test_bn_bwd_apply_dual_matches_two_applies():
+    """One pass over dz for a downsample block's two BNs == two bn_bwd_apply_sums."""
+    from serverless_learn_amd.ops import cnn as K
+
+    torch.manual_seed(7)
+    n, h, c = 4, 8, 256
+    dz = bf(torch.randn(n, h, h, c, device=DEV))
+    xs = [bf(torch.randn(n, h, h, c, device=DEV) + 0.2) for _ in range(2)]
+    sums = [torch.randn(2 * c, device=DEV) * 10 for _ in range(2)]
+    coefs = []
+    for _ in range(2):
+        cf = torch.zeros(4 * c, device=DEV)
+        cf[:c] = torch.rand(c, device=DEV) + 0.5
+        cf[c:2 * c] = torch.randn(c, device=DEV)
+        cf[2 * c:3 * c] = torch.randn(c, device=DEV) * 0.1
+        cf[3 * c:] = torch.rand(c, device=DEV) + 0.5
+        coefs.append(cf)
+    ref, got = [], []
+    for i in range(2):
+        gg, gb, dx = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV), torch.empty_like(dz)
+        K.bn_bwd_apply_sums(dz, None, xs[i], sums[i], coefs[i], gg, gb, dx)
+        ref.append((dx, gg, gb))
+        got.append((torch.empty_like(dz), torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)))
+    K.bn_bwd_apply_dual(dz, xs[0], sums[0], coefs[0], got[0][1], got[0][2], got[0][0],
+                        xs[1], sums[1], coefs[1], got[1][1], got[1][2], got[1][0])
+    torch.cuda.synchronize()
+    for (dx, gg, gb), (dx2, gg2, gb2) in zip(ref, got):
+        assert rel(dx2, dx) < 1e-3 and torch.allclose(gg2, gg) and torch.allclose(gb2, gb)
+
+
 def test_bn_forward_backward_matches_torch():
     from serverless_learn_amd.ops import cnn as K
 
