@@ -129,7 +129,7 @@ PYBIND11_MODULE(_slcore, m) {
       .def(py::init<>())
       .def("register_birth", &Registry::register_birth, py::arg("addr"), py::arg("hostname") = "",
            py::arg("num_gpus") = 0, py::arg("incarnation") = 0, py::arg("now") = 0.0)
-      .def("deregister", &Registry::deregister)
+      .def("deregister", &Registry::deregister, py::arg("addr"), py::arg("incarnation") = 0)
       .def("heartbeat_ok", &Registry::heartbeat_ok)
       .def("heartbeat_fail", &Registry::heartbeat_fail)
       .def("evict_stale", &Registry::evict_stale)

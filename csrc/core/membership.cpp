@@ -33,9 +33,12 @@ std::pair<uint64_t, bool> Registry::register_birth(const std::string& addr, cons
   return {++epoch_, true};
 }
 
-bool Registry::deregister(const std::string& addr) {
+bool Registry::deregister(const std::string& addr, uint64_t incarnation) {
   std::lock_guard<std::mutex> g(mu_);
-  if (members_.erase(addr) == 0) return false;
+  auto it = members_.find(addr);
+  if (it == members_.end()) return false;
+  if (incarnation != 0 && it->second.incarnation != incarnation) return false;
+  members_.erase(it);
   ++epoch_;
   return true;
 }

@@ -36,8 +36,9 @@ class Registry {
   // Returns (epoch after the call, whether membership changed).
   std::pair<uint64_t, bool> register_birth(const std::string& addr, const std::string& hostname,
                                            uint32_t num_gpus, uint64_t incarnation, double now);
-  // Graceful leave. Returns true if the member existed.
-  bool deregister(const std::string& addr);
+  // Graceful leave. Returns true if the member existed. A non-zero `incarnation` must match the
+  // registered one, so a late leave from a dead process cannot remove its successor at the same address.
+  bool deregister(const std::string& addr, uint64_t incarnation = 0);
   void heartbeat_ok(const std::string& addr, double now);
   // A failed heartbeat; evicts after `max_misses` consecutive misses. Returns true if evicted.
   bool heartbeat_fail(const std::string& addr, int max_misses);

@@ -24,6 +24,24 @@ __global__ __launch_bounds__(256) void gossip_apply_kernel(float* __restrict__ m
   }
 }
 
+// K7b -- client-side absorb of a reply r while training may have advanced m during the RPC:
+//     m += alpha * r
+//     o += sent + alpha * r   (sent = the delta this client put on the wire; absent if a
+//                              server-side exchange reset o in the meantime)
+// so o advances by exactly what was shared and steps taken during the RPC stay unshared.
+__global__ __launch_bounds__(256) void gossip_absorb_kernel(float* __restrict__ m, float* __restrict__ o,
+                                                            const double* __restrict__ r, long kr, double alpha,
+                                                            const double* __restrict__ sent, long ks, long n) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double ar = (i < kr) ? alpha * r[i] : 0.0;
+    double oi = (double)o[i];
+    if (sent && i < ks) oi += sent[i];
+    m[i] = (float)((double)m[i] + ar);
+    o[i] = (float)(oi + ar);
+  }
+}
+
 // K5 -- flat fused SGD over a whole model's parameter vector (one launch for
 // every tensor): torch.optim.SGD semantics (dampening 0, no nesterov), with
 // optional momentum buffer and optional bf16 shadow copy for the GEMM kernels.
@@ -86,6 +104,15 @@ int sl_gossip_apply(float* m, float* o, const double* din, long kin, double alph
   if (n <= 0) return 0;
   if (kin > n) return -1;
   hipLaunchKernelGGL(gossip_apply_kernel, dim3(grid_for(n, 1)), dim3(256), 0, stream, m, o, din, kin, alpha, dout, n);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_gossip_absorb(float* m, float* o, const double* r, long kr, double alpha, const double* sent, long ks,
+                     long n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (kr > n || ks > n) return -1;
+  hipLaunchKernelGGL(gossip_absorb_kernel, dim3(grid_for(n, 1)), dim3(256), 0, stream, m, o, r, kr, alpha, sent, ks, n);
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -44,6 +44,8 @@ class GossipState:
         self.compat = compat
         self.lock = threading.RLock()
         self.exchanges = 0
+        self.serves = 0  # server-side exchanges (each sets o = m)
+        self._serves_at_send = 0
 
     # -- helpers -------------------------------------------------------------
     def _grow(self, n: int) -> None:
@@ -64,29 +66,48 @@ class GossipState:
 
     # -- client side -----------------------------------------------------------
     def make_delta(self) -> np.ndarray:
-        """d = m - o (float64, as it goes on the wire)."""
+        """d = m - o (float64, as it goes on the wire).
+
+        Remembers how many server-side exchanges had happened, so ``absorb`` can
+        tell whether ``o`` moved while the RPC was in flight."""
         with self.lock:
+            self._serves_at_send = self.serves
             return (self.model.double() - self.old.double()).cpu().numpy()
 
     def absorb(self, reply: np.ndarray, sent: np.ndarray) -> None:
-        """Apply the peer's reply; then o = m (worker.cc:155-164, :215)."""
+        """Apply the peer's reply (worker.cc:155-164) and advance ``o``.
+
+        The reference then sets ``o = m`` (:215).  Training keeps stepping while the
+        RPC is in flight, so ``m`` already holds progress that was never sent; copying
+        it into ``o`` would drop it from every later exchange.  ``o`` instead advances
+        by exactly what was shared: ``o += sent + a*r``.  If this worker served an
+        exchange in the meantime, that serve already set ``o = m`` (its reply carried
+        everything, ``sent`` included), so only ``a*r`` is added.  With no concurrent
+        steps both rules give ``o = m``, so the exchange math of SURVEY.md §3.4 is
+        unchanged."""
         with self.lock:
             r = torch.from_numpy(np.asarray(reply, dtype=np.float64))
             self._grow(r.numel())
             a = self.alpha
-            if not self.compat:
-                s = torch.from_numpy(np.asarray(sent, dtype=np.float64))
-                if s.numel() == r.numel():
-                    r = r - a * s  # remove the echo of our own delta: a*(r - a*d) = a*dB
+            s = torch.from_numpy(np.asarray(sent, dtype=np.float64))
+            if not self.compat and s.numel() == r.numel():
+                r = r - a * s  # remove the echo of our own delta: a*(r - a*d) = a*dB
+            if self.serves != self._serves_at_send or s.numel() > self.model.numel():
+                s = None  # o was reset by a serve in between: `sent` is already accounted for
             if self._use_kernel():
                 from ..ops import gossip as gk
 
-                gk.delta_apply(self.model, self.old, r.to(self.model.device), a, None)
+                gk.absorb(self.model, self.old, r.to(self.model.device), a,
+                          None if s is None else s.to(self.model.device))
             else:
                 n = r.numel()
                 m = self.model[:n]
                 m.copy_((m.double() + a * r).to(m.dtype))
-                self.old.copy_(self.model)
+                o = self.old.double()
+                if s is not None:
+                    o[:s.numel()] += s
+                o[:n] += a * r
+                self.old.copy_(o.to(self.old.dtype))
             self.exchanges += 1
 
     # -- server side -----------------------------------------------------------
@@ -108,6 +129,7 @@ class GossipState:
                 m[:n].copy_((m[:n].double() + a * d).to(m.dtype))
                 reply = (m.double() - self.old.double()).numpy()
                 self.old.copy_(m)
+            self.serves += 1
             self.exchanges += 1
             return reply
 

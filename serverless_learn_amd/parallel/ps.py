@@ -8,6 +8,17 @@ master-side broadcast loop ``periodically_send_updates`` (:268-293) is never
 started.  Here it is reachable: workers running ``--sync ps`` call it every
 gossip interval, and the master can optionally broadcast its own progress to a
 random worker (``broadcast_once``), which is what the dead loop intended.
+
+One shared ``old`` (the reference's rule, ``per_client=False``) makes every
+reply exactly ``alpha*d`` -- the caller's own delta echoed back, because ``o``
+was set to ``m`` by whichever exchange came last.  An echo-free client removes
+that echo and is left with nothing, so no model ever learns from another.
+The default therefore keeps one ``old`` *per client*: the reply is everything
+the PS model gained since that client's previous exchange (the other clients'
+``alpha``-scaled deltas plus its own ``alpha*d``), which the echo-free client
+turns into ``alpha * (others' progress)``.  Without concurrent clients and with
+a single client the two rules are identical.
+
 The model lives in float64 (the wire type) and is guarded by a lock (the
 reference mutates it from handler threads unlocked).
 """
@@ -17,45 +28,78 @@ import threading
 
 import numpy as np
 
+# gRPC metadata key a worker sets to name itself on Master.ExchangeUpdates
+PS_CLIENT_MD = "sl-client"
+
+
+def _grown(v: np.ndarray, n: int) -> np.ndarray:
+    return v if v.size >= n else np.concatenate([v, np.zeros(n - v.size)])
+
 
 class ParameterServer:
-    def __init__(self, alpha: float = 0.5):
+    def __init__(self, alpha: float = 0.5, per_client: bool = True):
         self.alpha = float(alpha)
+        self.per_client = per_client
         self.model = np.zeros(0, np.float64)
-        self.old = np.zeros(0, np.float64)
+        self.old = np.zeros(0, np.float64)          # the reference's single old_state
+        self.olds: dict[str, np.ndarray] = {}       # per-client: PS model at that client's last exchange
+        self.base = np.zeros(0, np.float64)         # what a client that never exchanged has seen
         self.lock = threading.Lock()
         self.exchanges = 0
 
     def _grow(self, n: int) -> None:
-        k = self.model.size
-        if n > k:
-            self.model = np.concatenate([self.model, np.zeros(n - k)])
-            self.old = np.concatenate([self.old, np.zeros(n - k)])
+        self.model = _grown(self.model, n)
+        self.old = _grown(self.old, n)
 
-    def exchange(self, delta: np.ndarray) -> np.ndarray:
+    def _old_for(self, client: str | None) -> np.ndarray:
+        if not self.per_client or client is None:
+            return self.old
+        o = self.olds.get(client)
+        # a new client has seen nothing yet: everything the PS holds is news to it
+        o = _grown(self.base.copy() if o is None else o, self.model.size)
+        self.olds[client] = o
+        return o
+
+    def _set_old(self, client: str | None) -> None:
+        if not self.per_client or client is None:
+            self.old = self.model.copy()
+        else:
+            self.olds[client] = self.model.copy()
+
+    def exchange(self, delta: np.ndarray, client: str | None = None) -> np.ndarray:
+        """m += alpha*d; reply m - o[client]; o[client] = m (master.cc:95-114)."""
         with self.lock:
             d = np.asarray(delta, np.float64)
             self._grow(d.size)
             self.model[:d.size] += self.alpha * d
-            reply = self.model - self.old
-            self.old = self.model.copy()
+            reply = self.model - self._old_for(client)
+            self._set_old(client)
             self.exchanges += 1
             return reply
 
-    def pending_delta(self) -> np.ndarray:
+    def pending_delta(self, client: str | None = None) -> np.ndarray:
         """m - o: what the master would send in a broadcast (master.cc:276-282)."""
         with self.lock:
-            return self.model - self.old
+            return self.model - self._old_for(client)
 
-    def absorb_reply(self, reply: np.ndarray) -> None:
-        """Client-side mixing of a worker's reply to a master broadcast; then o = m."""
+    def absorb_reply(self, reply: np.ndarray, sent: np.ndarray | None = None, client: str | None = None) -> None:
+        """Master-side mixing of a worker's reply to a broadcast; then o[client] = m.
+
+        With ``sent`` given (echo-free), the echo ``alpha*sent`` is removed first, as the
+        worker-side client does (parallel/gossip.py)."""
         with self.lock:
             r = np.asarray(reply, np.float64)
             self._grow(r.size)
+            if sent is not None and self.per_client:
+                s = np.asarray(sent, np.float64)
+                r = r.copy()
+                r[:s.size] -= self.alpha * s
             self.model[:r.size] += self.alpha * r
-            self.old = self.model.copy()
+            self._set_old(client)
 
     def set_model(self, flat: np.ndarray) -> None:
         with self.lock:
             self.model = np.asarray(flat, np.float64).copy()
             self.old = self.model.copy()
+            self.base = self.model.copy()
+            self.olds.clear()

@@ -33,12 +33,12 @@ from concurrent import futures
 from .._core import core
 from ..ckpt.format import CKPT_BASE
 from ..config import Config
-from ..parallel.ps import ParameterServer
+from ..parallel.ps import PS_CLIENT_MD, ParameterServer
 from ..proto import messages as pb
 from ..utils.log import Logger
 from ..utils.metrics import Metrics
 from ..wire.codec import decode_update, encode_update
-from .transport import Channels, RpcFailure, RpcServer
+from .transport import Channels, RpcFailure, RpcServer, metadata_dict
 
 
 def _free_port() -> int:
@@ -57,7 +57,7 @@ class Master:
         self.metrics = Metrics("master")
         self.log = Logger("master", self.addr_requested, self.metrics)
         self.registry = core().Registry()
-        self.ps = ParameterServer(self.cfg.learn_rate)
+        self.ps = ParameterServer(self.cfg.learn_rate, per_client=not self.cfg.gossip_compat)
         self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
         self._lock = threading.Lock()
         self.incarnation: dict[str, int] = {}
@@ -97,10 +97,11 @@ class Master:
 
     def _deregister(self, request: bytes, context) -> bytes:
         info = pb.WorkerBirthInfo.FromString(request)
-        existed = self.registry.deregister(info.addr)
-        with self._lock:
-            self.delivered.pop(info.addr, None)
-            self.ckpt_delivered.pop(info.addr, None)
+        existed = self.registry.deregister(info.addr, info.incarnation)
+        if existed:
+            with self._lock:
+                self.delivered.pop(info.addr, None)
+                self.ckpt_delivered.pop(info.addr, None)
         self.log.info("deregister", worker=info.addr, existed=existed, epoch=self.registry.epoch(),
                       world=len(self.registry.members()))
         if existed:
@@ -122,7 +123,11 @@ class Master:
     # ---- parameter server ----------------------------------------------------
     def _exchange_updates(self, request: bytes, context) -> bytes:
         delta = decode_update(request, "float64")
-        reply = self.ps.exchange(delta)
+        # Each client's exchanges are tracked separately (ParameterServer docstring); the
+        # reference's Update carries no sender, so workers name themselves in metadata and a
+        # reference-style client falls back to its connection's peer string.
+        client = metadata_dict(context).get(PS_CLIENT_MD) or context.peer()
+        reply = self.ps.exchange(delta, client)
         return encode_update(reply)
 
     def broadcast_once(self) -> bool:
@@ -131,13 +136,13 @@ class Master:
         if not members:
             return False
         target = random.choice(members)
-        delta = self.ps.pending_delta()
+        delta = self.ps.pending_delta(target)
         try:
             raw = self.channels.unary(target, "Worker", "ExchangeUpdates", encode_update(delta))
         except RpcFailure as e:
             self.log.warn("ps_broadcast_failed", to=target, error=str(e))
             return False
-        self.ps.absorb_reply(decode_update(raw, "float64"))
+        self.ps.absorb_reply(decode_update(raw, "float64"), delta, target)
         return True
 
     # ---- heartbeats / failure detection --------------------------------------

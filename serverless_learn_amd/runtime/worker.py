@@ -42,6 +42,7 @@ from ..data.synthetic import HEADER_SIZE, MAGIC as SHARD_MAGIC, decode_header
 from ..models import make_trainer
 from ..parallel.dp import ElasticGroup, GroupBroken
 from ..parallel.gossip import GossipState
+from ..parallel.ps import PS_CLIENT_MD
 from ..proto import messages as pb
 from ..utils import trace
 from ..utils.fault import FaultInjector
@@ -88,6 +89,7 @@ class Worker:
         self.files_received: list[int] = []
         self.state = "idle"
         self.registered = threading.Event()
+        self._last_checkup = time.monotonic()
         self.has_data = threading.Event()
         self._pending_shard = None
         self._stop = threading.Event()
@@ -161,13 +163,27 @@ class Worker:
             except Exception as e:
                 self.log.warn("ingest_failed", file_num=file_num, error=repr(e))
                 return pb.ReceiveFileAck(ok=False).SerializeToString()
+        if size > 0 and got != size:
+            # a stream that ended early (sender died, deadline): the tail of the buffer is
+            # uninitialised -- never train on it or ack it
+            self.log.warn("ingest_short", file_num=file_num, announced=size, got=int(got))
+            return pb.ReceiveFileAck(ok=False).SerializeToString()
+        hdr = None
+        if is_shard:
+            try:
+                hdr = decode_header(head)
+                n, d = hdr["n"], hdr["height"] * hdr["width"] * hdr["channels"]
+            except Exception as e:
+                self.log.warn("ingest_bad_header", file_num=file_num, error=repr(e))
+                return pb.ReceiveFileAck(ok=False).SerializeToString()
+            if n <= 0 or d <= 0 or HEADER_SIZE + n * d + n > got:
+                self.log.warn("ingest_bad_header", file_num=file_num, n=n, d=d, got=int(got))
+                return pb.ReceiveFileAck(ok=False).SerializeToString()
         dt = time.perf_counter() - t0
         self.bytes_ingested += got
         self.files_received.append(file_num)
         kind = "data"
         if is_shard:
-            hdr = decode_header(head)
-            n, d = hdr["n"], hdr["height"] * hdr["width"] * hdr["channels"]
             if isinstance(buf, np.ndarray):
                 buf = torch.from_numpy(buf)
             x = buf[HEADER_SIZE:HEADER_SIZE + n * d].view(n, d)
@@ -186,6 +202,7 @@ class Worker:
 
     def _check_up(self, request: bytes, context) -> bytes:
         pl = pb.PeerList.FromString(request)
+        self._last_checkup = time.monotonic()
         with self.view_lock:
             self.view = {"epoch": pl.epoch, "peers": list(pl.peer_addrs), "rank": pl.rank,
                          "world": pl.world_size, "rendezvous": pl.rendezvous, "resume_file": pl.resume_file}
@@ -250,21 +267,46 @@ class Worker:
         return file_num
 
     # ---- loops -------------------------------------------------------------------
-    def _register_loop(self) -> None:
-        delay = 0.1
+    def _register_once(self) -> bool:
         info = pb.WorkerBirthInfo(addr=self.addr, num_gpus=1 if self.device.type == "cuda" else 0,
                                   hostname=socket.gethostname(), incarnation=self.incarnation)
+        raw = self.channels.unary(self.cfg.master_addr, "Master", "RegisterBirth", info.SerializeToString())
+        return pb.RegisterBirthAck.FromString(raw).ok
+
+    def _register_loop(self) -> None:
+        """Register with retry/backoff, then keep watching the master's view of us.
+
+        The reference registers once and never again (worker.cc:249-252).  Here a worker
+        the master evicted (missed CheckUps during a network blip or a long stall) notices
+        -- CheckUps stop for longer than the eviction window, or a PeerList arrives that no
+        longer lists it -- and registers again (same incarnation: it is the same process,
+        so the master treats it as a fresh join and bumps the epoch)."""
+        delay = 0.1
+        silence = max(2.0, self.cfg.max_misses * self.cfg.checkup_interval * 2.0 + self.cfg.rpc_timeout_s)
         while not self._stop.is_set():
-            try:
-                raw = self.channels.unary(self.cfg.master_addr, "Master", "RegisterBirth", info.SerializeToString())
-                if pb.RegisterBirthAck.FromString(raw).ok:
-                    self.registered.set()
-                    self.log.info("registered", master=self.cfg.master_addr)
-                    return
-            except RpcFailure as e:
-                self.log.warn("register_retry", error=e.code.name if e.code else "", delay=delay)
-            self._stop.wait(delay)
-            delay = min(delay * 2, 5.0)
+            if not self.registered.is_set():
+                try:
+                    if self._register_once():
+                        self._last_checkup = time.monotonic()
+                        self.registered.set()
+                        self.log.info("registered", master=self.cfg.master_addr)
+                        delay = 0.1
+                        continue
+                except RpcFailure as e:
+                    self.log.warn("register_retry", error=e.code.name if e.code else "", delay=delay)
+                self._stop.wait(delay)
+                delay = min(delay * 2, 5.0)
+                continue
+            self._stop.wait(min(1.0, silence / 4))
+            with self.view_lock:
+                dropped = self.view["epoch"] > 0 and self.view["rank"] < 0
+            quiet = time.monotonic() - self._last_checkup > silence
+            if dropped or quiet:
+                self.log.warn("reregister", reason="not_in_peer_list" if dropped else "no_checkups",
+                              silent_s=round(time.monotonic() - self._last_checkup, 2))
+                with self.view_lock:
+                    self.view = dict(self.view, epoch=0, rank=-1)
+                self.registered.clear()
 
     def _maybe_regroup(self) -> None:
         with self.view_lock:
@@ -279,22 +321,39 @@ class Worker:
             if not ok:
                 self._stop.wait(0.2)
                 return
-            self._set_world(max(1, v["world"]))
-            if self.trainer is not None and self.group.active:
-                t = self.trainer
-                try:
-                    self.group.sync_state([t.params, t.mom])
-                    step = torch.tensor([self.step], dtype=torch.int64, device=t.params.device)
-                    self.group.broadcast_(step, 0)
-                    self.step = int(step.item())
-                except GroupBroken as e:
-                    self.log.warn("state_sync_failed", error=str(e))
-                    return
-                self._after_external_update()
-                t.allreduce = self.group.allreduce_
-            elif self.trainer is not None:
-                self.trainer.allreduce = None
+            if self.group.active:
+                # Every member must take part in the state broadcast, so a member whose
+                # first shard has not arrived yet builds its (untrained) trainer now;
+                # the shard is loaded into it later.
+                with self.train_lock:
+                    self._ensure_trainer()
+                    self._set_world(max(1, v["world"]))
+                    t = self.trainer
+                    try:
+                        self.group.sync_state([t.params, t.mom])
+                        step = torch.tensor([self.step], dtype=torch.int64, device=t.params.device)
+                        self.group.broadcast_(step, 0)
+                        self.step = int(step.item())
+                    except GroupBroken as e:
+                        self.log.warn("state_sync_failed", error=str(e))
+                        return
+                    self._after_external_update()
+            else:
+                self._set_world(max(1, v["world"]))
+        self._install_allreduce()
         self.state = "training"
+
+    def _install_allreduce(self) -> None:
+        """Gradient hook follows the group: set whenever a >1 group is live, cleared otherwise.
+
+        Called after every re-form and before every step, so a trainer created after the
+        group formed (first shard arriving late) still reduces its gradients."""
+        if self.trainer is None:
+            return
+        want = self.group.allreduce_ if (self.group.active and self.group.world > 1) else None
+        if self.trainer.allreduce != want:
+            self.trainer.allreduce = want
+            self._set_world(max(1, self.group.world) if want is not None else 1)
 
     def _train_loop(self) -> None:
         if self.cfg.model == "simulate":
@@ -312,6 +371,7 @@ class Worker:
             have_data = self.trainer is not None and self.trainer.x is not None
             if self.cfg.sync == "allreduce":
                 self._maybe_regroup()
+                self._install_allreduce()
                 if self.view["world"] > 1:
                     if not self.group.active:
                         self._stop.wait(0.05)
@@ -381,7 +441,9 @@ class Worker:
             return False
         if self.cfg.sync == "ps":
             target, service = self.cfg.master_addr, "Master"
+            md = ((PS_CLIENT_MD, self.addr),)
         else:
+            md = None
             with self.view_lock:
                 peers = [p for p in self.view["peers"] if p != self.addr]
             if not peers:  # the reference computes rand() % 0 here (worker.cc:200)
@@ -391,7 +453,7 @@ class Worker:
             with self.train_lock:
                 delta = self.gossip.make_delta()
             try:
-                raw = self.channels.unary(target, service, "ExchangeUpdates", encode_update(delta))
+                raw = self.channels.unary(target, service, "ExchangeUpdates", encode_update(delta), metadata=md)
             except RpcFailure as e:  # the reference applies the reply even on failure (worker.cc:153-165)
                 self.log.warn("gossip_failed", peer=target, error=e.code.name if e.code else "")
                 return False

@@ -132,3 +132,36 @@ def test_elastic_kill_two_respawn_two_resume_from_checkpoint():
         assert min(steps) > max(s0), (steps, s0)  # resumed, not restarted from 0
     finally:
         c.stop()
+
+
+def test_ps_workers_exchange_through_master(cluster):
+    a = cluster.add_worker(sync="ps")
+    b = cluster.add_worker(sync="ps")
+    assert cluster.wait_for(lambda: cluster.master.ps.exchanges >= 6 and a.step > 0 and b.step > 0, 60)
+    # the PS tracks each worker's exchanges separately (named by metadata, not the TCP peer)
+    assert {a.addr, b.addr} <= set(cluster.master.ps.olds)
+    assert cluster.master.ps.model.size == a.trainer.n_params
+
+
+def test_evicted_worker_registers_again(cluster, monkeypatch):
+    monkeypatch.setenv("SL_FAULT", "drop:CheckUp:p=0")
+    w = cluster.add_worker(sync="none")
+    assert cluster.wait_for(lambda: w.addr in cluster.master.registry.members() and w.step > 0, 30)
+    epoch = cluster.master.registry.epoch()
+    w.fault.drop["CheckUp"] = 1.0  # heartbeats fail (a network blip): the master evicts it
+    assert cluster.wait_for(lambda: w.addr not in cluster.master.registry.members(), 30)
+    w.fault.drop["CheckUp"] = 0.0
+    assert cluster.wait_for(lambda: w.addr in cluster.master.registry.members(), 30)
+    assert cluster.master.registry.epoch() > epoch + 1
+
+
+def test_allreduce_member_whose_shard_arrives_late_stays_in_lockstep(cluster, monkeypatch):
+    """The group forms before one member has any data: its trainer is built for the
+    state broadcast, the gradient hook is installed, and both replicas stay identical."""
+    a = cluster.add_worker(sync="allreduce", batch=512, max_steps=60)
+    monkeypatch.setenv("SL_FAULT", "delay:ReceiveFile:ms=1500")
+    b = cluster.add_worker(sync="allreduce", batch=512, max_steps=60)
+    monkeypatch.delenv("SL_FAULT")
+    assert cluster.wait_for(lambda: a.state == "done" and b.state == "done", 120), (a.step, b.step, a.state, b.state)
+    assert a.trainer.allreduce is not None and b.trainer.allreduce is not None
+    assert torch.equal(a.trainer.params, b.trainer.params)

@@ -43,3 +43,14 @@ def test_evict_stale_and_assignment():
     r.register_birth("c:1", "h", 0, 3, 10.0)
     assert r.assignment(2) == [("b:1", 0), ("c:1", 1)]
     assert r.assignment(2, 1) == [("b:1", 1), ("c:1", 0)]
+
+
+def test_deregister_checks_incarnation():
+    r = core().Registry()
+    r.register_birth("a:1", incarnation=7)
+    r.register_birth("a:1", incarnation=8)  # the process restarted at the same address
+    e = r.epoch()
+    assert not r.deregister("a:1", 7)  # a late leave from the dead process
+    assert r.members() == ["a:1"] and r.epoch() == e
+    assert r.deregister("a:1", 8)
+    assert r.members() == []

@@ -57,6 +57,28 @@ def test_gossip_echo_free_client_absorb():
     np.testing.assert_allclose(g.model.cpu().numpy(), expect, atol=1e-6)
 
 
+def test_gossip_absorb_kernel_keeps_in_flight_progress():
+    """K7b on device: o advances by exactly what was shared; a step taken during the RPC stays pending."""
+    rng = np.random.default_rng(3)
+    n = 65_537
+    m0 = rng.standard_normal(n).astype(np.float32)
+    g = GossipState(torch.from_numpy(m0).cuda(), 0.5, compat=False)
+    g.model += 1.0
+    sent = g.make_delta()
+    step = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).cuda()
+    g.model += step                                  # training during the RPC
+    reply = rng.standard_normal(n)
+    before_m = g.model.clone()
+    before_o = g.old.clone()
+    g.absorb(reply, sent)
+    r = reply - 0.5 * sent
+    m_ref = (before_m.cpu().double().numpy() + 0.5 * r).astype(np.float32)
+    o_ref = (before_o.cpu().double().numpy() + sent + 0.5 * r).astype(np.float32)
+    np.testing.assert_array_equal(g.model.cpu().numpy(), m_ref)
+    np.testing.assert_array_equal(g.old.cpu().numpy(), o_ref)
+    np.testing.assert_allclose(g.make_delta(), step.cpu().double().numpy(), atol=1e-5)
+
+
 def test_sgd_flat_kernel_matches_torch():
     from serverless_learn_amd.ops.optim import sgd_flat
 

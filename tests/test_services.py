@@ -145,3 +145,27 @@ def test_deadline_expiry_on_hung_peer(ch, monkeypatch):
     finally:
         w.fault.release()
         w.stop(leave=False)
+
+
+def test_receive_file_short_stream_is_rejected(ch):
+    """A stream that ends before the announced size is not acked (nor trained on)."""
+    from serverless_learn_amd.data.synthetic import make_shard
+    from serverless_learn_amd.runtime.file_server import FILE_SIZE_MD
+
+    w = Worker("127.0.0.1:0", fast_config(model="simulate", master_addr="127.0.0.1:1")).start()
+    try:
+        data = bytes(make_shard(256, shard_index=0, num_shards=1, seed=0, dataset="synthetic-mnist"))
+        md = ((FILE_NUM_MD, "0"), (FILE_SIZE_MD, str(len(data))))
+        short = pb.ReceiveFileAck.FromString(ch.stream_unary(w.addr, "Worker", "ReceiveFile",
+                                                             codec.iter_chunks(data[:len(data) // 2]), metadata=md))
+        assert not short.ok and w._pending_shard is None
+        # a header that claims more records than the file holds is rejected too
+        md2 = ((FILE_NUM_MD, "0"), (FILE_SIZE_MD, str(len(data) // 2)))
+        bad = pb.ReceiveFileAck.FromString(ch.stream_unary(w.addr, "Worker", "ReceiveFile",
+                                                           codec.iter_chunks(data[:len(data) // 2]), metadata=md2))
+        assert not bad.ok and w._pending_shard is None
+        full = pb.ReceiveFileAck.FromString(ch.stream_unary(w.addr, "Worker", "ReceiveFile",
+                                                            codec.iter_chunks(data), metadata=md))
+        assert full.ok and w._pending_shard is not None
+    finally:
+        w.stop(leave=False)

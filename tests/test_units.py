@@ -158,3 +158,62 @@ def test_metrics_from_log_events_and_http_exposition():
         assert 'sl_samples_per_second{role="worker"} 1.5e+06' in body
     finally:
         m.close()
+
+
+def test_gossip_absorb_keeps_progress_made_during_the_rpc():
+    """Steps taken while the exchange is in flight stay unshared (sent next time), not lost."""
+    A = GossipState(torch.zeros(6, dtype=torch.float64), alpha=0.5)
+    B = GossipState(torch.zeros(6, dtype=torch.float64), alpha=0.5)
+    A.model += 1.0                    # progress before the exchange
+    d = A.make_delta()
+    A.model += 10.0                   # a training step lands while the RPC is in flight
+    r = B.serve(d)
+    A.absorb(r, d)
+    # the in-flight step is still pending in A's next delta
+    np.testing.assert_allclose(A.make_delta(), 10.0)
+    # the classic o = m rule would have dropped it: A.model - A.old would be 0
+    np.testing.assert_allclose(A.model.numpy(), 11.0)
+
+
+def test_gossip_absorb_after_an_intervening_serve():
+    """A serve that lands during the client's RPC resets o = m; absorb must not re-add `sent`."""
+    A = GossipState(torch.zeros(3, dtype=torch.float64), alpha=0.5)
+    B = GossipState(torch.zeros(3, dtype=torch.float64), alpha=0.5)
+    C = GossipState(torch.zeros(3, dtype=torch.float64), alpha=0.5)
+    A.model += 2.0
+    d = A.make_delta()
+    rC = A.serve(C.make_delta())      # C exchanges with A while A's own RPC to B is in flight
+    np.testing.assert_allclose(rC, 2.0)  # A's progress went to C in that reply
+    r = B.serve(d)
+    A.absorb(r, d)
+    np.testing.assert_allclose(A.make_delta(), 0.0)   # nothing double-counted, nothing pending
+    np.testing.assert_allclose(A.old.numpy(), A.model.numpy())
+
+
+def test_ps_per_client_mixes_models_between_workers():
+    """sync=ps: two workers learn each other's progress through the master's PS."""
+    from serverless_learn_amd.parallel.ps import ParameterServer
+
+    for alpha, share in ((1.0, 1.0), (0.5, 0.25)):
+        ps = ParameterServer(alpha)
+        A = GossipState(torch.zeros(4, dtype=torch.float64), alpha=alpha)
+        B = GossipState(torch.zeros(4, dtype=torch.float64), alpha=alpha)
+        A.model += 3.0
+        B.model -= 5.0
+        for _ in range(2):
+            for name, w in (("A", A), ("B", B)):
+                d = w.make_delta()
+                w.absorb(ps.exchange(d, name), d)
+        # each keeps its own progress and gains alpha^2 (PS alpha, client alpha) of the other's
+        np.testing.assert_allclose(A.model.numpy(), 3.0 + share * -5.0)
+        np.testing.assert_allclose(B.model.numpy(), -5.0 + share * 3.0)
+        np.testing.assert_allclose(ps.model, alpha * (3.0 - 5.0))
+
+
+def test_ps_reference_single_old_echoes_the_callers_delta():
+    """The reference rule (one old_state, master.cc:95-114): every reply is alpha*d."""
+    from serverless_learn_amd.parallel.ps import ParameterServer
+
+    ps = ParameterServer(0.5, per_client=False)
+    np.testing.assert_allclose(ps.exchange(np.full(3, 4.0), "A"), 2.0)
+    np.testing.assert_allclose(ps.exchange(np.full(3, -2.0), "B"), -1.0)
