@@ -60,6 +60,10 @@ def parse(argv=None):
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL over xGMI, the production path); gloo only to rehearse several ranks "
                          "sharing one GPU (RCCL refuses duplicate devices)")
+    ap.add_argument("--allreduce", choices=["auto", "xgmi", "pg"], default="auto",
+                    help="MLP gradient all-reduce for N>1: xgmi = one-shot over IPC-mapped peer buffers fused "
+                         "into the update kernel (hipGraph-capturable); pg = the process group's all-reduce "
+                         "(RCCL); auto = xgmi, falling back to pg if any rank cannot map its peers")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     mlp = a.model == "mlp"
@@ -133,12 +137,26 @@ def main(argv=None) -> int:
 
         tr = FusedResNetTrainer(batch=B, device=dev, lr=args.lr, momentum=args.momentum, world_size=world, seed=0)
         n_params, model_name = tr.spec.n_logical, "resnet18-cifar (11.17M params)"
+    xg = None
+    collective = None
     if world > 1:
         # identical start: broadcast rank 0's weights
         flat = tr.get_flat()
         dist.broadcast(flat, 0)
         tr.set_flat(flat)
-        if mlp:
+        collective = "rccl" if args.dist_backend == "nccl" else "gloo"
+        if mlp and args.allreduce in ("auto", "xgmi"):
+            from serverless_learn_amd.parallel.xgmi import XgmiExchange, dist_collectives
+
+            try:
+                xg = XgmiExchange(tr.n_pad, rank, world, dev, *dist_collectives())
+                tr.enable_xgmi(xg)
+                collective = "xgmi-ipc"
+            except RuntimeError as e:
+                if args.allreduce == "xgmi":
+                    raise
+                print(f"xgmi all-reduce unavailable, using the process group: {e}", file=sys.stderr)
+        if mlp and xg is None:
             tr.allreduce = lambda g: dist.all_reduce(g)
         else:
             tr.bucket_bytes = int(args.bucket_mb * (1 << 20))
@@ -146,7 +164,8 @@ def main(argv=None) -> int:
             tr.bucket_wait = lambda handles: [h.wait() for h in handles]
     tr.load_shard(x, y)
 
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    # the xGMI exchange needs no host sync, so the N>1 MLP step is graph-captured like N=1
+    use_graph = args.graph == "on" or (args.graph == "auto" and (world == 1 or xg is not None))
     warm_eager = min(args.warmup, 3)
     for _ in range(warm_eager):
         tr.step()
@@ -161,20 +180,49 @@ def main(argv=None) -> int:
     first_loss = tr.stats().loss
 
     # ---- 3. timed region ----------------------------------------------------
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def timed() -> float:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(args.steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    def replicas_agree() -> bool:
+        # every replica must hold the same weights after lock-step DP (checks the exchange too)
+        ck = tr.get_flat().double()
+        lo, hi = ck.clone(), ck.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        return bool(torch.equal(lo, hi))
+
+    elapsed = timed()
+    replicas_identical = replicas_agree() if world > 1 else None
+    xgmi_fallback = None
+    if xg is not None:
+        bad = torch.tensor([1.0 if (xg.error() or not replicas_identical) else 0.0], device=dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if bad.item() > 0:
+            # never report a number from a broken exchange: re-sync, switch to the process
+            # group's all-reduce and time the K steps again
+            xgmi_fallback = "barrier timeout" if xg.error() else "replicas diverged"
+            print(f"xgmi exchange failed ({xgmi_fallback}); re-timing with the process group", file=sys.stderr)
+            tr.enable_xgmi(None)
+            flat = tr.get_flat()
+            dist.broadcast(flat, 0)
+            tr.set_flat(flat)
+            tr.allreduce = lambda g: dist.all_reduce(g)
+            use_graph, collective = False, ("rccl" if args.dist_backend == "nccl" else "gloo")
+            run = lambda n: [tr.step() for _ in range(n)]
+            run(3)
+            elapsed = timed()
+            replicas_identical = replicas_agree()
     st = tr.stats()
     global_batch = B * world
     value = global_batch * args.steps / elapsed
@@ -202,7 +250,7 @@ def main(argv=None) -> int:
             "hipgraph": use_graph,
             "steps_per_graph": (args.unroll if mlp else 1) if use_graph else 0,
             "ingest": args.ingest,
-            "collective_backend": ("rccl" if args.dist_backend == "nccl" else "gloo") if world > 1 else None,
+            "collective_backend": collective,
         },
         "baseline_note": "reference publishes no number; vs_baseline is vs its derived data-delivery "
                          "ceiling of 25,478 samples/s/worker (BASELINE.md)",
@@ -210,7 +258,10 @@ def main(argv=None) -> int:
         "train_loss_last": round(st.loss, 4),
         "train_acc_last": round(st.accuracy, 4),
         "ingest_s": round(t_ingest, 3),
+        "replicas_identical": replicas_identical,
     }
+    if xgmi_fallback:
+        out["xgmi_fallback"] = xgmi_fallback
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -218,6 +269,9 @@ def main(argv=None) -> int:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     if world > 1:
+        dist.barrier()
+        if xg is not None:
+            xg.close()
         dist.destroy_process_group()
     return 0
 

@@ -30,6 +30,7 @@
 //           reads) in the same pass; bumps the device batch cursor so the
 //           whole step replays from a hipGraph without host work.
 #include "common.h"
+#include "xgmi.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -1424,6 +1425,10 @@ struct SgdArgs {
   int mode;  // 0: refresh bf16 shadows from w; 1: reduce only (grad_out); 2: reduce/read + update
   uint16_t *w1h, *w2h, *w2th, *w3h, *w3th;
   int* cursor;
+  // xGMI hand-off (mode 1 only): grad_out / grad_out_alt are this rank's exchange slots 0 / 1,
+  // picked by the parity of the step in flight (xgmi.h)
+  float* grad_out_alt;
+  const unsigned* ar_ctl;
 };
 
 __device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) {
@@ -1452,8 +1457,8 @@ __device__ __forceinline__ float quad_sum(float v) {
 }
 
 // w0 / m0: the parameter and momentum, loaded by the caller ahead of the slab sums
-__device__ __forceinline__ void sgd_apply(const SgdArgs& a, long p, float gme, float w0, float m0) {
-  if (a.grad_out) a.grad_out[p] = gme;
+__device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p, float gme, float w0, float m0) {
+  if (gout) gout[p] = gme;
   if (a.mode == 1) return;
   float w = w0;
   float d = gme + a.wd * w;
@@ -1551,7 +1556,39 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
     gme = mine ? a.grad_in[p] : 0.f;
   }
   if (!mine) return;
-  sgd_apply(a, p, gme, w0, m0);
+  float* gout = a.grad_out;
+  if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
+  sgd_apply(a, gout, p, gme, w0, m0);
+}
+
+// Multi-GPU update (after sl_xgmi_barrier): one thread per 4 parameters sums the W ranks' reduced gradients
+// straight out of their exchange buffers over xGMI (rank order: identical on every
+// replica), then applies momentum SGD and refreshes the bf16 shadows -- the all-reduce
+// and the optimizer step in one launch, no RCCL call and no host sync (xgmi.h).
+__global__ __launch_bounds__(256) void mlp_sgd_xgmi_kernel(SgdArgs a, XgArgs x) {
+  __shared__ unsigned s_step;
+  if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
+  const unsigned s = xg_block_step(x, &s_step);  // xgmi_barrier_kernel ran just before
+  const long p0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (p0 < a.n) {
+    float4 v[XG_MAX_WORLD];
+#pragma unroll
+    for (int q = 0; q < XG_MAX_WORLD; ++q)
+      if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), xg_slot_off(x, s) + (unsigned)(p0 * 4));
+    const float4 w4 = *reinterpret_cast<const float4*>(a.w + p0);
+    const float4 m4 = a.mom ? *reinterpret_cast<const float4*>(a.mom + p0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 g = v[0];
+#pragma unroll
+    for (int q = 1; q < XG_MAX_WORLD; ++q)
+      if (q < x.world) {
+        g.x += v[q].x; g.y += v[q].y; g.z += v[q].z; g.w += v[q].w;
+      }
+    const float ga[4] = {g.x, g.y, g.z, g.w}, wa[4] = {w4.x, w4.y, w4.z, w4.w}, ma[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (p0 + j < a.n) sgd_apply(a, nullptr, p0 + j, ga[j], wa[j], ma[j]);
+  }
+  xg_finish(x, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1675,11 +1712,42 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   a.grad_in = grad_in; a.grad_out = grad_out; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = mode;
   a.xa = xa; a.xb = xb;
   a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
+  a.grad_out_alt = nullptr; a.ar_ctl = nullptr;
   if (mode != 0 && !slab && !grad_in) return -1;
   if (mode == 1 && !grad_out) return -1;
   if (slab && (slab_stride & 3)) return -1;
   const long groups = (P_N + 3) / 4;
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + 255) / 256), dim3(256), 0, stream, a);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+// Slab reduction straight into this rank's xGMI exchange slot for the step in flight.
+int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa, float xb, float* slot0,
+                       float* slot1, const unsigned* ctl, hipStream_t stream) {
+  if (!slab || !slot0 || !slot1 || !ctl || (slab_stride & 3)) return -1;
+  SgdArgs a = {};
+  a.slab = slab; a.slices = slices; a.slab_stride = slab_stride; a.grad_out = slot0; a.grad_out_alt = slot1;
+  a.ar_ctl = ctl; a.n = P_N; a.xa = xa; a.xb = xb; a.mode = 1;
+  const long groups = (P_N + 3) / 4;
+  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + 255) / 256), dim3(256), 0, stream, a);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_mlp_sgd_xgmi(float* w, float* mom, float lr, float mu, float wd, uint16_t* w1h, uint16_t* w2h,
+                    uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, char* const* bases, unsigned* ctl,
+                    long slot_bytes, int rank, int world, hipStream_t stream) {
+  if (!w || !bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return -1;
+  if (slot_bytes < ((P_N + 3) / 4) * 16 || (slot_bytes & 255)) return -1;
+  if (((uintptr_t)w | (uintptr_t)(mom ? mom : w)) & 15) return -2;
+  SgdArgs a = {};
+  a.w = w; a.mom = mom; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = 2;
+  a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
+  XgArgs x;
+  x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world;
+  const long groups = (P_N + 3) / 4;
+  hipLaunchKernelGGL(mlp_sgd_xgmi_kernel, dim3((groups + 255) / 256), dim3(256), 0, stream, a, x);
   SL_CHECK_LAUNCH();
   return 0;
 }

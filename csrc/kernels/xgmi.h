@@ -1,0 +1,124 @@
+// Cross-GPU exchange over xGMI: IPC-mapped peer buffers + an in-kernel step barrier.
+//
+// One process per GPU; every rank owns ONE exchange buffer allocated uncached
+// (hipDeviceMallocUncached: no L2 line of it is ever held, locally or on a
+// peer that maps it) and exports it with hipIpcGetMemHandle; every rank maps
+// every peer's buffer (hipIpcOpenMemHandle), so a kernel reads peer memory
+// straight over the xGMI links -- no RCCL call, no host involvement, and the
+// whole exchange is capturable in a hipGraph.
+//
+// Buffer layout (bytes):
+//   [0, XG_HDR)                       inbox: flag of rank q at q * 64 -- the last step id q signalled
+//   [XG_HDR, XG_HDR + slot)           payload slot 0 (even step ids)
+//   [XG_HDR + slot, XG_HDR + 2 slot)  payload slot 1 (odd step ids)
+//
+// Per step (step id s = completed steps + 1, kept on the device so graph
+// replays count on their own):
+//   1. producers write this rank's payload into slot (s & 1) of its OWN buffer
+//      (an ordinary kernel earlier in the stream; its end publishes the bytes);
+//   2. a one-wave barrier kernel stores s into inbox[rank] of EVERY buffer
+//      (system-scope store over xGMI), then waits until its own inbox holds
+//      >= s for every rank (bounded spin, see xg_signal_wait);
+//   3. the consumer kernel reads slot (s & 1) of every rank with system-scope
+//      loads and combines; its last block to finish advances the step counter.
+// Double buffering makes one barrier per step enough: a rank writes slot
+// (s & 1) again only at step s + 2, which it reaches after passing barrier
+// s + 1 -- and every peer signals s + 1 only after its step-s consumer kernel
+// (the reader of that slot) has finished.
+#pragma once
+#include "common.h"
+
+namespace sl {
+
+constexpr int XG_MAX_WORLD = 16;
+constexpr long XG_HDR = 4096;
+constexpr unsigned long long XG_TIMEOUT_TICKS = 100ull * 1000 * 1000 * 10;  // 10 s of the 100 MHz clock
+
+struct XgArgs {
+  char* const* bases;  // [world] device table: rank q's exchange buffer as mapped in this process
+  unsigned* ctl;       // local: [0] completed steps, [1] finished-block counter, [2] error (1 = timeout)
+  long slot_bytes;     // payload slot size, multiple of 256
+  int rank, world;
+};
+
+__device__ __forceinline__ unsigned* xg_inbox(char* base, int q) {
+  return reinterpret_cast<unsigned*>(base + (long)q * 64);
+}
+
+__device__ __forceinline__ char* xg_slot(const XgArgs& x, int q, unsigned s) {
+  return x.bases[q] + XG_HDR + (long)(s & 1u) * x.slot_bytes;
+}
+
+// Buffer descriptor over rank q's slots, from wave-uniform values (readfirstlane: no waterfall).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xg_rsrc(const XgArgs& x, int q) {
+  const unsigned long long b = reinterpret_cast<unsigned long long>(x.bases[q]);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b), hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  char* base = reinterpret_cast<char*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(XG_HDR + 2 * x.slot_bytes), 0x00020000);
+}
+
+// 16-byte payload load at system scope (sc0 sc1): served from memory, never from a line an
+// earlier step left in this XCD's L2 -- the slot is rewritten every second step, and a plain
+// load may hit such a stale copy (measured: a replica drifted at the 5th step without this).
+__device__ __forceinline__ float4 xg_load(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 17));
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+
+__device__ __forceinline__ unsigned xg_slot_off(const XgArgs& x, unsigned s) {
+  return (unsigned)(XG_HDR + (long)(s & 1u) * x.slot_bytes);
+}
+
+// Step id of the step in flight (completed + 1), for producers that pick the slot.
+__device__ __forceinline__ unsigned xg_step(const unsigned* ctl) {
+  return __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+// The step barrier, run by ONE wave (xgmi_barrier_kernel) between the producer and the
+// consumer kernels: lane q < world stores s into inbox[rank] of rank q's buffer (a
+// system-scope store over xGMI), then polls inbox[q] of this rank's own buffer until
+// rank q has signalled s (bounded: after XG_TIMEOUT_TICKS it records the error word
+// and gives up, so a lost peer never hangs the GPU).  Keeping the spin in one wave
+// matters: a consumer grid whose every block spun would hold every CU while it
+// waits, and ranks that share a GPU (tests) could then never run the peer's
+// producer kernels.
+__device__ __forceinline__ void xg_signal_wait(const XgArgs& x) {
+  const int lane = threadIdx.x;
+  const unsigned s = xg_step(x.ctl);
+  if (lane < x.world)
+    __hip_atomic_store(xg_inbox(x.bases[lane], x.rank), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane < x.world) {
+    unsigned* f = xg_inbox(x.bases[x.rank], lane);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - s) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > XG_TIMEOUT_TICKS) {
+        __hip_atomic_store(x.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // "" = system scope
+}
+
+// Step id for a consumer block (one load, shared through LDS).
+__device__ __forceinline__ unsigned xg_block_step(const XgArgs& x, unsigned* lds_step) {
+  if (threadIdx.x == 0) *lds_step = xg_step(x.ctl);
+  __syncthreads();
+  return *lds_step;
+}
+
+// Every block calls this once at its end; the last one advances the step counter.
+__device__ __forceinline__ void xg_finish(const XgArgs& x, unsigned s) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(x.ctl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(x.ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(x.ctl, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace sl

@@ -282,6 +282,7 @@ class FusedMLPTrainer:
         # kernel (22 % MFMA busy, latency-bound; profiles/r01_v10)
         self.l1_gemm = batch % 128 == 0 and os.environ.get("SL_MLP_L1", "0") == "1"
         self.allreduce = None  # callable(grad_tensor) -> None, sums in place (RCCL)
+        self.xgmi = None       # parallel.xgmi.XgmiExchange: all-reduce fused into the update (no RCCL)
         self.x = self.y = None
         self.n_batches = 1
         self.graph = None
@@ -320,7 +321,7 @@ class FusedMLPTrainer:
     def _launches(self):
         """Cached launches for the current buffers/hyper-parameters (rebuilt on change)."""
         key = (self.x.data_ptr() if self.x is not None else 0, self.n_batches, self.grad_scale, self.lr,
-               self.momentum, self.weight_decay)
+               self.momentum, self.weight_decay, id(self.xgmi))
         if getattr(self, "_lkey", None) == key:
             return self._lc
         n, p = self._n, self._n.ptr
@@ -346,6 +347,13 @@ class FusedMLPTrainer:
                                 p(self.grad) if from_grad else None, p(self.grad) if grad_out else None,
                                 self.lr, self.momentum, self.weight_decay, self.xa, self.xb, mode, *ws,
                                 p(self.cursor) if bump else None)
+        if self.xgmi is not None:
+            xg = self.xgmi
+            lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.n_pad, self.xa, self.xb,
+                                     xg.slot_ptr(0), xg.slot_ptr(1), xg.ctl.data_ptr())
+            lc["xbarrier"] = n.Launch("sl_xgmi_barrier", *xg.args())
+            lc["xupdate"] = n.Launch("sl_mlp_sgd_xgmi", p(self.params), p(self.mom), self.lr, self.momentum,
+                                     self.weight_decay, *ws, p(self.cursor), *xg.args())
         self._lc, self._lkey = lc, key
         return lc
 
@@ -397,10 +405,25 @@ class FusedMLPTrainer:
         for _ in range(n):
             self.step()
 
+    def enable_xgmi(self, exchange) -> None:
+        """Aggregate gradients through an :class:`~serverless_learn_amd.parallel.xgmi.XgmiExchange`
+        (the slab reduction lands in this rank's exchange slot; the update kernel sums every
+        rank's slot over xGMI and applies SGD).  ``None`` switches back."""
+        if exchange is not None and exchange.payload_floats < self.n_pad:
+            raise ValueError("exchange slot smaller than the parameter vector")
+        self.xgmi = exchange
+        self.graph = None
+        self._lkey = None
+
     def _step_eager(self) -> None:
         self._rows(True)
         self._wgrad()
-        if self.allreduce is None:
+        if self.xgmi is not None:
+            lc = self._launches()
+            lc["xreduce"]()
+            lc["xbarrier"]()
+            lc["xupdate"]()
+        elif self.allreduce is None:
             self._sgd(2, from_grad=False, grad_out=False)
         else:
             self._sgd(1, from_grad=False, grad_out=True, bump=False)

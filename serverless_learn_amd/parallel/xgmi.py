@@ -1,0 +1,169 @@
+"""One-shot all-reduce over xGMI through IPC-mapped peer buffers.
+
+Inside a node the 8 MI355X are fully connected by xGMI (7 links per GPU).  For
+the MLP's 1.08 MB gradient a ring all-reduce pays 2(W-1) latency-bound hops per
+step; here each rank instead *reads every peer's gradient directly* (W-1
+concurrent reads, one per link) and sums in rank order inside a kernel --
+protocol and memory-ordering argument in ``csrc/kernels/xgmi.h``.  The exchange
+needs no host synchronisation, so the whole multi-GPU step (forward, backward,
+all-reduce, optimizer) is captured in one hipGraph like the 1-GPU step.
+
+Setup is collective: every rank allocates one uncached exchange buffer, exports
+it with ``hipIpcGetMemHandle``, the 64-byte handles are all-gathered over the
+existing process group (RCCL or gloo), and each rank maps every peer's buffer.
+If any rank fails to map any peer, *all* ranks fall back to the process group's
+all-reduce (decided by one all-reduce of an ok flag), so a group never mixes
+the two paths.
+
+The reference has no collective at all -- only 5-second RPC gossip
+(/root/reference/src/worker.cc:194-219); this is the intra-node replacement.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Callable
+
+import torch
+
+from ..ops import _native as N
+
+N.register("sl_xgmi_header_bytes", [])
+N.register("sl_xgmi_alloc", [N.L, ctypes.POINTER(ctypes.c_void_p)])
+N.register("sl_xgmi_free", [N.P])
+N.register("sl_ipc_get_handle", [N.P, N.P])
+N.register("sl_ipc_handle_size", [])
+N.register("sl_ipc_open", [N.P, ctypes.POINTER(ctypes.c_void_p)])
+N.register("sl_ipc_close", [N.P])
+N.register("sl_xgmi_copyin", [N.P, N.P, N.L, N.I, N.I, N.P, N.L, N.P])
+N.register("sl_xgmi_barrier", [N.P, N.P, N.L, N.I, N.I, N.P])
+N.register("sl_xgmi_sum", [N.P, N.P, N.L, N.I, N.I, N.P, N.L, N.F, N.P])
+N.register("sl_xgmi_peek", [N.P, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.P, N.L, N.P])
+
+MAX_WORLD = 16
+
+
+def enabled() -> bool:
+    """``SL_XGMI=0`` forces the process-group (RCCL) all-reduce everywhere."""
+    return os.environ.get("SL_XGMI", "1") != "0"
+
+
+class XgmiExchange:
+    """IPC-mapped exchange buffers of a whole group (one per rank) + step counter.
+
+    ``allgather(bytes) -> list[bytes]`` and ``all_ok(bool) -> bool`` are the group's
+    collectives (used only here, at setup)."""
+
+    def __init__(self, payload_floats: int, rank: int, world: int, device: torch.device,
+                 allgather: Callable[[bytes], list], all_ok: Callable[[bool], bool]):
+        if not (1 <= world <= MAX_WORLD) or not (0 <= rank < world):
+            raise ValueError(f"xgmi exchange needs 1 <= world <= {MAX_WORLD}, got rank {rank} of {world}")
+        lib = N.lib()
+        self.rank, self.world, self.device = rank, world, device
+        self.payload_floats = int(payload_floats)
+        self.slot_bytes = (self.payload_floats * 4 + 255) // 256 * 256
+        self.hdr = int(lib.sl_xgmi_header_bytes())
+        self._own = ctypes.c_void_p()
+        self._opened: list[int] = []
+        self.table = None
+        ok = True
+        err = ""
+        with torch.cuda.device(device):
+            rc = lib.sl_xgmi_alloc(self.hdr + 2 * self.slot_bytes, ctypes.byref(self._own))
+            if rc != 0:
+                raise RuntimeError(f"xgmi exchange allocation failed ({rc})")
+            hsize = int(lib.sl_ipc_handle_size())
+            handle = (ctypes.c_char * hsize)()
+            rc = lib.sl_ipc_get_handle(self._own, handle)
+            mine = bytes(handle) if rc == 0 else b""
+            handles = allgather(mine)
+            bases = []
+            for q, h in enumerate(handles):
+                if q == rank:
+                    bases.append(self._own.value)
+                    continue
+                p = ctypes.c_void_p()
+                if len(h) != hsize:
+                    ok, err = False, f"rank {q} exported no IPC handle"
+                    break
+                buf = ctypes.create_string_buffer(h, hsize)
+                rc = lib.sl_ipc_open(buf, ctypes.byref(p))
+                if rc != 0:
+                    ok, err = False, f"hipIpcOpenMemHandle(rank {q}) failed ({rc})"
+                    break
+                self._opened.append(p.value)
+                bases.append(p.value)
+            ok = all_ok(ok)
+            if not ok:
+                self.close(sync=False)
+                raise RuntimeError("xgmi exchange unavailable: " + (err or "a peer failed to map its buffers"))
+            self.table = torch.tensor(bases, dtype=torch.int64, device=device)
+            self.ctl = torch.zeros(4, dtype=torch.int32, device=device)
+
+    # ---- pointers --------------------------------------------------------------
+    @property
+    def own(self) -> int:
+        return self._own.value
+
+    def slot_ptr(self, parity: int) -> int:
+        return self.own + self.hdr + (parity & 1) * self.slot_bytes
+
+    def args(self):
+        """(table, ctl, slot_bytes, rank, world) -- the launcher's XgArgs fields."""
+        return self.table.data_ptr(), self.ctl.data_ptr(), self.slot_bytes, self.rank, self.world
+
+    # ---- generic all-reduce ----------------------------------------------------
+    def allreduce_(self, t: torch.Tensor, scale: float = 1.0) -> None:
+        """Sum ``t`` over the group in place (fp32, contiguous, numel % 4 == 0)."""
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() % 4:
+            raise ValueError("xgmi allreduce_ needs a contiguous fp32 tensor with numel % 4 == 0")
+        if t.numel() > self.payload_floats:
+            raise ValueError("tensor larger than the exchange slot")
+        s = N.stream_ptr()
+        N.call("sl_xgmi_copyin", *self.args(), t.data_ptr(), t.numel(), s)
+        N.call("sl_xgmi_barrier", *self.args(), s)
+        N.call("sl_xgmi_sum", *self.args(), t.data_ptr(), t.numel(), float(scale), s)
+
+    def peek(self, q: int, parity: int, n: int, system: bool = True) -> torch.Tensor:
+        """Copy of rank ``q``'s slot ``parity`` (diagnostics/tests)."""
+        out = torch.empty((n + 3) // 4 * 4, dtype=torch.float32, device=self.device)
+        N.call("sl_xgmi_peek", *self.args(), q, parity, 1 if system else 0, out.data_ptr(), out.numel(),
+               N.stream_ptr())
+        return out[:n]
+
+    def steps_done(self) -> int:
+        return int(self.ctl[0].item())
+
+    def error(self) -> bool:
+        """True if a barrier gave up waiting for a peer (the results since are invalid)."""
+        return int(self.ctl[2].item()) != 0
+
+    def close(self, sync: bool = True) -> None:
+        """Unmap peers and free the buffer.  ``sync``: the caller has already made sure
+        (e.g. with a group barrier) that no peer still reads this rank's buffer."""
+        if sync:
+            torch.cuda.synchronize(self.device)
+        lib = N.lib()
+        for p in self._opened:
+            lib.sl_ipc_close(ctypes.c_void_p(p))
+        self._opened = []
+        if self._own.value:
+            lib.sl_xgmi_free(self._own)
+            self._own = ctypes.c_void_p()
+
+
+def dist_collectives(group=None):
+    """(allgather, all_ok) over a torch.distributed process group (default group)."""
+    import torch.distributed as dist
+
+    def allgather(b: bytes) -> list:
+        out = [None] * dist.get_world_size(group)
+        dist.all_gather_object(out, b, group=group)
+        return out
+
+    def all_ok(ok: bool) -> bool:
+        out = [None] * dist.get_world_size(group)
+        dist.all_gather_object(out, bool(ok), group=group)
+        return all(out)
+
+    return allgather, all_ok
