@@ -51,8 +51,9 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto")
-    ap.add_argument("--unroll", type=int, default=8,
-                    help="MLP: steps per hipGraph replay (each step still runs all its kernels on its own batch)")
+    ap.add_argument("--unroll", type=int, default=0,
+                    help="MLP: steps per hipGraph replay (each step still runs all its kernels on its own batch); "
+                         "0 = the timed step count itself when <= 256 (one replay times exactly K steps), else 8")
     ap.add_argument("--ingest", choices=["grpc", "local", "device"], default="grpc",
                     help="grpc: file server -> ReceiveFile -> pinned ring -> HBM; local: host-generated shard; "
                          "device: shard synthesised in HBM by the Philox kernel (K8)")
@@ -74,6 +75,7 @@ def parse(argv=None):
     # ResNet-18: 1,024 images per GPU (82 K img/s vs 71 K at 512 and 54 K at 256 on one MI355X;
     # ~3 GB of activations).
     a.batch = a.batch or (65536 if mlp else 1024)
+    a.unroll = a.unroll or (a.steps if a.steps <= 256 else 8)
     a.shard_batches = a.shard_batches or (4 if mlp else 4)
     a.lr = a.lr if a.lr is not None else (0.05 if mlp else 0.1)
     return a

@@ -171,6 +171,34 @@ class ElasticGroup:
             raise GroupBroken(repr(e)) from e
         self._run(work)
 
+    def allgather_fixed(self, data: bytes, size: int) -> list[bytes]:
+        """All-gather one ``size``-byte record per rank (``b""`` = this rank has none)."""
+        if self.pg is None:
+            return [data]
+        buf = torch.zeros(size + 1, dtype=torch.uint8)
+        if data:
+            if len(data) != size:
+                raise ValueError(f"record of {len(data)} bytes, expected {size}")
+            buf[0] = 1
+            buf[1:] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        if self.backend == "nccl":
+            buf = buf.to(self.device)
+        outs = [torch.empty_like(buf) for _ in range(self.world)]
+        try:
+            work = self.pg.allgather([outs], [buf])
+        except Exception as e:
+            self.broken = True
+            raise GroupBroken(repr(e)) from e
+        self._run(work)
+        return [bytes(o[1:].cpu().numpy().tobytes()) if int(o[0]) else b"" for o in outs]
+
+    def all_true(self, ok: bool) -> bool:
+        t = torch.tensor([1.0 if ok else 0.0])
+        if self.backend == "nccl":
+            t = t.to(self.device)
+        self.allreduce_(t, dist.ReduceOp.MIN)
+        return bool(t.item() > 0.5)
+
     def sync_state(self, tensors: list[torch.Tensor]) -> None:
         """Rank 0 broadcasts model/optimizer state to every member (N2)."""
         for t in tensors:

@@ -79,6 +79,7 @@ class Worker:
         self.view_lock = threading.Lock()
         self.view = {"epoch": 0, "peers": [], "rank": -1, "world": 0, "rendezvous": "", "resume_file": 0}
         self.trainer = None
+        self.xgmi = None  # parallel.xgmi.XgmiExchange while an RCCL group of MLP workers is live
         self.gossip: GossipState | None = None
         self.group = ElasticGroup(device=self.device, timeout_s=float(self.cfg.extra.get("dp_timeout_s", 30.0)))
         self.step = 0
@@ -316,6 +317,7 @@ class Worker:
         if v["epoch"] == self.group.epoch and not self.group.broken:
             return
         self.state = "regrouping"
+        self._drop_xgmi()
         with trace.span("regroup", epoch=v["epoch"], world=v["world"]):
             ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"])
             if not ok:
@@ -338,22 +340,56 @@ class Worker:
                         self.log.warn("state_sync_failed", error=str(e))
                         return
                     self._after_external_update()
+                    self._setup_xgmi()
             else:
                 self._set_world(max(1, v["world"]))
         self._install_allreduce()
         self.state = "training"
 
+    # ---- xGMI exchange (parallel/xgmi.py) -----------------------------------------
+    def _setup_xgmi(self) -> None:
+        """MLP on an RCCL group: aggregate through IPC-mapped exchange buffers over xGMI
+        instead of an RCCL all-reduce per step.  Collective over the group; any rank that
+        cannot map its peers makes every rank keep RCCL."""
+        from ..parallel import xgmi
+
+        t = self.trainer
+        if (t is None or not hasattr(t, "enable_xgmi") or self.group.backend != "nccl" or self.group.world < 2
+                or self.group.world > xgmi.MAX_WORLD or not xgmi.enabled()):
+            return
+        hsize = int(xgmi.N.lib().sl_ipc_handle_size())
+        try:
+            ex = xgmi.XgmiExchange(t.n_pad, self.group.rank, self.group.world, self.device,
+                                   lambda b: self.group.allgather_fixed(b, hsize), self.group.all_true)
+        except (RuntimeError, GroupBroken) as e:
+            self.log.warn("xgmi_unavailable", error=str(e))
+            return
+        self.xgmi = ex
+        t.enable_xgmi(ex)
+        self.log.info("xgmi_enabled", epoch=self.group.epoch, world=self.group.world)
+
+    def _drop_xgmi(self) -> None:
+        ex, self.xgmi = self.xgmi, None
+        if ex is None:
+            return
+        with self.train_lock:
+            if self.trainer is not None and hasattr(self.trainer, "enable_xgmi"):
+                self.trainer.enable_xgmi(None)
+        ex.close()
+
     def _install_allreduce(self) -> None:
         """Gradient hook follows the group: set whenever a >1 group is live, cleared otherwise.
 
         Called after every re-form and before every step, so a trainer created after the
-        group formed (first shard arriving late) still reduces its gradients."""
+        group formed (first shard arriving late) still reduces its gradients.  With the
+        xGMI exchange live the update kernel aggregates by itself: no hook."""
         if self.trainer is None:
             return
-        want = self.group.allreduce_ if (self.group.active and self.group.world > 1) else None
+        live = self.group.active and self.group.world > 1
+        want = self.group.allreduce_ if live and self.xgmi is None else None
         if self.trainer.allreduce != want:
             self.trainer.allreduce = want
-            self._set_world(max(1, self.group.world) if want is not None else 1)
+            self._set_world(max(1, self.group.world) if live else 1)
 
     def _train_loop(self) -> None:
         if self.cfg.model == "simulate":
@@ -407,6 +443,11 @@ class Worker:
             self.state = "training"
             self.fault.on_step(self.step)
             if self.cfg.log_every and self.step % self.cfg.log_every == 0:
+                if self.xgmi is not None and self.xgmi.error():
+                    # a peer stopped answering the step barrier: results since are void,
+                    # re-form (the master's next epoch) and resync from rank 0
+                    self.log.warn("xgmi_barrier_timeout", epoch=self.group.epoch)
+                    self.group.broken = True
                 st = self.trainer.stats()
                 now = time.perf_counter()
                 self.rate = (self.samples - s_last) / max(1e-9, now - t_last)
@@ -500,6 +541,7 @@ class Worker:
         self.has_data.set()
         for t in self._threads:
             t.join(timeout=10)
+        self._drop_xgmi()
         self.group.teardown()
         if self.server:
             self.server.stop()
