@@ -45,6 +45,12 @@ using namespace sl;
 #ifndef SL_WGRAD128_KS2_SLOTS
 #define SL_WGRAD128_KS2_SLOTS 4
 #endif
+#ifndef SL_GEMM_PIPE
+#define SL_GEMM_PIPE 0  // conv_gemm: both k-halves' fragment reads in flight, counted lgkmcnt
+#endif
+#ifndef SL_GEMM_PRIO
+#define SL_GEMM_PRIO 0  // conv_gemm: s_setprio(1) around the MFMA bursts
+#endif
 #ifndef SL_GEMM128_SLOTS
 #define SL_GEMM128_SLOTS 2
 #endif
@@ -314,6 +320,39 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     __builtin_amdgcn_s_barrier();  // stage kt visible; slot (kt - 1) % NSLOT free
     if (kt + NSLOT - 1 < nk) issue(kt + NSLOT - 1);
     const uint32_t sb = lds0 + (uint32_t)((kt % NSLOT) * SLOT * 2);
+#if SL_GEMM_PIPE
+    // both halves' fragment reads issued up front; the second half's land under the
+    // first half's MFMAs (counted lgkmcnt instead of a drain per half)
+    short8_t af[2][MT], bf[2][NT];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[h][i] = ds_b128(sb + aoff[i][h]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[h][j] = ds_b128(sb + boff[j][h]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#if SL_GEMM_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[h][i], bf[h][j], acc[i][j]);
+#if SL_GEMM_PRIO
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+#endif
+    }
+#else
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       short8_t af[MT], bf[NT];
@@ -323,11 +362,19 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
       for (int j = 0; j < NT; ++j) bf[j] = ds_b128(sb + boff[j][h]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+#if SL_GEMM_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+#if SL_GEMM_PRIO
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -415,6 +462,230 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
         dst[t] = f2bf(f);
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Large-tile forward / dgrad implicit GEMM for the uniform-tap case (SC % 64 == 0,
+// ncols % 128 == 0): 256 x 128 tiles, 512 threads = 8 waves (4 m x 2 n) of 64 x 64,
+// one workgroup per CU with a 144 KB ring of three 48 KB stages (two in flight,
+// counted vmcnt, one raw barrier per stage).  The A rows' pixel base offsets and
+// (ih0, iw0) are computed once per lane; per stage the tap is a workgroup-uniform
+// scalar, so a DMA piece's source is a few adds and unsigned compares.  The
+// 128 x 128 kernel above re-derives each piece's 64-bit address with quarter-rate
+// multiplies (5.5 VALU instructions per MFMA, profiles/r02_pmc_cnn), waits for all
+// its DMA every stage (two slots) and re-reads each operand byte more often
+// (64 vs 87 FLOP per byte staged).
+// ---------------------------------------------------------------------------
+#ifndef SL_GEMM_BIG
+#define SL_GEMM_BIG 1  // use conv_gemm_big_kernel where it applies
+#endif
+template <bool TRANSPOSED>
+__global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
+  constexpr int BM = 256, BN = 128, NSLOT = 3;
+  constexpr int MT = 4, NT = 4;     // 16 x 16 MFMA tiles per wave (64 x 64)
+  constexpr int PA = 4, PB = 2;     // DMA pieces (8 rows x 64 k, 1 KB) per wave per stage
+  constexpr int PS = PA + PB;
+  constexpr int SLOT = (BM + BN) * BK;  // elements: 48 KB
+  constexpr int CS_LD = BN + 8;
+  static_assert(BM * CS_LD <= NSLOT * SLOT, "epilogue tile must fit the ring");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSLOT * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = logical / tiles_n, tn = logical - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wm = wave >> 1, wn = wave & 1;
+  const bool phase = TRANSPOSED && g.ph >= 0;
+
+  // A rows of this lane: piece j covers rows 8 (wave * PA + j) .. +7 -> row + lane / 8,
+  // LDS chunk lane % 8 <- source chunk swz64(lane % 8, row)
+  int rbase[PA], rih[PA], riw[PA];
+  bool rok[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int row = 8 * (wave * PA + j) + (lane >> 3);
+    const Pix p = decode_pix(g, m0 + row);
+    int ih0, iw0;
+    if (!TRANSPOSED) {
+      ih0 = p.oh * g.stride - g.pad;
+      iw0 = p.ow * g.stride - g.pad;
+    } else if (phase) {
+      ih0 = p.oh;
+      iw0 = p.ow;
+    } else {  // stride-1 transposed gather: ih = oh + pad - kh
+      ih0 = p.oh + g.pad;
+      iw0 = p.ow + g.pad;
+    }
+    rih[j] = ih0;
+    riw[j] = iw0;
+    rok[j] = p.ok;
+    rbase[j] = ((p.n * g.SH + ih0) * g.SW + iw0) * g.SC + swz64(lane & 7, row) * 8;
+  }
+  int boffs[PB];
+  bool bok[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    const int row = 8 * (wave * PB + j) + (lane >> 3);
+    const int col = n0 + row;
+    bok[j] = col < e.ncols;
+    boffs[j] = col * g.wld + swz64(lane & 7, row) * 8;
+  }
+  const int cps_shift = g.c_shift - 6;  // log2(stages per tap)
+  auto issue = [&](int kt) {
+    uint16_t* As = smem + (kt % NSLOT) * SLOT;
+    uint16_t* Bs = As + BM * BK;
+    const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
+    int dh, dw, kb;
+    if (phase) {
+      dh = g.dh[tap];
+      dw = g.dw[tap];
+      kb = g.tapw[tap] * g.SC + ch0;
+    } else {
+      const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
+      dh = TRANSPOSED ? -kh : kh;
+      dw = TRANSPOSED ? -kw : kw;
+      kb = kt * BK;
+    }
+    const int soff = (dh * g.SW + dw) * g.SC + ch0;  // workgroup-uniform
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const bool v = rok[j] && (unsigned)(rih[j] + dh) < (unsigned)g.SH && (unsigned)(riw[j] + dw) < (unsigned)g.SW;
+      glds16(v ? g.src + (rbase[j] + soff) : g_conv_zero, (SL_LDS void*)(As + (wave * PA + j) * 8 * BK));
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j)
+      glds16(bok[j] ? e.w + (boffs[j] + kb) : g_conv_zero, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK));
+  };
+
+  uint32_t aoff[MT][2], boff[NT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int r = wm * 64 + i * 16 + lr;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) aoff[i][h] = (uint32_t)((r * BK + swz64(h * 4 + lg, r) * 8) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int r = wn * 64 + j * 16 + lr;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) boff[j][h] = (uint32_t)(((BM + r) * BK + swz64(h * 4 + lg, r) * 8) * 2);
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
+
+  floatx4_t acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = zero4();
+
+  const int nk = g.K / BK;  // uniform taps: K is a multiple of 64
+  for (int kt = 0; kt < NSLOT - 1 && kt < nk; ++kt) issue(kt);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's pieces of stage kt have landed once only stage kt + 1's (if issued) remain
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's have; every wave is done reading slot (kt - 1) % 3
+    if (kt + NSLOT - 1 < nk) issue(kt + NSLOT - 1);
+    const uint32_t sb = lds0 + (uint32_t)((kt % NSLOT) * SLOT * 2);
+    short8_t af[2][MT], bf[2][NT];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[h][i] = ds_b128(sb + aoff[i][h]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[h][j] = ds_b128(sb + boff[j][h]);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (h == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[h][i], bf[h][j], acc[i][j]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue (as conv_gemm_kernel, 8 waves) ----
+  if (e.stats) {
+    float* rep = rsum_replica(e.stats, 2 * e.ncols);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r];
+          s += v;
+          q += v * v;
+        }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      const int col = n0 + wn * 64 + j * 16 + lr;
+      if (lg == 0 && col < e.ncols) {
+        atomicAdd(rep + col, s);
+        atomicAdd(rep + e.ncols + col, q);
+      }
+    }
+    int* flag = reinterpret_cast<int*>(smem);
+    rsum_finish(e.stats, 2 * e.ncols, flag);
+    __syncthreads();
+  }
+  if (e.yf) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + lr;
+        if (col >= e.ncols) continue;
+        const float b = e.bias ? e.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * 64 + i * 16 + 4 * lg + r;
+          if (row < g.M) e.yf[(long)row * e.ncols + col] = acc[i][j][r] + b;
+        }
+      }
+  }
+  if (!e.y) return;
+  uint16_t* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int cl = wn * 64 + j * 16 + lr;
+      const float b = (e.bias && n0 + cl < e.ncols) ? e.bias[n0 + cl] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cs[(wm * 64 + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[i][j][r] + b);
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int q = tid; q < BM * CPR; q += 512) {
+    const int rl = q / CPR, cc = (q - rl * CPR) * 8;
+    const int row = m0 + rl, col = n0 + cc;
+    if (row >= g.M || col >= e.ncols) continue;
+    short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+    long orow = row;
+    if (phase) {
+      const Pix pq = decode_pix(g, row);
+      orow = ((long)pq.n * g.FH + 2 * pq.oh + g.ph) * g.FW + 2 * pq.ow + g.pw;
+    }
+    uint16_t* dst = e.y + orow * e.ldy + col;
+    if (e.add) {
+      const short8_t a = ld8(e.add + orow * e.ldy + col);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)a[t]));
+    }
+    *reinterpret_cast<short8_t*>(dst) = v;
   }
 }
 
@@ -699,8 +970,26 @@ static int gemm_smallm_tiles() {
   return v;
 }
 
+static int gemm_big_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("SL_GEMM_BIG");
+    v = s ? atoi(s) : SL_GEMM_BIG;
+  }
+  return v;
+}
+
 template <bool T>
 static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) {
+  // 256 x 128 tiles: uniform taps (64-channel stages), whole 128-column tiles, and enough
+  // tiles for every CU; transposed gathers only in phase mode or at stride 1
+  const long big_tiles = (long)((g.M + 255) / 256) * (e.ncols / 128);
+  if (gemm_big_enabled() && (g.SC & 63) == 0 && (g.K & 63) == 0 && (e.ncols & 127) == 0 && big_tiles >= 256 &&
+      (!T || g.ph >= 0 || g.stride == 1) && (g.wld & 7) == 0 && (!e.y || (e.ldy & 7) == 0)) {
+    hipLaunchKernelGGL((conv_gemm_big_kernel<T>), dim3(big_tiles), dim3(512), 0, stream, g, e, e.ncols / 128);
+    SL_CHECK_LAUNCH();
+    return 0;
+  }
   const bool small_n = e.ncols <= 64;
   // prefer 128-row tiles while they still fill the 512 two-per-CU slots once
   // (ResNet-18 stage 4: 512 128x128 tiles beat 1024 64x128 tiles)

@@ -9,7 +9,7 @@ for rep in 1 2; do
 for v in "$@"; do
   so=""; [ "$v" != "base" ] && so=serverless_learn_amd/_native/variants/libslkernels_$v.so
   SL_KERNELS_SO=$so timeout -k 10 150 python bench.py --model resnet18 --ingest device --steps 30 --warmup 5 > gpurun_out/abc_${v}_$rep.log 2>&1 || exit 1
-  echo "$v rep=$rep $(grep -o '"value": [0-9.]*' gpurun_out/abc_${v}_$rep.log)"
+  echo "$v rep=$rep $(grep -o '"value": [0-9.]*\|"train_loss_last": [0-9.]*' gpurun_out/abc_${v}_$rep.log | tr '\n' ' ')"
 done
 done
 for v in "$@"; do

@@ -31,6 +31,10 @@ CONV_CASES = [
     (8, 1, 512, 10, 1, 1, 0),    # FC as a 1x1 conv (cout not a multiple of 8)
     (2, 4, 512, 512, 3, 1, 1),
     (3, 7, 64, 64, 3, 2, 1),     # stride-2 dgrad by parity classes, odd extent (4 + 3 rows)
+    # >= 256 tiles of 256 x 128: the large-tile kernel (conv_gemm_big_kernel)
+    (256, 16, 128, 128, 3, 1, 1),   # forward + stride-1 transposed dgrad
+    (1024, 16, 128, 256, 3, 2, 1),  # forward + phase-mode dgrad (parity classes of 65,536 rows)
+    (256, 8, 256, 512, 3, 1, 1),    # stage-4 shape forward
 ]
 
 
