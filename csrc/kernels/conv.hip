@@ -45,11 +45,17 @@ using namespace sl;
 #ifndef SL_WGRAD128_KS2_SLOTS
 #define SL_WGRAD128_KS2_SLOTS 4
 #endif
+#ifndef SL_GEMM_CHEAP
+#define SL_GEMM_CHEAP 1  // conv_gemm: 32-bit precomputed gather bases on the uniform-tap path
+#endif
 #ifndef SL_GEMM_PIPE
 #define SL_GEMM_PIPE 0  // conv_gemm: both k-halves' fragment reads in flight, counted lgkmcnt
 #endif
 #ifndef SL_GEMM_PRIO
 #define SL_GEMM_PRIO 0  // conv_gemm: s_setprio(1) around the MFMA bursts
+#endif
+#ifndef SL_WGRAD_SHIFT
+#define SL_WGRAD_SHIFT 1  // conv_wgrad: shift-only gather addressing for power-of-two shapes
 #endif
 #ifndef SL_GEMM128_SLOTS
 #define SL_GEMM128_SLOTS 2
@@ -255,6 +261,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
   }
   const bool uniform_tap = (g.SC & 63) == 0;
   const int cps_shift = g.c_shift - 6;  // log2(stages per tap) on the fast path
+  // cheap path: transposed gathers only at stride 1 or in phase mode; 32-bit offsets
+  const bool cheap = SL_GEMM_CHEAP && (!TRANSPOSED || g.ph >= 0 || g.stride == 1) &&
+                     (long)g.N * g.SH * g.SW * g.SC < (1L << 31);
+  int rb32[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    int ih0 = ra[j].ih0, iw0 = ra[j].iw0;
+    rb32[j] = ((pa[j].n * g.SH + ih0) * g.SW + iw0) * g.SC + ca[j] * 8;
+  }
   const uint16_t* pb[PB];
   int cb[PB];
 #pragma unroll
@@ -268,7 +283,26 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     uint16_t* As = smem + (kt % NSLOT) * SLOT;
     uint16_t* Bs = As + BM * BK;
     int kb = kt * BK;  // B-operand column of this stage
-    if (uniform_tap) {
+    if (uniform_tap && cheap) {
+      // 32-bit row bases + a workgroup-uniform tap offset (as conv_gemm_big_kernel)
+      const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
+      int dh, dw;
+      if (TRANSPOSED && g.ph >= 0) {
+        dh = g.dh[tap];
+        dw = g.dw[tap];
+        kb = g.tapw[tap] * g.SC + ch0;
+      } else {
+        const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
+        dh = TRANSPOSED ? -kh : kh;
+        dw = TRANSPOSED ? -kw : kw;
+      }
+      const int soff = (dh * g.SW + dw) * g.SC + ch0;
+#pragma unroll
+      for (int j = 0; j < PA; ++j) {
+        const bool v = ra[j].ok && (unsigned)(ra[j].ih0 + dh) < (unsigned)g.SH && (unsigned)(ra[j].iw0 + dw) < (unsigned)g.SW;
+        glds16(v ? g.src + (rb32[j] + soff) : g_conv_zero, (SL_LDS void*)(As + (wave * PA + j) * 8 * BK));
+      }
+    } else if (uniform_tap) {
       const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
       int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
       if (TRANSPOSED && g.ph >= 0) {
@@ -729,6 +763,9 @@ struct WgradArgs {
   int ldy, cout;
   float* dw;            // [cout][K] fp32, accumulated
   int tiles_k, tiles_co, slices, steps_per_slice;
+  // all-shift gather addressing (SL_WGRAD_SHIFT): log2(SW) and log2(SH*SW*SC) when powers of
+  // two (with hw_shift, w_shift, c_shift, s_shift of g), else -1
+  int sw_shift, img_shift;
 };
 
 // KS = 2: 8 waves, waves 4-7 take the second 32 pixels of every 64-pixel stage
@@ -784,10 +821,34 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
     bkw[j] = tap - ((tap * g.kw_magic) >> 16) * g.KW;
     bch[j] = kk & (g.SC - 1);
   }
+  // all-shift addressing: the lane's dY row pointer advances by a uniform stride per stage,
+  // and the im2col pixel decode / NHWC offset are shifts and adds (no quarter-rate multiplies)
+  const bool shift_path = SL_WGRAD_SHIFT && a.img_shift >= 0 && g.hw_shift >= 0 && g.w_shift >= 0;
+  const uint16_t* abase[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) abase[j] = acol[j] ? acol[j] + (long)(mbeg + arow[j]) * a.ldy : nullptr;
   auto issue = [&](int st) {
     uint16_t* Ai = smem + (st % NSLOT) * SLOT;
     uint16_t* Bi = Ai + IMG_A;
     const int mb = mbeg + st * WGM;
+    if (shift_path) {
+      const long astep = (long)st * WGM * a.ldy;
+#pragma unroll
+      for (int j = 0; j < PA; ++j)
+        glds16((abase[j] && mb + arow[j] < g.M) ? abase[j] + astep : g_conv_zero,
+               (SL_LDS void*)(Ai + (wave * PA + j) * RA * BMO));
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        const int m = mb + brow[j];
+        const int n = m >> g.hw_shift, r = m & ((1 << g.hw_shift) - 1);
+        const int oh = r >> g.w_shift, ow = r & ((1 << g.w_shift) - 1);
+        const int ih = (oh << g.s_shift) - g.pad + bkh[j], iw = (ow << g.s_shift) - g.pad + bkw[j];
+        const bool ok = m < g.M && (unsigned)ih < (unsigned)g.SH && (unsigned)iw < (unsigned)g.SW;
+        const int off = (n << a.img_shift) + (((ih << a.sw_shift) + iw) << g.c_shift) + bch[j];
+        glds16(ok ? g.src + off : g_conv_zero, (SL_LDS void*)(Bi + (wave * PB + j) * RB * BNO));
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const int m = mb + arow[j];
@@ -1082,6 +1143,9 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   if (OH == H && OW == W && sl_conv3x3_wgrad_c64_applicable(H, W, C, cout, KH, KW, stride, pad, ldy))
     return sl_conv3x3_wgrad_c64(x, dy, ldy, N, H, dw, stream);
   a.dy = dy; a.ldy = ldy; a.cout = cout; a.dw = dw;
+  a.sw_shift = ilog2(W);
+  a.img_shift = (a.sw_shift >= 0 && ilog2(H) >= 0) ? ilog2(H * W * C) : -1;
+  if (a.img_shift >= 0 && (long)N * H * W * C >= (1L << 31)) a.img_shift = -1;  // 32-bit offsets
   const int BMO = cout <= 64 ? 64 : 128;
   a.tiles_co = (cout + BMO - 1) / BMO;
   a.tiles_k = (a.g.K + 127) / 128;

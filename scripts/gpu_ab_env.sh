@@ -5,8 +5,7 @@ set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out/abe
 var=$1; shift
-bash scripts/gpu_step.sh 400 abe/tests.log python -u -m pytest tests/test_cnn_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
-grep -q "passed" gpurun_out/abe/tests.log && ! grep -q "failed" gpurun_out/abe/tests.log || exit 1
+for v in "$@"; do env $var=$v bash scripts/gpu_step.sh 400 abe/tests_$v.log python -u -m pytest tests/test_cnn_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1; grep -q "passed" gpurun_out/abe/tests_$v.log && ! grep -q "failed" gpurun_out/abe/tests_$v.log || exit 1; done
 for rep in 1 2; do
 for v in "$@"; do
   env $var=$v timeout -k 10 150 python bench.py --model resnet18 --ingest device --steps 30 --warmup 5 > gpurun_out/abe/${v}_$rep.log 2>&1 || exit 1
