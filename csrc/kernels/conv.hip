@@ -514,6 +514,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #ifndef SL_GEMM_BIG
 #define SL_GEMM_BIG 1  // use conv_gemm_big_kernel where it applies
 #endif
+
 template <bool TRANSPOSED>
 __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
   constexpr int BM = 256, BN = 128, NSLOT = 3;

@@ -11,5 +11,5 @@ run sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_V
 run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_MFMA GRBM_GUI_ACTIVE
 run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE
 for f in gpurun_out/pmcc_*/run_counter_collection.csv; do echo $f; done
-python scripts/pmc_table.py gpurun_out/pmcc_*/run_counter_collection.csv --match conv_ > gpurun_out/pmc_cnn_table.txt
+python scripts/pmc_table.py gpurun_out/pmcc_*/run_counter_collection.csv --match conv > gpurun_out/pmc_cnn_table.txt
 cat gpurun_out/pmc_cnn_table.txt
