@@ -29,6 +29,8 @@ class Config:
     simulated_train_interval_ms: int = 2000
     push_interval_ms: int = 5000
     checkup_interval_ms: int = 5000
+    ps_broadcast_interval_ms: int = 0  # master -> random worker PS exchange (master.cc:268-293, never
+                                       # started in the reference; it would run every 5000 ms); 0 = off
     # --- learning constants (master.cc:60) ---
     learn_rate: float = 0.5            # gossip / PS mixing coefficient alpha
     # --- data plane (file_server.cc:40,46) ---
@@ -79,6 +81,10 @@ class Config:
     @property
     def push_interval(self) -> float:
         return self.push_interval_ms / 1000.0
+
+    @property
+    def ps_broadcast_interval(self) -> float:
+        return self.ps_broadcast_interval_ms / 1000.0
 
     @property
     def checkup_interval(self) -> float:

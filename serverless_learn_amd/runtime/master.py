@@ -58,6 +58,7 @@ class Master:
         self.log = Logger("master", self.addr_requested, self.metrics)
         self.registry = core().Registry()
         self.ps = ParameterServer(self.cfg.learn_rate, per_client=not self.cfg.gossip_compat)
+        self.ps_broadcasts = 0
         self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
         self._lock = threading.Lock()
         self.incarnation: dict[str, int] = {}
@@ -143,6 +144,7 @@ class Master:
             self.log.warn("ps_broadcast_failed", to=target, error=str(e))
             return False
         self.ps.absorb_reply(decode_update(raw, "float64"), delta, target)
+        self.ps_broadcasts += 1
         return True
 
     # ---- heartbeats / failure detection --------------------------------------
@@ -259,8 +261,11 @@ class Master:
             self.metrics.serve(self.cfg.metrics_port)
         self.log.info("serving", rendezvous=self.rendezvous)
         if loops:
-            for fn, iv, name in ((self.checkup_once, self.cfg.checkup_interval, "checkup"),
-                                 (self.push_once, self.cfg.push_interval, "push")):
+            loops = [(self.checkup_once, self.cfg.checkup_interval, "checkup"),
+                     (self.push_once, self.cfg.push_interval, "push")]
+            if self.cfg.ps_broadcast_interval_ms > 0:  # the reference's unstarted periodically_send_updates
+                loops.append((self.broadcast_once, self.cfg.ps_broadcast_interval, "ps_broadcast"))
+            for fn, iv, name in loops:
                 ev = threading.Event()
                 self._wakes.append(ev)
                 t = threading.Thread(target=self._loop, args=(fn, iv, name, ev), daemon=True, name=f"sl-master-{name}")

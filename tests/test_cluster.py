@@ -165,3 +165,17 @@ def test_allreduce_member_whose_shard_arrives_late_stays_in_lockstep(cluster, mo
     assert cluster.wait_for(lambda: a.state == "done" and b.state == "done", 120), (a.step, b.step, a.state, b.state)
     assert a.trainer.allreduce is not None and b.trainer.allreduce is not None
     assert torch.equal(a.trainer.params, b.trainer.params)
+
+
+def test_master_ps_broadcast_loop():
+    """The reference's never-started periodically_send_updates (master.cc:268-293), enabled."""
+    c = LocalCluster(fast_config(ps_broadcast_interval_ms=150))
+    try:
+        a = c.add_worker(sync="ps")
+        b = c.add_worker(sync="ps")
+        assert c.wait_for(lambda: c.master.ps_broadcasts >= 3 and a.gossip is not None and b.gossip is not None
+                          and a.gossip.serves + b.gossip.serves >= 3, 60), \
+            (c.master.ps_broadcasts, a.gossip and a.gossip.serves, b.gossip and b.gossip.serves)
+        assert {a.addr, b.addr} & set(c.master.ps.olds)
+    finally:
+        c.stop()
