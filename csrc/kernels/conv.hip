@@ -735,7 +735,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 // ---------------------------------------------------------------------------
 template <int W>
 __device__ __forceinline__ int swz_tr(int c, int r) {
-  if (W == 16) return c ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1);
+  if (W >= 16) return c ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1);  // 16 / 32 chunks per row
   return c ^ ((((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1);
 }
 
@@ -767,7 +767,56 @@ struct WgradArgs {
   // all-shift gather addressing (SL_WGRAD_SHIFT): log2(SW) and log2(SH*SW*SC) when powers of
   // two (with hw_shift, w_shift, c_shift, s_shift of g), else -1
   int sw_shift, img_shift;
+  // split-K partials: slab [slices][cout][K] written with plain stores and summed into dw by
+  // wgrad_slab_reduce_kernel (null: fp32 atomics into dw, ~1.3 TB/s chip-wide)
+  float* ws;
 };
+
+__device__ __forceinline__ void wgrad_out(const WgradArgs& a, int s, int co, int k, float v) {
+  if (a.ws) a.ws[((long)s * a.cout + co) * a.g.K + k] = v;
+  else if (a.slices > 1) atomicAdd(a.dw + (long)co * a.g.K + k, v);
+  else a.dw[(long)co * a.g.K + k] += v;
+}
+
+// dw[i] += sum_s ws[s][i] (a fixed summation tree: deterministic, unlike the atomics).  8 lanes
+// per float4 group each sum every 8th slice with all their loads in flight, then combine by
+// shuffles: one thread per group was latency-bound (1.9 TB/s on 57 slices).
+constexpr int SLAB_G = 8;
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float4* __restrict__ ws, int slices, long n4,
+                                                                float4* __restrict__ dw) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int part = (int)(t % SLAB_G);
+  const long i = t / SLAB_G;
+  const bool live = i < n4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    constexpr int U = 8;
+    for (int s0 = part; s0 < slices; s0 += SLAB_G * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int sl = s0 + u * SLAB_G;
+        v[u] = sl < slices ? ws[(long)sl * n4 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < SLAB_G; m <<= 1) {
+    acc.x += __shfl_xor(acc.x, m);
+    acc.y += __shfl_xor(acc.y, m);
+    acc.z += __shfl_xor(acc.z, m);
+    acc.w += __shfl_xor(acc.w, m);
+  }
+  if (live && part == 0) {
+    float4 d = dw[i];
+    d.x += acc.x; d.y += acc.y; d.z += acc.z; d.w += acc.w;
+    dw[i] = d;
+  }
+}
 
 // KS = 2: 8 waves, waves 4-7 take the second 32 pixels of every 64-pixel stage
 // (two waves per SIMD inside one workgroup); the k-halves are summed through LDS.
@@ -940,11 +989,144 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
   for (int q = tid; q < BMO * BNO; q += NTW) {
     const int rl = q >> 7, cl = q & 127;
     const int co = co0 + rl, k = k0 + cl;
-    if (co < a.cout && k < g.K) {
-      float* dst = a.dw + (long)co * g.K + k;
-      if (a.slices > 1) atomicAdd(dst, Os[rl * OUT_LD + cl]);
-      else *dst += Os[rl * OUT_LD + cl];
+    if (co < a.cout && k < g.K) wgrad_out(a, s, co, k, Os[rl * OUT_LD + cl]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Large-tile weight gradient for cout % 256 == 0 (ResNet-18 stages 3-4): 256 (co) x 128 (k)
+// tiles, 8 waves of 64 x 64, one workgroup per CU, 3-slot 144 KB ring (two 64-pixel stages
+// in flight), shift-only gather addressing (power-of-two shapes).  Same idea as
+// conv_gemm_big_kernel: twice the output per byte staged, no vmcnt(0) per stage.
+// ---------------------------------------------------------------------------
+#ifndef SL_WGRAD_BIG
+#define SL_WGRAD_BIG 1
+#endif
+__global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
+  constexpr int BMO = 256, BNO = 128, NSLOT = 3, WGM = 64;
+  constexpr int WA = BMO / 8, WB = BNO / 8;       // 16-B chunks per image row: 32 / 16
+  constexpr int MT = 4, NT = 4;                   // 64 x 64 per wave (4 co x 2 k waves)
+  constexpr int RA = 64 / WA, RB = 64 / WB;       // rows per 1 KB DMA piece: 2 / 4
+  constexpr int PA = (WGM / RA) / 8, PB = (WGM / RB) / 8;  // pieces per wave per stage: 4 / 2
+  constexpr int PS = PA + PB;
+  constexpr int IMG_A = WGM * BMO, IMG_B = WGM * BNO;      // elements
+  constexpr int SLOT = IMG_A + IMG_B;                       // 48 KB
+  constexpr int OUT_LD = BNO + 4;
+  static_assert(BMO * OUT_LD * 2 <= NSLOT * SLOT, "fp32 epilogue tile must fit the ring");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSLOT * SLOT];
+
+  const ConvGeom& g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = a.tiles_k * a.tiles_co;
+  const int s = logical / tiles;
+  const int t = logical - s * tiles;
+  const int tco = t / a.tiles_k, tk = t - tco * a.tiles_k;
+  const int co0 = tco * BMO, k0 = tk * BNO;
+  const int mbeg = s * a.steps_per_slice * WGM;
+  const int nst = min(a.steps_per_slice, (g.M - mbeg + WGM - 1) / WGM);
+
+  // A (dY) pieces: row RA (wave * PA + j) + lane / WA, chunk lane % WA <- co chunk swz
+  int arow[PA];
+  const uint16_t* abase[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    arow[j] = RA * (wave * PA + j) + lane / WA;
+    const int co = co0 + swz_tr<WA>(lane % WA, arow[j]) * 8;
+    abase[j] = a.dy + (long)(mbeg + arow[j]) * a.ldy + co;
+  }
+  // B (im2col) pieces: the lane's k chunk (tap, channels) is fixed for the workgroup
+  int brow[PB], bkh[PB], bkw[PB], bch[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    brow[j] = RB * (wave * PB + j) + lane / WB;
+    const int kk = k0 + swz_tr<WB>(lane % WB, brow[j]) * 8;
+    const int tap = kk >> g.c_shift;
+    bkh[j] = (tap * g.kw_magic) >> 16;
+    bkw[j] = tap - bkh[j] * g.KW;
+    bch[j] = kk & (g.SC - 1);
+  }
+  auto issue = [&](int st) {
+    uint16_t* Ai = smem + (st % NSLOT) * SLOT;
+    uint16_t* Bi = Ai + IMG_A;
+    const int mb = mbeg + st * WGM;
+    const long astep = (long)st * WGM * a.ldy;
+#pragma unroll
+    for (int j = 0; j < PA; ++j)
+      glds16(mb + arow[j] < g.M ? abase[j] + astep : g_conv_zero, (SL_LDS void*)(Ai + (wave * PA + j) * RA * BMO));
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int m = mb + brow[j];
+      const int n = m >> g.hw_shift, r = m & ((1 << g.hw_shift) - 1);
+      const int oh = r >> g.w_shift, ow = r & ((1 << g.w_shift) - 1);
+      const int ih = (oh << g.s_shift) - g.pad + bkh[j], iw = (ow << g.s_shift) - g.pad + bkw[j];
+      const bool ok = m < g.M && (unsigned)ih < (unsigned)g.SH && (unsigned)iw < (unsigned)g.SW;
+      const int off = (n << a.img_shift) + (((ih << a.sw_shift) + iw) << g.c_shift) + bch[j];
+      glds16(ok ? g.src + off : g_conv_zero, (SL_LDS void*)(Bi + (wave * PB + j) * RB * BNO));
     }
+  };
+
+  uint32_t aoff[MT], boff[NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) aoff[i] = tr_off<WA>(wm * 64 + i * 16, lane);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) boff[j] = (uint32_t)(IMG_A * 2) + tr_off<WB>(wn * 64 + j * 16, lane);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
+
+  floatx4_t acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = zero4();
+
+  for (int st = 0; st < NSLOT - 1 && st < nst; ++st) issue(st);
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + NSLOT - 1 < nst) issue(st + NSLOT - 1);
+    const uint32_t sb = lds0 + (uint32_t)((st % NSLOT) * SLOT * 2);
+    short8_t af[2][MT], bf[2][NT];
+    auto reads = [&](auto kk) {
+      constexpr int H = decltype(kk)::value;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[H][i] = tr8<WA, H * 32 * WA * 16>(sb + aoff[i]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[H][j] = tr8<WB, H * 32 * WB * 16>(sb + boff[j]);
+    };
+    reads(std::integral_constant<int, 0>{});
+    reads(std::integral_constant<int, 1>{});
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (h == 0) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");  // h0 landed (counter max 15 < 16 h1 reads)
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[h][i], bf[h][j], acc[i][j]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // fp32 tile through LDS so each wave's atomics cover contiguous rows
+  float* Os = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Os[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * OUT_LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  for (int q = tid; q < BMO * BNO; q += 512) {
+    const int rl = q >> 7, cl = q & 127;
+    const int co = co0 + rl, k = k0 + cl;
+    if (co < a.cout && k < g.K) wgrad_out(a, s, co, k, Os[rl * OUT_LD + cl]);
   }
 }
 
@@ -1081,7 +1263,8 @@ int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int
 int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
                    const uint16_t* add, float* stats, hipStream_t stream);
 int sl_conv3x3_wgrad_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldy);
-int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, hipStream_t stream);
+int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, float* ws,
+                         long ws_floats, hipStream_t stream);
 
 // Forward: x [N][H][W][C] -> y [N][OH][OW][ldy] (cols < cout), w [cout][KH][KW][C].
 int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w, int cout, int KH, int KW,
@@ -1135,18 +1318,79 @@ int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint
 
 // Weight gradient: dw[cout][KH][KW][C] += sum over pixels of dy x im2col(x)
 // (fp32, accumulated: the caller zeroes the flat gradient once per step).
+static int wgrad_big_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SL_WGRAD_BIG");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
+static long g_wgrad_ws_need = 0;  // largest slab a call wanted (floats); the caller grows its workspace
+long sl_conv_wgrad_ws_need() { return g_wgrad_ws_need; }
+void sl_wgrad_note_need(long floats) {
+  if (floats > g_wgrad_ws_need) g_wgrad_ws_need = floats;
+}
+
+// dw[0..n) += sum over `slices` partial vectors of n floats (n % 4 == 0, 16-B aligned)
+int sl_wgrad_slab_reduce(const float* ws, int slices, long n, float* dw, hipStream_t stream) {
+  const long n4 = n / 4;
+  const long g = (n4 * SLAB_G + 255) / 256;
+  hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((int)g), dim3(256), 0, stream, reinterpret_cast<const float4*>(ws),
+                     slices, n4, reinterpret_cast<float4*>(dw));
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+static int wgrad_finish(WgradArgs& a, float* ws, long ws_floats, hipStream_t stream, bool launch_reduce) {
+  (void)ws_floats;
+  if (!launch_reduce) return 0;
+  return sl_wgrad_slab_reduce(ws, a.slices, (long)a.cout * a.g.K, a.dw, stream);
+}
+
+// slab mode when a workspace big enough for this call's partials is given; else atomics
+static bool wgrad_use_slab(WgradArgs& a, float* ws, long ws_floats) {
+  a.ws = nullptr;
+  if (a.slices <= 1 || ((long)a.cout * a.g.K) % 4) return false;
+  const long need = (long)a.slices * a.cout * a.g.K;
+  if (need > g_wgrad_ws_need) g_wgrad_ws_need = need;
+  if (!ws || need > ws_floats || ((uintptr_t)ws & 15) || ((uintptr_t)a.dw & 15)) return false;
+  a.ws = ws;
+  return true;
+}
+
 int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t* dy, int ldy, int cout, int KH,
-                  int KW, int stride, int pad, int OH, int OW, float* dw, int target_wgs, hipStream_t stream) {
+                  int KW, int stride, int pad, int OH, int OW, float* dw, int target_wgs, float* ws, long ws_floats,
+                  hipStream_t stream) {
   WgradArgs a;
+  a.ws = nullptr;
   if (fill_geom(a.g, x, N, H, W, C, OH, OW, KH, KW, stride, pad)) return -1;
   if ((ldy & 7) || ldy < cout) return -2;
   if (((uintptr_t)x | (uintptr_t)dy) & 15) return -3;
   if (OH == H && OW == W && sl_conv3x3_wgrad_c64_applicable(H, W, C, cout, KH, KW, stride, pad, ldy))
-    return sl_conv3x3_wgrad_c64(x, dy, ldy, N, H, dw, stream);
+    return sl_conv3x3_wgrad_c64(x, dy, ldy, N, H, dw, ws, ws_floats, stream);
   a.dy = dy; a.ldy = ldy; a.cout = cout; a.dw = dw;
   a.sw_shift = ilog2(W);
   a.img_shift = (a.sw_shift >= 0 && ilog2(H) >= 0) ? ilog2(H * W * C) : -1;
   if (a.img_shift >= 0 && (long)N * H * W * C >= (1L << 31)) a.img_shift = -1;  // 32-bit offsets
+  const bool shift_ok = a.img_shift >= 0 && a.g.hw_shift >= 0 && a.g.w_shift >= 0;
+  if (SL_WGRAD_BIG && wgrad_big_enabled() && shift_ok && (cout & 255) == 0 && ldy >= cout && (a.g.K & 127) == 0 &&
+      (a.g.SC & 7) == 0) {
+    a.tiles_co = cout / 256;
+    a.tiles_k = a.g.K / 128;
+    const int tiles = a.tiles_co * a.tiles_k;
+    const int total_steps = (a.g.M + 63) / 64;
+    const int target = target_wgs > 0 ? target_wgs / 2 : 256;  // one workgroup per CU
+    int slices = tiles >= target ? 1 : (target + tiles - 1) / tiles;
+    if (slices > total_steps) slices = total_steps;
+    a.steps_per_slice = (total_steps + slices - 1) / slices;
+    a.slices = (total_steps + a.steps_per_slice - 1) / a.steps_per_slice;
+    const bool slab = wgrad_use_slab(a, ws, ws_floats);
+    hipLaunchKernelGGL(conv_wgrad_big_kernel, dim3(tiles * a.slices), dim3(512), 0, stream, a);
+    SL_CHECK_LAUNCH();
+    return wgrad_finish(a, ws, ws_floats, stream, slab);
+  }
   const int BMO = cout <= 64 ? 64 : 128;
   a.tiles_co = (cout + BMO - 1) / BMO;
   a.tiles_k = (a.g.K + 127) / 128;
@@ -1160,12 +1404,13 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   a.steps_per_slice = (total_steps + slices - 1) / slices;
   a.slices = (total_steps + a.steps_per_slice - 1) / a.steps_per_slice;
   dim3 grid(tiles * a.slices);
+  const bool slab = wgrad_use_slab(a, ws, ws_floats);
   if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3, 1>), grid, dim3(256), 0, stream, a);
   else if (SL_WGRAD128_KS == 2)
     hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_KS2_SLOTS, 2>), grid, dim3(512), 0, stream, a);
   else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS, 1, SL_WGRAD128_WGM>), grid, dim3(256), 0, stream, a);
   SL_CHECK_LAUNCH();
-  return 0;
+  return wgrad_finish(a, ws, ws_floats, stream, slab);
 }
 
 // Multi-tensor weight re-layout; `descs` is a device array of WtDesc.

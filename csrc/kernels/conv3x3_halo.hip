@@ -343,6 +343,7 @@ struct WgradHaloArgs {
   int ldy;
   int N, H, tiles;
   float* dw;           // [64][9][64] fp32, accumulated
+  float* ws;           // non-null: [gridDim.x][64][9][64] partials, summed by sl_wgrad_slab_reduce
 };
 
 template <int OFF>
@@ -478,7 +479,11 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
       for (int t = 0; t < NTAP; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          atomicAdd(a.dw + ((long)(16 * i + 4 * lg + r) * 9 + T0 + t) * HC + 16 * cb + lr, acc[i][t][r]);
+        {
+          const long o = ((long)(16 * i + 4 * lg + r) * 9 + T0 + t) * HC + 16 * cb + lr;
+          if (a.ws) a.ws[(long)blockIdx.x * (64 * 9 * HC) + o] = acc[i][t][r];
+          else atomicAdd(a.dw + o, acc[i][t][r]);
+        }
   };
   if (th == 0) run(std::integral_constant<int, 0>{});
   else run(std::integral_constant<int, 5>{});
@@ -490,8 +495,11 @@ int sl_conv3x3_wgrad_c64_applicable(int H, int W, int C, int cout, int KH, int K
   return sl_conv3x3_c64_applicable(H, W, C, cout, KH, KW, stride, pad, C) && C == HC && ldy == HC;
 }
 
-int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw,
-                         hipStream_t stream) {
+int sl_wgrad_slab_reduce(const float* ws, int slices, long n, float* dw, hipStream_t stream);
+void sl_wgrad_note_need(long floats);
+
+int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, float* ws,
+                         long ws_floats, hipStream_t stream) {
   if (N <= 0 || H <= 0 || H % TR || ldy != HC || !dw) return -1;
   if ((((uintptr_t)x) | ((uintptr_t)dy)) & 15) return -3;
   if (g_num_cus <= 0) {
@@ -504,8 +512,14 @@ int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, 
   a.x = x; a.dy = dy; a.ldy = ldy; a.N = N; a.H = H; a.dw = dw;
   a.tiles = N * (H / TR);
   const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;
+  // each persistent workgroup's partial dW: a slab + one ordered reduce (plain stores) rather
+  // than 36,864 fp32 atomics per workgroup at the chip-wide atomic rate
+  const long need = (long)grid * 64 * 9 * HC;
+  sl_wgrad_note_need(need);
+  a.ws = (ws && need <= ws_floats && !((uintptr_t)ws & 15) && !((uintptr_t)dw & 15)) ? ws : nullptr;
   hipLaunchKernelGGL(conv3x3_wgrad_c64_kernel, dim3(grid), dim3(WNT), 0, stream, a);
   SL_CHECK_LAUNCH();
+  if (a.ws) return sl_wgrad_slab_reduce(a.ws, grid, 64L * 9 * HC, dw, stream);
   return 0;
 }
 

@@ -155,6 +155,7 @@ class FusedResNetTrainer:
         self.bucket_wait = None   # callable(handles) -> None, before the optimizer
         self.allreduce = None     # callable(grad) -> None (simple, non-overlapped)
         self.bucket_bytes = 16 << 20
+        self.wgws = K.WgradWorkspace(dev)  # split-K slab of the weight gradients (grown on the first step)
 
         items = [(c.w, c.wt, c.spec.cout, c.spec.k * c.spec.k, c.spec.cin, c.ldt)
                  for c in self.conv.values() if c.spec.name != "stem"]
@@ -243,7 +244,7 @@ class FusedResNetTrainer:
                 handles.append(self.bucket_hook(self.grad[lo:pending_from]))
                 pending_from = lo
 
-        K.conv_wgrad(self.feat, self.dlogits, spec.classes, 1, 1, 0, self.fc_gw)
+        K.conv_wgrad(self.feat, self.dlogits, spec.classes, 1, 1, 0, self.fc_gw, ws=self.wgws)
         K.conv_dgrad(self.dlogits, self.fc_wt, 512, 1, 1, 0, self.dfeat)
         K.avgpool_bwd(self.dfeat.view(self.batch, 512), self.dfeat_in)
         dy = self.dfeat_in
@@ -264,18 +265,18 @@ class FusedResNetTrainer:
                 # dc2 and dcs from one read of dz
                 K.bn_bwd_apply_dual(st["dz"], st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"],
                                     st["cs"], bd.sums, bd.coef, bd.ggamma, bd.gbeta, st["dcs"])
-                K.conv_wgrad(st["x"], st["dcs"], blk.down.cout, 1, blk.down.stride, 0, cd.g)
+                K.conv_wgrad(st["x"], st["dcs"], blk.down.cout, 1, blk.down.stride, 0, cd.g, ws=self.wgws)
                 K.conv_dgrad(st["dcs"], cd.wt, blk.down.cin, 1, blk.down.stride, 0, st["dxs"])
                 add = st["dxs"]
             else:
                 K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
-            K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g)
+            K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g, ws=self.wgws)
             K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"])
             # a1 = relu(bn1(c1)): the mask is re-derived from c1 and bn1's coefficients
             K.bn_bwd_reduce(st["da1"], None, st["c1"], b1.sums_buf, mask_coef=b1.coef)
             K.bn_bwd_apply_sums(st["da1"], None, st["c1"], b1.sums, b1.coef, b1.ggamma, b1.gbeta, st["dc1"],
                                 mask_coef=b1.coef)
-            K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g)
+            K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g, ws=self.wgws)
             K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, st["dx"], add=add)
             dy = st["dx"]
             maybe_bucket(blk.conv1.off)
@@ -288,12 +289,14 @@ class FusedResNetTrainer:
         K.bn_bwd_apply_sums(dy, None, self.c0, sbn.sums, sbn.coef, sbn.ggamma, sbn.gbeta, self.dc0,
                             mask_coef=sbn.coef)
         sc = spec.stem_conv
-        K.conv_wgrad(self.x0, self.dc0, 64, sc.k, sc.stride, sc.pad, self.conv["stem"].g)
+        K.conv_wgrad(self.x0, self.dc0, 64, sc.k, sc.stride, sc.pad, self.conv["stem"].g, ws=self.wgws)
         maybe_bucket(0, force=True)
         return handles
 
     def _step_eager(self) -> None:
         self.grad.zero_()
+        if not torch.cuda.is_current_stream_capturing():
+            self.wgws.grow()  # size the split-K slab before any capture (first call: atomics)
         self.forward(train=True)
         handles = self.backward()
         if self.bucket_wait is not None:

@@ -19,7 +19,8 @@ P, I, L, F = N.P, N.I, N.L, N.F
 
 N.register("sl_conv_fwd", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, I, P, P, P, P])
 N.register("sl_conv_dgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, P, P])
-N.register("sl_conv_wgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, I, P])
+N.register("sl_conv_wgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, I, P, L, P])
+N.register("sl_conv_wgrad_ws_need", [], ctypes.c_long)
 N.register("sl_conv_wt", [P, I, L, P])
 N.register("sl_conv_wt_desc_size", [])
 N.register("sl_input_norm", [P, P, P, I, I, L, P, P, F, F, F, F, F, F, P])
@@ -99,13 +100,32 @@ def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None):
 _WGRAD_WGS = int(os.environ.get("SL_WGRAD_WGS", "768"))  # swept 512..2048, profiles/r01_v16
 
 
-def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: int = 0):
-    """dw [cout, k*k*C] fp32 += sum over pixels dy^T im2col(x)."""
+class WgradWorkspace:
+    """Slab for the weight gradient's split-K partials (plain stores + one ordered reduce
+    launch instead of fp32 atomics into dw).  Sized by the launcher's own request: a call
+    that finds it too small falls back to atomics and records the size it wanted, and
+    :meth:`grow` (outside graph capture) makes the next call fit."""
+
+    def __init__(self, device, floats: int = 0):
+        self.device = device
+        self.buf = torch.empty(max(4, floats), dtype=torch.float32, device=device)
+
+    def grow(self) -> bool:
+        need = int(N.lib().sl_conv_wgrad_ws_need())
+        if need > self.buf.numel():
+            self.buf = torch.empty(need, dtype=torch.float32, device=self.device)
+            return True
+        return False
+
+
+def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: int = 0, ws=None):
+    """dw [cout, k*k*C] fp32 += sum over pixels dy^T im2col(x).  ``ws``: WgradWorkspace."""
     n, h, wd, c = x.shape
     _, oh, ow, ldy = dy.shape
     assert dw.dtype == torch.float32 and dw.numel() >= cout * k * k * c
+    buf = ws.buf if ws is not None else None
     N.call("sl_conv_wgrad", _bf16(x), n, h, wd, c, _bf16(dy), ldy, cout, k, k, stride, pad, oh, ow, p(dw),
-           int(target_wgs or _WGRAD_WGS), N.stream_ptr())
+           int(target_wgs or _WGRAD_WGS), p(buf), int(buf.numel()) if buf is not None else 0, N.stream_ptr())
 
 
 class WtDesc(ctypes.Structure):

@@ -34,7 +34,8 @@ CONV_CASES = [
     # >= 256 tiles of 256 x 128: the large-tile kernel (conv_gemm_big_kernel)
     (256, 16, 128, 128, 3, 1, 1),   # forward + stride-1 transposed dgrad
     (1024, 16, 128, 256, 3, 2, 1),  # forward + phase-mode dgrad (parity classes of 65,536 rows)
-    (256, 8, 256, 512, 3, 1, 1),    # stage-4 shape forward
+    (256, 8, 256, 512, 3, 1, 1),    # stage-4 shape forward; large-tile weight gradient (cout 512)
+    (64, 16, 128, 256, 3, 1, 1),    # large-tile weight gradient, cout 256, K 1152
 ]
 
 
@@ -81,9 +82,15 @@ def test_conv_fwd_dgrad_wgrad(case):
     K.conv_dgrad(dyp, wt.reshape(-1), c, k, s, p, dx, add=add)
     dw = torch.zeros(cout, k, k, c, device=DEV)
     K.conv_wgrad(x, dyp, cout, k, s, p, dw, target_wgs=64)
+    # split-K partials through the slab + ordered reduce instead of atomics
+    ws = K.WgradWorkspace(DEV)
+    ws.grow()
+    dw2 = torch.zeros_like(dw)
+    K.conv_wgrad(x, dyp, cout, k, s, p, dw2, target_wgs=64, ws=ws)
     torch.cuda.synchronize()
     assert rel(dx.float() - add.float(), dx_ref) < 2e-2
     assert rel(dw, dw_ref) < 1e-2
+    assert rel(dw2, dw_ref) < 1e-2
 
 
 def test_stats_fold_fresh_across_repeated_launches():
@@ -554,6 +561,14 @@ def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h, cin):
     y, st, dx, dw = outs[1]
     assert rel(dw, dw_ref) < 1e-2
     assert rel(dw, outs[0][3]) < 1e-3
+    # the direct kernel's per-workgroup partials through the slab + ordered reduce
+    ws = K.WgradWorkspace(DEV)
+    K.conv_wgrad(x, dy, c, 3, 1, 1, torch.zeros(c, 3, 3, cin, device=DEV))
+    ws.grow()
+    dws = torch.full((c, 3, 3, cin), 0.25, device=DEV)
+    K.conv_wgrad(x, dy, c, 3, 1, 1, dws, ws=ws)
+    torch.cuda.synchronize()
+    assert rel(dws - 0.25, dw_ref) < 1e-2
     r2 = ref.reshape(-1, c)
     assert rel(y, ref) < 1.5e-2
     assert rel(st[:c], r2.sum(0)) < 1e-2 and rel(st[c:], (r2 * r2).sum(0)) < 1e-2
