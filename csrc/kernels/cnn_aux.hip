@@ -200,8 +200,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     if (qsel < 2) atomicAdd(rep + qsel * C + c, acc);
     else atomicAdd(rep2 + (qsel - 2) * C + c, acc);
   }
-  rsum_finish(sums, 2 * C, reinterpret_cast<int*>(&part[0][24]));
-  if (x2) rsum_finish(sums2, 2 * C, reinterpret_cast<int*>(&part[1][24]));
 }
 
 // dcoef layout [3][C]: a, b, c with dx = a*dz + b*x + c.  grad_gamma/beta += (flat gradient).
@@ -604,6 +602,8 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------
+extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream);  // conv.hip
+
 extern "C" {
 
 long sl_rsum_floats(int n) { return rsum_floats(n); }
@@ -668,6 +668,8 @@ int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, ymask, dz_out, sums, x2, sums2, rows,
                      C);
   SL_CHECK_LAUNCH();
+  if (int rc = sl_rsum_fold(sums, 2 * C, stream)) return rc;
+  if (x2) return sl_rsum_fold(sums2, 2 * C, stream);
   return 0;
 }
 

@@ -86,44 +86,22 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // Contention-free cross-workgroup sums of n values (per-channel statistics).
 // A thousand workgroups atomically adding into the same n words serialise on
 // those words (MI355X_MICROARCH.md "Global float atomics", contention row), so
-// each workgroup adds into replica (blockIdx % SL_REP) of a [SL_REP][n] array,
-// then takes a ticket; the last of the grid folds the replicas into out[n].
-// Release/acquire per cdna_hip_programming.md Guideline 16: every wave drains
-// its atomics (vmcnt 0), workgroup barrier, one lane agent-release + drained
-// ticket add; the last arriver agent-acquires before reading the replicas.
-// Buffer layout (rsum_floats(n) floats, zeroed before the launch):
-//   [SL_REP][n] replicas | [n] result | u32 ticket (+3 pad)
+// each workgroup adds into replica (blockIdx % SL_REP) of a [SL_REP][n] array
+// and a separate launch, rsum_fold_kernel (conv.hip, sl_rsum_fold), folds the
+// replicas into out[n] once the producers are done.  The fold used to be done
+// by the last workgroup of the producer itself (agent-release fence + ticket per
+// workgroup): with ~1000-8000 workgroups per launch the per-workgroup release
+// (an L2 writeback on a multi-XCD part) and the single-address ticket cost
+// ~1 ms per ResNet-18 step (profiles/r02_rsum); the kernel boundary orders the
+// replica atomics for free.
+// Buffer layout (rsum_floats(n) floats, replicas zeroed before the producers):
+//   [SL_REP][n] replicas | [n] result | 4 pad
 // ---------------------------------------------------------------------------
 constexpr int SL_REP = 32;
 __host__ __device__ constexpr long rsum_floats(int n) { return (long)(SL_REP + 1) * n + 4; }
 
 __device__ __forceinline__ float* rsum_replica(float* buf, int n) { return buf + (long)(blockIdx.x % SL_REP) * n; }
 __device__ __forceinline__ float* rsum_result(float* buf, int n) { return buf + (long)SL_REP * n; }
-
-// Call from ALL threads of the workgroup after its atomics are issued.
-__device__ __forceinline__ void rsum_finish(float* buf, int n, int* lds_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float* out = rsum_result(buf, n);
-  unsigned* ticket = reinterpret_cast<unsigned*>(out + n);
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *lds_flag = (t == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (!*lds_flag) return;
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    float acc = 0.f;
-#pragma unroll 8
-    for (int r = 0; r < SL_REP; ++r) acc += __hip_atomic_load(buf + (long)r * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    out[i] = acc;
-  }
-}
 
 }  // namespace sl
 

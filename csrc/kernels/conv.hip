@@ -28,6 +28,7 @@
 // (sum, sum of squares of the fp32 accumulator -> fp32 atomics), bias, fp32
 // output (logits), residual add (dgrad of a tensor that also feeds a skip).
 #include "common.h"
+#include "bn_bwd_epi.h"
 
 #include <type_traits>
 
@@ -98,6 +99,7 @@ struct ConvEpi {
   const float* bias;    // [ncols] (nullable)
   const uint16_t* add;  // [M][ldy] bf16 added to the result (nullable)
   float* stats;         // rsum buffer of 2*ncols (sum, sum of squares), zeroed (nullable)
+  BnBwdEpi bn;          // data gradient only: ReLU mask + BN-backward sums of the output (bn.x null: off)
 };
 
 struct Pix {
@@ -438,9 +440,6 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
         atomicAdd(rep + e.ncols + col, q);
       }
     }
-    int* flag = reinterpret_cast<int*>(smem);  // ring is drained; reused as the last-arriver flag
-    rsum_finish(e.stats, 2 * e.ncols, flag);
-    __syncthreads();
   }
   if (e.yf) {
 #pragma unroll
@@ -458,7 +457,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
       }
   }
   if (!e.y) return;
-  // bf16 tile through LDS -> coalesced 16-B row stores (+ bias, + residual)
+  // bf16 tile through LDS -> coalesced 16-B row stores (+ bias, + residual, + fused BN backward)
   uint16_t* Cs = smem;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -469,33 +468,58 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #pragma unroll
       for (int r = 0; r < 4; ++r) Cs[(wm * (BM / 2) + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[i][j][r] + b);
     }
-  __syncthreads();
+  // A thread's 16-B chunks: column chunk tid % CPR of rows tid / CPR + i * (256 / CPR).  Their
+  // residual / BN operands are loaded here, all in flight under the staging barrier.
   constexpr int CPR = BN / 8;  // 16-B chunks per row
-  for (int q = tid; q < BM * CPR; q += 256) {
-    const int rl = q / CPR, cc = (q - rl * CPR) * 8;
-    const int row = m0 + rl, col = n0 + cc;
-    if (row >= g.M || col >= e.ncols) continue;
-    short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+  constexpr int EIT = BM * CPR / 256;
+  const int cc = (tid % CPR) * 8, col = n0 + cc;
+  const bool full = col + 8 <= e.ncols;
+  // fused BN backward (TRANSPOSED only; the host guarantees ncols % 8 == 0, ldy == ncols)
+  const bool bnb = TRANSPOSED && e.bn.x;
+  long eoff[EIT];
+  short8_t ea[EIT];
+  BnbIn ebn[EIT];
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int row = m0 + tid / CPR + it * (256 / CPR);
     long orow = row;  // phase mode: parity-class pixel -> full-output pixel
     if (TRANSPOSED && g.ph >= 0) {
       const Pix q = decode_pix(g, row);
       orow = ((long)q.n * g.FH + 2 * q.oh + g.ph) * g.FW + 2 * q.ow + g.pw;
     }
-    uint16_t* dst = e.y + orow * e.ldy + col;
-    if (col + 8 <= e.ncols) {
-      if (e.add) {
-        const short8_t a = ld8(e.add + orow * e.ldy + col);
+    eoff[it] = orow * e.ldy + col;
+    const bool ok = row < g.M && full;
+    if (ok && e.add) ea[it] = ld8(e.add + eoff[it]);
+    if (ok && bnb) bnb_load(e.bn, eoff[it], ebn[it]);
+  }
+  BnbAcc bacc;
+  float msc[8], msh[8];
+  if (bnb) bnb_init(e.bn, e.ncols, full ? col : 0, bacc, msc, msh);
+  __syncthreads();
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)a[t]));
+  for (int it = 0; it < EIT; ++it) {
+    const int rl = tid / CPR + it * (256 / CPR), row = m0 + rl;
+    if (row >= g.M || col >= e.ncols) continue;
+    short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+    uint16_t* dst = e.y + eoff[it];
+    if (full) {
+      if (e.add) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
       }
+      if (bnb) bnb_chunk(e.bn, ebn[it], v, msc, msh, bacc);
       *reinterpret_cast<short8_t*>(dst) = v;
     } else {
       for (int t = 0; t < 8 && col + t < e.ncols; ++t) {
         float f = bf2f((uint16_t)v[t]);
-        if (e.add) f += bf2f(e.add[orow * e.ldy + col + t]);
+        if (e.add) f += bf2f(e.add[eoff[it] + t]);
         dst[t] = f2bf(f);
       }
     }
+  }
+  if (bnb) {
+    __syncthreads();  // staging reads done: the ring holds the fold
+    bnb_fold<256, CPR>(e.bn, bacc, reinterpret_cast<float*>(smem), n0, e.ncols);
   }
 }
 
@@ -672,9 +696,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
         atomicAdd(rep + e.ncols + col, q);
       }
     }
-    int* flag = reinterpret_cast<int*>(smem);
-    rsum_finish(e.stats, 2 * e.ncols, flag);
-    __syncthreads();
   }
   if (e.yf) {
 #pragma unroll
@@ -702,25 +723,44 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 #pragma unroll
       for (int r = 0; r < 4; ++r) Cs[(wm * 64 + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[i][j][r] + b);
     }
-  __syncthreads();
-  constexpr int CPR = BN / 8;
-  for (int q = tid; q < BM * CPR; q += 512) {
-    const int rl = q / CPR, cc = (q - rl * CPR) * 8;
-    const int row = m0 + rl, col = n0 + cc;
-    if (row >= g.M || col >= e.ncols) continue;
-    short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+  // operand prefetch as in conv_gemm_kernel (ncols % 128 == 0: every chunk is whole)
+  constexpr int CPR = BN / 8, EIT = BM * CPR / 512;
+  const int cc = (tid % CPR) * 8, col = n0 + cc;
+  const bool bnb = TRANSPOSED && e.bn.x;  // fused BN backward (see conv_gemm_kernel)
+  long eoff[EIT];
+  short8_t ea[EIT];
+  BnbIn ebn[EIT];
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int row = m0 + tid / CPR + it * (512 / CPR);
     long orow = row;
     if (phase) {
       const Pix pq = decode_pix(g, row);
       orow = ((long)pq.n * g.FH + 2 * pq.oh + g.ph) * g.FW + 2 * pq.ow + g.pw;
     }
-    uint16_t* dst = e.y + orow * e.ldy + col;
-    if (e.add) {
-      const short8_t a = ld8(e.add + orow * e.ldy + col);
+    eoff[it] = orow * e.ldy + col;
+    if (row < g.M && e.add) ea[it] = ld8(e.add + eoff[it]);
+    if (row < g.M && bnb) bnb_load(e.bn, eoff[it], ebn[it]);
+  }
+  BnbAcc bacc;
+  float msc[8], msh[8];
+  if (bnb) bnb_init(e.bn, e.ncols, col, bacc, msc, msh);
+  __syncthreads();
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)a[t]));
+  for (int it = 0; it < EIT; ++it) {
+    const int rl = tid / CPR + it * (512 / CPR), row = m0 + rl;
+    if (row >= g.M) continue;
+    short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+    if (e.add) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
     }
-    *reinterpret_cast<short8_t*>(dst) = v;
+    if (bnb) bnb_chunk(e.bn, ebn[it], v, msc, msh, bacc);
+    *reinterpret_cast<short8_t*>(e.y + eoff[it]) = v;
+  }
+  if (bnb) {
+    __syncthreads();
+    bnb_fold<512, CPR>(e.bn, bacc, reinterpret_cast<float*>(smem), n0, e.ncols);
   }
 }
 
@@ -1223,30 +1263,72 @@ static int gemm_big_enabled() {
   return v;
 }
 
+// Kernel choice for one implicit GEMM: 0 = 256 x 128 large tile, else the 128/64 tile shape.
+struct GemmPlan {
+  int big, BM, BN, tiles_n;
+  long grid;
+};
+
 template <bool T>
-static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) {
+static GemmPlan plan_gemm(const ConvGeom& g, const ConvEpi& e) {
+  GemmPlan p{};
   // 256 x 128 tiles: uniform taps (64-channel stages), whole 128-column tiles, and enough
   // tiles for every CU; transposed gathers only in phase mode or at stride 1
   const long big_tiles = (long)((g.M + 255) / 256) * (e.ncols / 128);
   if (gemm_big_enabled() && (g.SC & 63) == 0 && (g.K & 63) == 0 && (e.ncols & 127) == 0 && big_tiles >= 256 &&
       (!T || g.ph >= 0 || g.stride == 1) && (g.wld & 7) == 0 && (!e.y || (e.ldy & 7) == 0)) {
-    hipLaunchKernelGGL((conv_gemm_big_kernel<T>), dim3(big_tiles), dim3(512), 0, stream, g, e, e.ncols / 128);
-    SL_CHECK_LAUNCH();
-    return 0;
+    p.big = 1; p.BM = 256; p.BN = 128; p.tiles_n = e.ncols / 128; p.grid = big_tiles;
+    return p;
   }
   const bool small_n = e.ncols <= 64;
   // prefer 128-row tiles while they still fill the 512 two-per-CU slots once
   // (ResNet-18 stage 4: 512 128x128 tiles beat 1024 64x128 tiles)
   const int tn128 = (e.ncols + (small_n ? 63 : 127)) / (small_n ? 64 : 128);
   const bool small_m = (long)((g.M + 127) / 128) * tn128 < gemm_smallm_tiles();
-  const int BMv = small_m ? 64 : 128, BNv = small_n ? 64 : 128;
-  const int tiles_m = (g.M + BMv - 1) / BMv, tiles_n = (e.ncols + BNv - 1) / BNv;
-  dim3 grid(tiles_m * tiles_n), block(256);
+  p.BM = small_m ? 64 : 128;
+  p.BN = small_n ? 64 : 128;
+  p.tiles_n = (e.ncols + p.BN - 1) / p.BN;
+  p.grid = (long)((g.M + p.BM - 1) / p.BM) * p.tiles_n;
+  return p;
+}
+
+template <bool T>
+static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) {
+  const GemmPlan p = plan_gemm<T>(g, e);
+  dim3 grid((unsigned)p.grid);
+  if (p.big) {
+    hipLaunchKernelGGL((conv_gemm_big_kernel<T>), grid, dim3(512), 0, stream, g, e, p.tiles_n);
+    SL_CHECK_LAUNCH();
+    return 0;
+  }
+  dim3 block(256);
   // LDS ring sized for two workgroups per CU (<= 72 KB each)
-  if (BMv == 128 && BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 128, T, SL_GEMM128_SLOTS>), grid, block, 0, stream, g, e, tiles_n);
-  else if (BMv == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 64, T, 3>), grid, block, 0, stream, g, e, tiles_n);
-  else if (BNv == 128) hipLaunchKernelGGL((conv_gemm_kernel<64, 128, T, 3>), grid, block, 0, stream, g, e, tiles_n);
-  else hipLaunchKernelGGL((conv_gemm_kernel<64, 64, T, 4>), grid, block, 0, stream, g, e, tiles_n);
+  if (p.BM == 128 && p.BN == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 128, T, SL_GEMM128_SLOTS>), grid, block, 0, stream, g, e, p.tiles_n);
+  else if (p.BM == 128) hipLaunchKernelGGL((conv_gemm_kernel<128, 64, T, 3>), grid, block, 0, stream, g, e, p.tiles_n);
+  else if (p.BN == 128) hipLaunchKernelGGL((conv_gemm_kernel<64, 128, T, 3>), grid, block, 0, stream, g, e, p.tiles_n);
+  else hipLaunchKernelGGL((conv_gemm_kernel<64, 64, T, 4>), grid, block, 0, stream, g, e, p.tiles_n);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+// Fold of the rsum replicas into the result row (common.h): one launch after the producers.
+// 64 threads per block, all SL_REP loads of a thread in flight at once: the launch is
+// latency-bound (2C <= 1024 values), so keep it to one round trip and spread it over CUs.
+__global__ __launch_bounds__(64) void rsum_fold_kernel(float* buf, int n) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  float v[SL_REP];
+#pragma unroll
+  for (int r = 0; r < SL_REP; ++r) v[r] = buf[(long)r * n + i];
+  float acc = 0.f;
+#pragma unroll
+  for (int r = 0; r < SL_REP; ++r) acc += v[r];
+  rsum_result(buf, n)[i] = acc;
+}
+
+extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream) {
+  if (!buf || n <= 0) return -1;
+  hipLaunchKernelGGL(rsum_fold_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, buf, n);
   SL_CHECK_LAUNCH();
   return 0;
 }
@@ -1262,6 +1344,8 @@ int sl_conv_set_phase(int on) {
 int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldw);
 int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
                    const uint16_t* add, float* stats, hipStream_t stream);
+int sl_conv3x3_c64_bn(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
+                      const uint16_t* add, float* stats, const BnBwdEpi* bn, hipStream_t stream);
 int sl_conv3x3_wgrad_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int stride, int pad, int ldy);
 int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, float* ws,
                          long ws_floats, hipStream_t stream);
@@ -1274,25 +1358,29 @@ int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w
   if (fill_geom(g, x, N, H, W, C, OH, OW, KH, KW, stride, pad)) return -1;
   if (y && (ldy < cout || (ldy & 7))) return -2;
   if ((g.K & 7) || (((uintptr_t)x | (uintptr_t)w) & 15)) return -3;
-  if (y && !yf && !bias && OH == H && OW == W && sl_conv3x3_c64_applicable(H, W, C, cout, KH, KW, stride, pad, C))
-    return sl_conv3x3_c64(x, w, C, 0, N, H, y, ldy, nullptr, stats, stream);
-  ConvEpi e{w, cout, y, ldy, yf, bias, nullptr, stats};
-  return launch_gemm<false>(g, e, stream);
+  int rc;
+  if (y && !yf && !bias && OH == H && OW == W && sl_conv3x3_c64_applicable(H, W, C, cout, KH, KW, stride, pad, C)) {
+    rc = sl_conv3x3_c64(x, w, C, 0, N, H, y, ldy, nullptr, stats, stream);
+  } else {
+    ConvEpi e{w, cout, y, ldy, yf, bias, nullptr, stats, {}};
+    rc = launch_gemm<false>(g, e, stream);
+  }
+  if (rc || !stats) return rc;
+  return sl_rsum_fold(stats, 2 * cout, stream);
 }
 
-// Data gradient: dy [N][OH][OW][ldd] (SC = ldd channels, zero beyond cout),
-// wt [cin][KH][KW][ldd] -> dx [N][H][W][cin] (+= add if given).
-int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int KH, int KW,
-                  int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add, hipStream_t stream) {
-  ConvGeom g;
-  if (fill_geom(g, dy, N, OH, OW, ldd, H, W, KH, KW, stride, pad)) return -1;
-  if (cin & 7) return -2;
-  if (((uintptr_t)dy | (uintptr_t)wt) & 15) return -3;
-  if (H == OH && W == OW && ldd == 64 && sl_conv3x3_c64_applicable(OH, OW, ldd, cin, KH, KW, stride, pad, ldd))
-    return sl_conv3x3_c64(dy, wt, 64, 1, N, OH, dx, cin, add, nullptr, stream);
-  ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr};
+static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt,
+                        int cin, int KH, int KW, int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add,
+                        const BnBwdEpi* bn, hipStream_t stream) {
+  if (H == OH && W == OW && ldd == 64 && !(bn && bn->x2) &&
+      sl_conv3x3_c64_applicable(OH, OW, ldd, cin, KH, KW, stride, pad, ldd))
+    return sl_conv3x3_c64_bn(dy, wt, 64, 1, N, OH, dx, cin, add, nullptr, bn, stream);
+  ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr, {}};
+  if (bn) e.bn = *bn;
   if (g_conv_phase && stride == 2 && KH == 3 && KW == 3 && pad == 1 && (ldd & 63) == 0) {
     // four parity classes of dX, each a dense GEMM over its own taps (1, 2, 2, 4 of the 9)
+    ConvGeom qs[4];
+    int nq = 0;
     for (int ph = 0; ph < 2; ++ph)
       for (int pw = 0; pw < 2; ++pw) {
         ConvGeom q = g;
@@ -1308,12 +1396,52 @@ int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint
           }
         q.ntaps = t;
         q.K = t * ldd;
-        const int rc = launch_gemm<true>(q, e, stream);
-        if (rc) return rc;
+        qs[nq++] = q;
       }
+    for (int i = 0; i < nq; ++i) {
+      const int rc = launch_gemm<true>(qs[i], e, stream);
+      if (rc) return rc;
+    }
     return 0;
   }
   return launch_gemm<true>(g, e, stream);
+}
+
+// Data gradient: dy [N][OH][OW][ldd] (SC = ldd channels, zero beyond cout),
+// wt [cin][KH][KW][ldd] -> dx [N][H][W][cin] (+= add if given).  bn (nullable, bn->x
+// set): the output is the gradient of a ReLU(BatchNorm) input -- it is stored masked and
+// that BN's backward sums are accumulated in the epilogue (bn_bwd_epi.h).
+int sl_conv_dgrad_bn(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int KH, int KW,
+                     int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add, const BnBwdEpi* bn,
+                     hipStream_t stream) {
+  ConvGeom g;
+  if (fill_geom(g, dy, N, OH, OW, ldd, H, W, KH, KW, stride, pad)) return -1;
+  if (cin & 7) return -2;
+  if (((uintptr_t)dy | (uintptr_t)wt) & 15) return -3;
+  const bool fuse = bn && bn->x;
+  if (fuse && (!bn->sums || (bn->x2 && !bn->sums2) || (bn->ymask && bn->mcoef) ||
+               (((uintptr_t)bn->x | (uintptr_t)bn->x2 | (uintptr_t)dx) & 15)))
+    return -4;
+  int rc = dgrad_launch(g, dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, fuse ? bn : nullptr,
+                        stream);
+  if (rc || !fuse) return rc;
+  if ((rc = sl_rsum_fold(bn->sums, 2 * cin, stream))) return rc;
+  return bn->x2 ? sl_rsum_fold(bn->sums2, 2 * cin, stream) : 0;
+}
+
+int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int KH, int KW,
+                  int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add, hipStream_t stream) {
+  return sl_conv_dgrad_bn(dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, nullptr, stream);
+}
+
+// ctypes entry: the BnBwdEpi fields as scalars
+int sl_conv_dgrad_bnx(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int KH, int KW,
+                      int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add, const uint16_t* bx,
+                      const uint8_t* ymask, const float* mcoef, float* sums, const uint16_t* x2, float* sums2,
+                      hipStream_t stream) {
+  BnBwdEpi b{bx, ymask, mcoef, sums, x2, sums2};
+  return sl_conv_dgrad_bn(dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, bx ? &b : nullptr,
+                          stream);
 }
 
 // Weight gradient: dw[cout][KH][KW][C] += sum over pixels of dy x im2col(x)

@@ -26,6 +26,7 @@
 // statistics of the fp32 accumulator (sum, sum of squares) kept per lane over
 // all tiles of the workgroup and folded once through the replica buffers.
 #include "common.h"
+#include "bn_bwd_epi.h"
 
 #include <stdlib.h>
 
@@ -78,6 +79,7 @@ struct HaloArgs {
   const uint16_t* add;  // [N*H*32][ldy] residual (nullable)
   float* stats;         // rsum buffer for 2*64 values (nullable)
   int tiles;
+  BnBwdEpi bn;          // dgrad: ReLU mask + BN-backward sums of the output (bn.x null: off)
 };
 
 template <int CIN>
@@ -150,6 +152,11 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   const uint32_t b_base = (uint32_t)((lr * L::W_CH + lg) * 16);
 
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  // fused BN backward: the epilogue's 8-channel chunk of a thread is (tid & 7) in every tile
+  const bool bnb = a.bn.x != nullptr;
+  BnbAcc bacc;
+  float msc[8], msh[8];
+  if (bnb) bnb_init(a.bn, HC, (tid & 7) * 8, bacc, msc, msh);
 
   int t = blockIdx.x;
   if (t < a.tiles) halo_load(t);
@@ -224,19 +231,29 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           Cs[(wave * (TPIX / NWF) + i * 16 + 4 * lg + r) * OUT_LD + j * 16 + lr] = f2bf(acc[i][j][r]);
-    __syncthreads();
+    // residual / BN operands of this thread's chunks, in flight under the staging barrier
+    constexpr int EIT = TPIX * 8 / NTF;
     const long pix0 = (long)t * TPIX;  // tiles are whole 8-row bands: pixel index = tile * 256
+    const int c = (tid & 7) * 8;
+    short8_t ea[EIT];
+    BnbIn ebn[EIT];
 #pragma unroll
-    for (int k = 0; k < TPIX * 8 / NTF; ++k) {
-      const int q = tid + k * NTF;
-      const int p = q >> 3, c = (q & 7) * 8;
+    for (int k = 0; k < EIT; ++k) {
+      const long off = (pix0 + ((tid + k * NTF) >> 3)) * a.ldy + c;
+      if (a.add) ea[k] = ld8(a.add + off);
+      if (bnb) bnb_load<false>(a.bn, off, ebn[k]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EIT; ++k) {
+      const int p = (tid + k * NTF) >> 3;
       short8_t v = *reinterpret_cast<const short8_t*>(Cs + p * OUT_LD + c);
       const long m = pix0 + p;
       if (a.add) {
-        const short8_t ad = ld8(a.add + m * a.ldy + c);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (short)f2bf(bf2f((uint16_t)v[e]) + bf2f((uint16_t)ad[e]));
+        for (int e = 0; e < 8; ++e) v[e] = (short)f2bf(bf2f((uint16_t)v[e]) + bf2f((uint16_t)ea[k][e]));
       }
+      if (bnb) bnb_chunk<false>(a.bn, ebn[k], v, msc, msh, bacc);
       *reinterpret_cast<short8_t*>(a.y + m * a.ldy + c) = v;
     }
     __syncthreads();  // staging reads done before the next halo lands
@@ -261,8 +278,10 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
         atomicAdd(rep + HC + j * 16 + lr, q);
       }
     }
-    int* flag = reinterpret_cast<int*>(smem);
-    rsum_finish(a.stats, 2 * HC, flag);
+  }
+  if (bnb) {
+    __syncthreads();  // the last tile's staging reads are done (no halo follows)
+    bnb_fold<NTF, HC / 8>(a.bn, bacc, reinterpret_cast<float*>(smem), 0, HC);
   }
 }
 
@@ -290,10 +309,13 @@ int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int
 }
 
 // cin: 64 (forward or, with flip, data gradient) or 8 (forward only).
-int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
-                   const uint16_t* add, float* stats, hipStream_t stream) {
+// bn (nullable; dgrad only, ldy == 64): the output is stored ReLU-masked and its BatchNorm's
+// backward sums are accumulated (bn_bwd_epi.h).
+int sl_conv3x3_c64_bn(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
+                      const uint16_t* add, float* stats, const BnBwdEpi* bn, hipStream_t stream) {
   if (N <= 0 || H <= 0 || H % TR || ldy < HC || (ldy & 7) || !y || (cin != 64 && cin != 8) || (cin == 8 && flip))
     return -1;
+  if (bn && (ldy != HC || stats || bn->x2)) return -2;  // no second BN here (register budget)
   if ((((uintptr_t)src) | ((uintptr_t)w) | ((uintptr_t)y) | ((uintptr_t)add)) & 15) return -3;
   if (g_num_cus <= 0) {
     int dev = 0;
@@ -304,11 +326,18 @@ int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, in
   HaloArgs a;
   a.src = src; a.w = w; a.flip = flip; a.N = N; a.H = H; a.y = y; a.ldy = ldy; a.add = add; a.stats = stats;
   a.tiles = N * (H / TR);
+  a.bn = BnBwdEpi{};
+  if (bn) a.bn = *bn;
   const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;  // persistent: one workgroup per CU (130 KB LDS)
   if (cin == 64) hipLaunchKernelGGL(conv3x3_kernel<64>, dim3(grid), dim3(NTF), 0, stream, a);
   else hipLaunchKernelGGL(conv3x3_kernel<8>, dim3(grid), dim3(NTF), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
+}
+
+int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
+                   const uint16_t* add, float* stats, hipStream_t stream) {
+  return sl_conv3x3_c64_bn(src, w, cin, flip, N, H, y, ldy, add, stats, nullptr, stream);
 }
 
 }  // extern "C"

@@ -11,9 +11,13 @@ Per step:
   forward   input_norm -> [conv (+BN stats in the epilogue) -> bn_apply with
             the finalize folded in (+residual, ReLU)] x 20 -> avgpool -> fc -> 
             softmax-CE (loss, dlogits, dbias)
-  backward  per block, in reverse: bn_bwd_reduce + bn_bwd_apply (ReLU mask
-            fused), conv wgrad (split-K, fp32 atomics straight into the flat
-            gradient) and dgrad (residual gradient fused into its epilogue)
+  backward  per block, in reverse: bn_bwd_apply (ReLU mask fused), conv wgrad
+            (split-K partials in a slab + one ordered reduce into the flat
+            gradient) and dgrad, whose epilogue adds the residual gradient,
+            applies the next BN's ReLU mask and accumulates that BN's backward
+            sums (csrc/kernels/bn_bwd_epi.h), so only the first BN after the
+            average pool still needs a bn_bwd_reduce pass (SL_BNB_FUSE=0: one
+            per BN, as before)
   comms     optional: the flat gradient is laid out in forward order, so
             when a block's backward is done its whole parameter range is final
             -> a bucket hook can launch RCCL all-reduce of that range while
@@ -24,6 +28,7 @@ Per step:
 """
 from __future__ import annotations
 
+import os
 import torch
 
 from .mlp import StepStats
@@ -156,6 +161,8 @@ class FusedResNetTrainer:
         self.allreduce = None     # callable(grad) -> None (simple, non-overlapped)
         self.bucket_bytes = 16 << 20
         self.wgws = K.WgradWorkspace(dev)  # split-K slab of the weight gradients (grown on the first step)
+        # BN-backward sums in the data-gradient epilogues instead of bn_bwd_reduce passes
+        self.fuse_bn_bwd = os.environ.get("SL_BNB_FUSE", "1") != "0"
 
         items = [(c.w, c.wt, c.spec.cout, c.spec.k * c.spec.k, c.spec.cin, c.ldt)
                  for c in self.conv.values() if c.spec.name != "stem"]
@@ -248,17 +255,32 @@ class FusedResNetTrainer:
         K.conv_dgrad(self.dlogits, self.fc_wt, 512, 1, 1, 0, self.dfeat)
         K.avgpool_bwd(self.dfeat.view(self.batch, 512), self.dfeat_in)
         dy = self.dfeat_in
-        for st in reversed(self.blocks):
+        fuse = self.fuse_bn_bwd
+        sbn = self.bn[spec.stem_bn.name]
+        rblocks = list(reversed(self.blocks))
+
+        def block_out_bn(st):
+            # BN backward of a block output y = relu(bn2(c2) + sc): the mask is the forward's
+            # 1-bit image of y; a downsample shortcut's BN (input cs) is fed by the same dz
+            blk = st["spec"]
+            b2 = self.bn[blk.bn2.name]
+            d = dict(x=st["c2"], sums=b2.sums_buf, y_mask=st["ym"])
+            if blk.down is not None:
+                d.update(x2=st["cs"], sums2=self.bn[blk.dbn.name].sums_buf)
+            return d
+
+        for i, st in enumerate(rblocks):
             blk: BlockSpec = st["spec"]
             c1, c2 = self.conv[blk.conv1.name], self.conv[blk.conv2.name]
             b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
-            # y = relu(bn2(c2) + sc): dz = dy * 1[y > 0] feeds bn2 and the shortcut; the
-            # mask comes from the forward's 1-bit image of y, not from y itself
-            # with a downsample shortcut its BN sums (same dz, input cs) come from the same pass
+            # y = relu(bn2(c2) + sc): dz = dy * 1[y > 0] feeds bn2 and the shortcut.  Fused: the
+            # previous conv1 data gradient (next block's) already stored dz and the sums.
             down = blk.down is not None
             bd = self.bn[blk.dbn.name] if down else None
-            K.bn_bwd_reduce(dy, None, st["c2"], b2.sums_buf, dz_out=st["dz"], y_mask=st["ym"],
-                            x2=st["cs"] if down else None, sums2=bd.sums_buf if down else None)
+            if not (fuse and i > 0):
+                bo = block_out_bn(st)
+                K.bn_bwd_reduce(dy, None, bo["x"], bo["sums"], dz_out=st["dz"], y_mask=bo["y_mask"],
+                                x2=bo.get("x2"), sums2=bo.get("sums2"))
             add = st["dz"]
             if down:
                 cd = self.conv[blk.down.name]
@@ -271,21 +293,36 @@ class FusedResNetTrainer:
             else:
                 K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
             K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g, ws=self.wgws)
-            K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"])
             # a1 = relu(bn1(c1)): the mask is re-derived from c1 and bn1's coefficients
-            K.bn_bwd_reduce(st["da1"], None, st["c1"], b1.sums_buf, mask_coef=b1.coef)
+            bn1 = dict(x=st["c1"], sums=b1.sums_buf, mask_coef=b1.coef)
+            if fuse:
+                K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"], bn=bn1)
+            else:
+                K.conv_dgrad(st["dc2"], c2.wt, blk.conv2.cin, 3, 1, 1, st["da1"])
+                K.bn_bwd_reduce(st["da1"], None, st["c1"], b1.sums_buf, mask_coef=b1.coef)
             K.bn_bwd_apply_sums(st["da1"], None, st["c1"], b1.sums, b1.coef, b1.ggamma, b1.gbeta, st["dc1"],
                                 mask_coef=b1.coef)
             K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g, ws=self.wgws)
-            K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, st["dx"], add=add)
-            dy = st["dx"]
+            # the input gradient is the previous block's output gradient (its dz, stored masked
+            # with that block's BN sums) or, for the first block, the stem BN's
+            nxt = None
+            if fuse and i + 1 < len(rblocks):
+                nxt = block_out_bn(rblocks[i + 1])
+                dx = rblocks[i + 1]["dz"]
+            elif fuse and spec.stem != "imagenet":
+                nxt = dict(x=self.c0, sums=sbn.sums_buf, mask_coef=sbn.coef)
+                dx = st["dx"]
+            else:
+                dx = st["dx"]
+            K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, dx, add=add, bn=nxt)
+            dy = dx
             maybe_bucket(blk.conv1.off)
         # stem
-        sbn = self.bn[spec.stem_bn.name]
         if spec.stem == "imagenet":
             K.maxpool_bwd(dy, self.p0_arg, self.da0)
             dy = self.da0
-        K.bn_bwd_reduce(dy, None, self.c0, sbn.sums_buf, mask_coef=sbn.coef)
+        if not (fuse and spec.stem != "imagenet"):
+            K.bn_bwd_reduce(dy, None, self.c0, sbn.sums_buf, mask_coef=sbn.coef)
         K.bn_bwd_apply_sums(dy, None, self.c0, sbn.sums, sbn.coef, sbn.ggamma, sbn.gbeta, self.dc0,
                             mask_coef=sbn.coef)
         sc = spec.stem_conv

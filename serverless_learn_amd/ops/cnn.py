@@ -19,6 +19,7 @@ P, I, L, F = N.P, N.I, N.L, N.F
 
 N.register("sl_conv_fwd", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, I, P, P, P, P])
 N.register("sl_conv_dgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, P, P])
+N.register("sl_conv_dgrad_bnx", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P])
 N.register("sl_conv_wgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, I, P, L, P])
 N.register("sl_conv_wgrad_ws_need", [], ctypes.c_long)
 N.register("sl_conv_wt", [P, I, L, P])
@@ -57,7 +58,7 @@ def _f32(t):
 
 
 def rsum_floats(n: int) -> int:
-    """Size of a cross-workgroup sum buffer for n values (replicas | result | ticket)."""
+    """Size of a cross-workgroup sum buffer for n values (replicas | result | pad)."""
     return int(N.lib().sl_rsum_floats(n))
 
 
@@ -84,15 +85,33 @@ def conv_fwd(x, w, cout: int, k: int, stride: int, pad: int, y=None, yf=None, bi
     return oh, ow
 
 
-def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None):
-    """dy [N,OH,OW,Cd] bf16 (Cd channels, zero beyond cout), wt [cin, k*k*Cd] -> dx [N,H,W,cin] (+ add)."""
+def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None, bn=None):
+    """dy [N,OH,OW,Cd] bf16 (Cd channels, zero beyond cout), wt [cin, k*k*Cd] -> dx [N,H,W,cin] (+ add).
+
+    ``bn``: dx is the gradient at the input of ``relu(bn(x))`` (or of a block output
+    ``relu(bn(x) + shortcut)``): a dict with ``x`` (the BN input, dx's shape), ``sums``
+    (its zeroed rsum buffer) and the ReLU mask as ``mask_coef`` or ``y_mask`` -- the keys
+    of :func:`bn_bwd_reduce`, optionally with ``x2``/``sums2``.  dx is then stored masked
+    and the BN-backward sums are accumulated by the conv epilogue, replacing a
+    :func:`bn_bwd_reduce` pass (csrc/kernels/bn_bwd_epi.h)."""
     n, oh, ow, cd = dy.shape
     _, h, wd, ci = dx.shape
     assert ci == cin
     if add is not None:
         assert add.shape == dx.shape and add.dtype == torch.bfloat16
-    N.call("sl_conv_dgrad", _bf16(dy), n, oh, ow, cd, _bf16(wt), cin, k, k, stride, pad, h, wd, _bf16(dx),
-           _bf16(add) if add is not None else None, N.stream_ptr())
+    if bn is None:
+        N.call("sl_conv_dgrad", _bf16(dy), n, oh, ow, cd, _bf16(wt), cin, k, k, stride, pad, h, wd, _bf16(dx),
+               _bf16(add) if add is not None else None, N.stream_ptr())
+        return
+    x, ym, mc, x2 = bn["x"], bn.get("y_mask"), bn.get("mask_coef"), bn.get("x2")
+    assert x.shape == dx.shape and dx.is_contiguous() and (ym is None or mc is None)
+    if ym is not None:
+        assert ym.dtype == torch.uint8 and ym.numel() * 8 == x.numel() and ym.is_contiguous()
+    assert (x2 is None) == (bn.get("sums2") is None) and (x2 is None or x2.shape == x.shape)
+    N.call("sl_conv_dgrad_bnx", _bf16(dy), n, oh, ow, cd, _bf16(wt), cin, k, k, stride, pad, h, wd, _bf16(dx),
+           _bf16(add) if add is not None else None, _bf16(x), p(ym) if ym is not None else None,
+           _f32(mc) if mc is not None else None, _f32(bn["sums"]), _bf16(x2) if x2 is not None else None,
+           _f32(bn["sums2"]) if x2 is not None else None, N.stream_ptr())
 
 
 # split-K target for the implicit-GEMM weight gradient (workgroups per launch);
