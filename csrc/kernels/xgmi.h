@@ -109,11 +109,15 @@ __device__ __forceinline__ unsigned xg_block_step(const XgArgs& x, unsigned* lds
   return *lds_step;
 }
 
-// Every block calls this once at its end; the last one advances the step counter.
+// Every block calls this once at its end; the last one advances the step counter.  The
+// count is relaxed: a block's read of the step id (xg_block_step) completed before its
+// first barrier, so the advance cannot overtake it, and the consumer's other writes reach
+// later kernels through the kernel boundary.  An acq_rel add here cost every block an
+// agent-scope release, i.e. an L2 writeback on this 8-XCD part (profiles/r02_bnfuse).
 __device__ __forceinline__ void xg_finish(const XgArgs& x, unsigned s) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(x.ctl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned prev = __hip_atomic_fetch_add(x.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1) {
       __hip_atomic_store(x.ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(x.ctl, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
