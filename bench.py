@@ -65,6 +65,9 @@ def parse(argv=None):
                     help="MLP gradient all-reduce for N>1: xgmi = one-shot over IPC-mapped peer buffers fused "
                          "into the update kernel (hipGraph-capturable); pg = the process group's all-reduce "
                          "(RCCL); auto = xgmi, falling back to pg if any rank cannot map its peers")
+    ap.add_argument("--autotune", type=int, default=6,
+                    help="--allreduce auto with N>1: untimed steps per candidate (xGMI exchange vs the process "
+                         "group) before the timed region; the faster one is timed (0 = keep xGMI)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     mlp = a.model == "mlp"
@@ -181,6 +184,44 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     first_loss = tr.stats().loss
 
+    def pg_mode():
+        tr.enable_xgmi(None)
+        tr.allreduce = lambda g: dist.all_reduce(g)
+        return lambda n: [tr.step() for _ in range(n)]
+
+    autotune = None
+    if xg is not None and args.allreduce == "auto" and args.autotune > 0:
+        # the xGMI exchange is validated on ranks sharing one GPU; on a real node its speed
+        # depends on the peer links, so time a few untimed steps of it against the process
+        # group's all-reduce and keep the faster (max over ranks decides, identically everywhere)
+        def clock(fn, n):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn(n)
+            torch.cuda.synchronize()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item()) / n
+        t_x = clock(run, args.autotune)
+        run_pg = pg_mode()
+        run_pg(2)
+        t_p = clock(run_pg, args.autotune)
+        autotune = {"xgmi_ms": round(t_x * 1e3, 4), "pg_ms": round(t_p * 1e3, 4), "steps": args.autotune}
+        if t_p < t_x:
+            run, use_graph = run_pg, False
+            collective = "rccl" if args.dist_backend == "nccl" else "gloo"
+            xg_keep = xg
+            xg = None
+        else:
+            tr.enable_xgmi(xg)
+            tr.allreduce = None
+            if use_graph:
+                tr.capture(warmup=0, unroll=args.unroll)
+            run = getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
+            run(2)
+        torch.cuda.synchronize()
+
     # ---- 3. timed region ----------------------------------------------------
     def timed() -> float:
         if world > 1:
@@ -215,13 +256,11 @@ def main(argv=None) -> int:
             # group's all-reduce and time the K steps again
             xgmi_fallback = "barrier timeout" if xg.error() else "replicas diverged"
             print(f"xgmi exchange failed ({xgmi_fallback}); re-timing with the process group", file=sys.stderr)
-            tr.enable_xgmi(None)
+            run = pg_mode()
             flat = tr.get_flat()
             dist.broadcast(flat, 0)
             tr.set_flat(flat)
-            tr.allreduce = lambda g: dist.all_reduce(g)
             use_graph, collective = False, ("rccl" if args.dist_backend == "nccl" else "gloo")
-            run = lambda n: [tr.step() for _ in range(n)]
             run(3)
             elapsed = timed()
             replicas_identical = replicas_agree()
@@ -264,6 +303,8 @@ def main(argv=None) -> int:
     }
     if xgmi_fallback:
         out["xgmi_fallback"] = xgmi_fallback
+    if autotune:
+        out["allreduce_autotune"] = autotune
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -272,8 +313,9 @@ def main(argv=None) -> int:
                 f.write(line + "\n")
     if world > 1:
         dist.barrier()
-        if xg is not None:
-            xg.close()
+        for ex in (xg, locals().get("xg_keep")):
+            if ex is not None:
+                ex.close()
         dist.destroy_process_group()
     return 0
 
