@@ -124,3 +124,34 @@ def test_device_synth_matches_numpy_reference():
         assert np.array_equal(lab.cpu().numpy(), ref_lab)
         diff = np.abs(img.cpu().numpy().astype(int) - ref_img.astype(int))
         assert diff.max() <= 1 and (diff > 0).mean() < 0.01, (kind, diff.max(), (diff > 0).mean())
+
+
+@pytest.mark.parametrize("argv", [
+    ["--steps", "4", "--warmup", "2", "--ingest", "local", "--batch", "4096"],
+    ["--model", "resnet18", "--steps", "2", "--warmup", "1", "--ingest", "device", "--batch", "64"],
+])
+def test_bench_prints_the_driver_json_contract(argv, capsys):
+    """bench.py's one JSON line: the fields the driver reads, the BASELINE.json metric for the
+    MLP, whole-job value = global batch x steps / time."""
+    import json
+    import os
+
+    import bench
+
+    assert bench.main(argv) == 0
+    line = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    for k in ("model", "global_batch", "seq_len", "parallelism"):
+        assert k in out["config"], k
+    assert out["n_gpus"] == 1 and out["steps"] == int(argv[argv.index("--steps") + 1])
+    assert out["higher_is_better"] is True and out["scaling"] == "weak" and out["dtype"] == "bf16"
+    assert "synthetic" in out["data"] and out["config"]["parallelism"] == "dp1"
+    b = out["config"]["global_batch"]
+    assert abs(out["value"] - b / (out["ms_per_step"] / 1e3)) / out["value"] < 0.03  # ms_per_step is rounded
+    if "--model" not in argv:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        with open(os.path.join(root, "BASELINE.json")) as f:
+            assert out["metric"] == json.load(f)["metric"]
