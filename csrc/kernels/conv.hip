@@ -49,12 +49,6 @@ using namespace sl;
 #ifndef SL_GEMM_CHEAP
 #define SL_GEMM_CHEAP 1  // conv_gemm: 32-bit precomputed gather bases on the uniform-tap path
 #endif
-#ifndef SL_GEMM_PIPE
-#define SL_GEMM_PIPE 0  // conv_gemm: both k-halves' fragment reads in flight, counted lgkmcnt
-#endif
-#ifndef SL_GEMM_PRIO
-#define SL_GEMM_PRIO 0  // conv_gemm: s_setprio(1) around the MFMA bursts
-#endif
 #ifndef SL_WGRAD_SHIFT
 #define SL_WGRAD_SHIFT 1  // conv_wgrad: shift-only gather addressing for power-of-two shapes
 #endif
@@ -356,39 +350,6 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     __builtin_amdgcn_s_barrier();  // stage kt visible; slot (kt - 1) % NSLOT free
     if (kt + NSLOT - 1 < nk) issue(kt + NSLOT - 1);
     const uint32_t sb = lds0 + (uint32_t)((kt % NSLOT) * SLOT * 2);
-#if SL_GEMM_PIPE
-    // both halves' fragment reads issued up front; the second half's land under the
-    // first half's MFMAs (counted lgkmcnt instead of a drain per half)
-    short8_t af[2][MT], bf[2][NT];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int i = 0; i < MT; ++i) af[h][i] = ds_b128(sb + aoff[i][h]);
-#pragma unroll
-      for (int j = 0; j < NT; ++j) bf[h][j] = ds_b128(sb + boff[j][h]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#if SL_GEMM_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[h][i], bf[h][j], acc[i][j]);
-#if SL_GEMM_PRIO
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(0);
-#endif
-    }
-#else
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       short8_t af[MT], bf[NT];
@@ -398,19 +359,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
       for (int j = 0; j < NT; ++j) bf[j] = ds_b128(sb + boff[j][h]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-#if SL_GEMM_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-#if SL_GEMM_PRIO
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(0);
-#endif
     }
-#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

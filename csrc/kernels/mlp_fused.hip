@@ -61,9 +61,6 @@ using namespace sl;
 #ifndef SL_WG_PIPE
 #define SL_WG_PIPE 1  // software-pipelined wgrad main loop (0: the plain loop)
 #endif
-#ifndef SL_WG_PRIO
-#define SL_WG_PRIO 0  // s_setprio(1) around the wgrad MFMA bursts
-#endif
 #ifndef SL_WG_KO
 #define SL_WG_KO 0  // timing knockouts of mlp_wgrad_kernel (1 no MFMAs, 2 no LDS-DMA after stage 0)
 #endif
@@ -1163,9 +1160,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
           else b1[j] = wg_tr8<KB>(sb + b_addr[j]);
         }
         __builtin_amdgcn_sched_barrier(0);
-#if SL_WG_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1181,10 +1175,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
-#if SL_WG_PRIO
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(0);
-#endif
       }
     }
   };
