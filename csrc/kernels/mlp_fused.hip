@@ -1466,7 +1466,7 @@ __device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p,
 // SGD_TPG threads per float4 group of parameters: each sums every SGD_TPG-th
 // slab slice, the group combines by DPP (quad perms, then row_half_mirror for 8).
 #ifndef SL_SGD_KO
-#define SL_SGD_KO 0  // timing knockouts of mlp_sgd_kernel (1: no shadow writes, 2: no slab reads)
+#define SL_SGD_KO 0  // timing knockouts of mlp_sgd_kernel (1: no shadow writes, 2: no slab reads, 3: empty)
 #endif
 #ifndef SL_SGD_TPG
 #define SL_SGD_TPG 4
@@ -1481,6 +1481,7 @@ __device__ __forceinline__ float group_sum(float v) {
 
 __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
+  if (SL_SGD_KO == 3) return;  // timing knockout 3: launch + kernel-boundary floor
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int part = (int)(t % SGD_TPG);
   const long p0 = (t / SGD_TPG) * 4;
