@@ -61,13 +61,14 @@ def parse(argv=None):
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL over xGMI, the production path); gloo only to rehearse several ranks "
                          "sharing one GPU (RCCL refuses duplicate devices)")
-    ap.add_argument("--allreduce", choices=["auto", "xgmi", "pg"], default="auto",
+    ap.add_argument("--allreduce", choices=["auto", "xgmi", "xgmi2", "pg"], default="auto",
                     help="MLP gradient all-reduce for N>1: xgmi = one-shot over IPC-mapped peer buffers fused "
-                         "into the update kernel (hipGraph-capturable); pg = the process group's all-reduce "
-                         "(RCCL); auto = xgmi, falling back to pg if any rank cannot map its peers")
+                         "into the update kernel (hipGraph-capturable); xgmi2 = two-shot (reduce-scatter + "
+                         "all-gather) through the same buffers; pg = the process group's all-reduce (RCCL); "
+                         "auto = the fastest of the three, timed before the timed region")
     ap.add_argument("--autotune", type=int, default=6,
-                    help="--allreduce auto with N>1: untimed steps per candidate (xGMI exchange vs the process "
-                         "group) before the timed region; the faster one is timed (0 = keep xGMI)")
+                    help="--allreduce auto with N>1: untimed steps per candidate (xGMI one-shot, xGMI two-shot, "
+                         "the process group) before the timed region; the fastest is timed (0 = keep one-shot xGMI)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     mlp = a.model == "mlp"
@@ -150,15 +151,16 @@ def main(argv=None) -> int:
         dist.broadcast(flat, 0)
         tr.set_flat(flat)
         collective = "rccl" if args.dist_backend == "nccl" else "gloo"
-        if mlp and args.allreduce in ("auto", "xgmi"):
+        if mlp and args.allreduce in ("auto", "xgmi", "xgmi2"):
             from serverless_learn_amd.parallel.xgmi import XgmiExchange, dist_collectives
 
             try:
-                xg = XgmiExchange(tr.n_pad, rank, world, dev, *dist_collectives())
+                xg = XgmiExchange(tr.n_pad, rank, world, dev, *dist_collectives(),
+                                  two_shot=args.allreduce == "xgmi2")
                 tr.enable_xgmi(xg)
-                collective = "xgmi-ipc"
+                collective = "xgmi-ipc-two-shot" if xg.two_shot else "xgmi-ipc"
             except RuntimeError as e:
-                if args.allreduce == "xgmi":
+                if args.allreduce in ("xgmi", "xgmi2"):
                     raise
                 print(f"xgmi all-reduce unavailable, using the process group: {e}", file=sys.stderr)
         if mlp and xg is None:
@@ -203,23 +205,35 @@ def main(argv=None) -> int:
             t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return float(t.item()) / n
-        t_x = clock(run, args.autotune)
+        def xgmi_mode(two_shot: bool):
+            xg.two_shot = two_shot
+            tr.enable_xgmi(xg)
+            tr.allreduce = None
+            if use_graph:
+                tr.capture(warmup=0, unroll=args.unroll)
+            fn = getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
+            fn(2)
+            return fn
+        # the graph candidates are timed as the timed region runs them: one replay of the
+        # k-step graph (a run of single-step replays behaves differently, e.g. with ranks
+        # sharing a GPU)
+        n_at = args.unroll if use_graph and args.unroll <= 256 else args.autotune
+        t_x = clock(run, n_at)
+        run_x2 = xgmi_mode(True)
+        t_x2 = clock(run_x2, n_at)
         run_pg = pg_mode()
         run_pg(2)
         t_p = clock(run_pg, args.autotune)
-        autotune = {"xgmi_ms": round(t_x * 1e3, 4), "pg_ms": round(t_p * 1e3, 4), "steps": args.autotune}
-        if t_p < t_x:
+        autotune = {"xgmi_ms": round(t_x * 1e3, 4), "xgmi_two_shot_ms": round(t_x2 * 1e3, 4),
+                    "pg_ms": round(t_p * 1e3, 4), "steps": n_at, "pg_steps": args.autotune}
+        if t_p < min(t_x, t_x2):
             run, use_graph = run_pg, False
             collective = "rccl" if args.dist_backend == "nccl" else "gloo"
             xg_keep = xg
             xg = None
         else:
-            tr.enable_xgmi(xg)
-            tr.allreduce = None
-            if use_graph:
-                tr.capture(warmup=0, unroll=args.unroll)
-            run = getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
-            run(2)
+            run = xgmi_mode(t_x2 < t_x)
+            collective = "xgmi-ipc-two-shot" if xg.two_shot else "xgmi-ipc"
         torch.cuda.synchronize()
 
     # ---- 3. timed region ----------------------------------------------------

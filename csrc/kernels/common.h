@@ -14,6 +14,7 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short short8_t __attribute__((ext_vector_type(8)));
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
 
 #define SL_LDS __attribute__((address_space(3)))
 
@@ -21,6 +22,11 @@ namespace sl {
 
 __device__ __forceinline__ floatx4_t mfma16(const short8_t& a, const short8_t& b, const floatx4_t& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)a, (bf16x8_t)b, c, 0, 0, 0);
+}
+// the same MFMA on fp16 operands (same cycles on gfx950)
+__device__ __forceinline__ floatx4_t mfma16h(const short8_t& a, const short8_t& b, const floatx4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b), c,
+                                                0, 0, 0);
 }
 
 // fp32 -> bf16 bits, round-to-nearest-even.  A plain cast lowers to the

@@ -17,7 +17,9 @@
 //           db1 / db2 are computed here from the LDS images as one fp32
 //           partial row per 64 rows, so H2 and dZ never reach HBM.
 //   K_wgrad (mlp_wgrad_kernel) grouped split-K GEMM dW = dH^T . A over the
-//           batch for dW1 (A = raw u8 X) and dW2 (A = H1): 256x128 tiles; both
+//           batch for dW1 (A = raw u8 X, taken as the exact fp16 1024 + u
+//           against a power-of-two-scaled fp16 dH1: one v_perm per two
+//           elements) and dW2 (A = H1, bf16): 256x128 tiles; both
 //           operands stream global -> LDS by LDS-DMA (global_load_lds_dwordx4,
 //           no VGPR staging) into a 3-slot ring of XOR-swizzled [64 batch
 //           rows][128] images (two stages in flight, counted vmcnt + raw
@@ -138,9 +140,10 @@ struct MlpRowArgs {
   const uint16_t *w1h, *w2h, *w3h, *w2th, *w3th;
   const float *b1, *b2, *b3;
   float xa, xb, grad_scale;
+  float dh1_scale;                     // dH1 goes to HBM as fp16 of dH1 * dh1_scale (a power of two)
   uint16_t* h1;                        // row-major [batch][256]
   float* w3p;                          // [batch / 64][W3P_LD] partial [dW3 | db3 | db1 | db2]
-  uint16_t *dh2, *dh1;                 // row-major [batch][256]
+  uint16_t *dh2, *dh1;                 // row-major [batch][256]: dH2 bf16, dH1 fp16 (scaled)
   float *loss, *correct, *logits;
   unsigned long long* stamps;  // diagnostics: per-workgroup phase timestamps (nullptr in production)
 };
@@ -207,6 +210,25 @@ __device__ __forceinline__ void copy_out(const uint16_t* src, int ld, uint16_t* 
   for (int q = tid; q < BM * CPR; q += NT) {
     const int r = q / CPR, c = (q - r * CPR) * 8;
     *reinterpret_cast<short8_t*>(dst + (long)r * gld + c) = *reinterpret_cast<const short8_t*>(src + r * ld + c);
+  }
+}
+
+// copy_out of a bf16 image to fp16 rows, scaled by a power of two (exact for the
+// normal range): the dH1 operand of the weight gradient's fp16 dW1 GEMM.
+template <int BM, int NT, int NCOLS>
+__device__ __forceinline__ void copy_out_f16(const uint16_t* src, int ld, uint16_t* dst, int gld, int tid, float scale) {
+  constexpr int CPR = NCOLS / 8;
+#pragma unroll
+  for (int q = tid; q < BM * CPR; q += NT) {
+    const int r = q / CPR, c = (q - r * CPR) * 8;
+    const short8_t v = *reinterpret_cast<const short8_t*>(src + r * ld + c);
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float f0 = bf2f((uint16_t)v[2 * j]) * scale, f1 = bf2f((uint16_t)v[2 * j + 1]) * scale;
+      w[j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(f0, f1));
+    }
+    *reinterpret_cast<uint4*>(dst + (long)r * gld + c) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
@@ -660,7 +682,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
     masked_out(R1);
   }
   __syncthreads();
-  copy_out<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid);
+  copy_out_f16<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid, a.dh1_scale);
   col_sums(R1, W3P_DB1);
   stamp(9);
 }
@@ -974,6 +996,23 @@ __device__ __forceinline__ short8_t u8x8_exact_bf16(uint2v_t v) {
   return __builtin_bit_cast(short8_t, u32x4{w[0], w[1], w[2], w[3]});
 }
 
+// 8 u8 -> 8 fp16 of (1024 + u), exact: fp16 steps by 1 over [1024, 2048), so the bits are
+// 0x6400 | u and one v_perm_b32 builds two of them (the bf16 form above costs 1.5 VALU per
+// element).  dW1 is then dH1^T (X + 1024); mlp_sgd_kernel removes the 1024 db1 term.
+__device__ __forceinline__ short8_t u8x8_f16_biased(uint2v_t v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(short8_t, u32x4{__builtin_amdgcn_perm(0x64646464u, v[0], 0x04010400u),
+                                            __builtin_amdgcn_perm(0x64646464u, v[0], 0x04030402u),
+                                            __builtin_amdgcn_perm(0x64646464u, v[1], 0x04010400u),
+                                            __builtin_amdgcn_perm(0x64646464u, v[1], 0x04030402u)});
+}
+// dW1 tiles (U8: dH1 fp16 x biased-fp16 X) and dW2 tiles (bf16) share the main loops
+template <bool U8>
+__device__ __forceinline__ floatx4_t wg_mma(const short8_t& b, const short8_t& a, const floatx4_t& c) {
+  if constexpr (U8) return mfma16h(b, a, c);
+  else return mfma16(b, a, c);
+}
+
 // vmcnt needs an immediate: wait until this wave has at most N younger stages
 // (of PPS LDS-DMA pieces each) in flight.
 template <int PPS>
@@ -1152,7 +1191,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (U8) {
 #pragma unroll
-          for (int j = 0; j < NB; ++j) b0[j] = u8x8_exact_bf16(r0[j]);
+          for (int j = 0; j < NB; ++j) b0[j] = u8x8_f16_biased(r0[j]);
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -1163,18 +1202,18 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(b0[j], a0[i], acc[i][j]);
+          for (int j = 0; j < NB; ++j) acc[i][j] = wg_mma<U8>(b0[j], a0[i], acc[i][j]);
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (U8) {
 #pragma unroll
-          for (int j = 0; j < NB; ++j) b1[j] = u8x8_exact_bf16(r1[j]);
+          for (int j = 0; j < NB; ++j) b1[j] = u8x8_f16_biased(r1[j]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
+          for (int j = 0; j < NB; ++j) acc[i][j] = wg_mma<U8>(b1[j], a1[i], acc[i][j]);
       }
     }
   };
@@ -1226,13 +1265,13 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
           short8_t b[NBR];
 #pragma unroll
           for (int j = 0; j < NB; ++j) {
-            if constexpr (U8) b[j] = u8x8_exact_bf16(fr[S][k][j]);
+            if constexpr (U8) b[j] = u8x8_f16_biased(fr[S][k][j]);
             else b[j] = fb[S][k][j];
           }
 #pragma unroll
           for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
-            for (int j = 0; j < NB; ++j) acc[i][j] = mfma16(b[j], fa[S][k][i], acc[i][j]);
+            for (int j = 0; j < NB; ++j) acc[i][j] = wg_mma<U8>(b[j], fa[S][k][i], acc[i][j]);
         }
       }
     };
@@ -1288,9 +1327,9 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int j = q / WG_MI, i = q % WG_MI;
-            if (j < NB) acc[i][j] = mfma16(fc[C][k][j], fa[C][k][i], acc[i][j]);
+            if (j < NB) acc[i][j] = wg_mma<U8>(fc[C][k][j], fa[C][k][i], acc[i][j]);
             if (k == 0 && q % WG_MI == 1 && j < NB) {
-              fc[C][1][j] = u8x8_exact_bf16(fr[C][1][j]);
+              fc[C][1][j] = u8x8_f16_biased(fr[C][1][j]);
               asm volatile("" : "+v"(fc[C][1][j]));
             }
             if (k == 1 && q == 8) {
@@ -1301,7 +1340,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
             }
             if (k == 1 && q >= 8 && (q & 1) == 0 && ((q - 8) >> 1) < NB) {
               short8_t& d = fc[N][0][(q - 8) >> 1];
-              d = u8x8_exact_bf16(fr[N][0][(q - 8) >> 1]);
+              d = u8x8_f16_biased(fr[N][0][(q - 8) >> 1]);
               asm volatile("" : "+v"(d));  // keep it here (LLVM sinks it past the back edge otherwise)
             }
             reads_after(sbn, k, q, nxt_c);
@@ -1321,7 +1360,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
               b[j] = __builtin_bit_cast(short8_t, u32x4k{fr[C][k][j][0], fr[C][k][j][1], fr[C][k][j][0], fr[C][k][j][1]});
             }
 #else
-            if constexpr (U8) b[j] = u8x8_exact_bf16(fr[C][k][j]);
+            if constexpr (U8) b[j] = u8x8_f16_biased(fr[C][k][j]);
 #endif
             else b[j] = fb[C][k][j];
           }
@@ -1329,7 +1368,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
           for (int q = 0; q < 16; ++q) {
             const int i = q / WG_NJ, j = q % WG_NJ;
 #if SL_WG_KO != 4  // 4: no DMA and no MFMAs (reads + barriers only)
-            if (j < NB) acc[i][j] = mfma16(b[j], fa[C][k][i], acc[i][j]);
+            if (j < NB) acc[i][j] = wg_mma<U8>(b[j], fa[C][k][i], acc[i][j]);
 #endif
             reads_after(sbn, k, q, nxt_c);
           }
@@ -1350,7 +1389,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #if SL_WG_CVT
     if constexpr (U8) {
 #pragma unroll
-      for (int j = 0; j < NB; ++j) fc[0][0][j] = u8x8_exact_bf16(fr[0][0][j]);
+      for (int j = 0; j < NB; ++j) fc[0][0][j] = u8x8_f16_biased(fr[0][0][j]);
     }
 #endif
     for (int st = 0; st < nst; st += 2) {
@@ -1411,7 +1450,9 @@ struct SgdArgs {
   float* grad_out;       // reduced gradient written here (all-reduce hand-off)
   long n;
   float lr, mu, wd;
-  float xa, xb;  // input normalisation: the slabs hold dH1^T X for raw u8 X (see mlp_wgrad_kernel)
+  // dW1 = xa * (slab dW1 rows) + xb * db1: the slabs hold s dH1^T (X + 1024) for raw u8 X (fp16 GEMM,
+  // see mlp_wgrad_kernel), so the host passes xa = xa_norm / s, xb = xb_norm - 1024 xa_norm
+  float xa, xb;
   int mode;  // 0: refresh bf16 shadows from w; 1: reduce only (grad_out); 2: reduce/read + update
   uint16_t *w1h, *w2h, *w2th, *w3h, *w3th;
   int* cursor;
@@ -1554,7 +1595,7 @@ __global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
 
 // Multi-GPU update (after sl_xgmi_barrier): one thread per 4 parameters sums the W ranks' reduced gradients
 // straight out of their exchange buffers over xGMI (rank order: identical on every
-// replica), then applies momentum SGD and refreshes the bf16 shadows -- the all-reduce
+// replica) -- or, two-shot, reads the chunk owner's all-reduced value -- then applies momentum SGD and refreshes the bf16 shadows -- the all-reduce
 // and the optimizer step in one launch, no RCCL call and no host sync (xgmi.h).
 __global__ __launch_bounds__(256) void mlp_sgd_xgmi_kernel(SgdArgs a, XgArgs x) {
   __shared__ unsigned s_step;
@@ -1562,18 +1603,26 @@ __global__ __launch_bounds__(256) void mlp_sgd_xgmi_kernel(SgdArgs a, XgArgs x) 
   const unsigned s = xg_block_step(x, &s_step);  // xgmi_barrier_kernel ran just before
   const long p0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (p0 < a.n) {
-    float4 v[XG_MAX_WORLD];
+    float4 g;
+    float4 w4, m4;
+    if (x.chunk4 > 0) {  // two-shot: the chunk's owner already summed it (xgmi_rs_kernel)
+      g = xg_load_reduced(x, s, p0 / 4);
+      w4 = *reinterpret_cast<const float4*>(a.w + p0);
+      m4 = a.mom ? *reinterpret_cast<const float4*>(a.mom + p0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      float4 v[XG_MAX_WORLD];
 #pragma unroll
-    for (int q = 0; q < XG_MAX_WORLD; ++q)
-      if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), xg_slot_off(x, s) + (unsigned)(p0 * 4));
-    const float4 w4 = *reinterpret_cast<const float4*>(a.w + p0);
-    const float4 m4 = a.mom ? *reinterpret_cast<const float4*>(a.mom + p0) : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 g = v[0];
+      for (int q = 0; q < XG_MAX_WORLD; ++q)
+        if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), xg_slot_off(x, s) + (unsigned)(p0 * 4));
+      w4 = *reinterpret_cast<const float4*>(a.w + p0);
+      m4 = a.mom ? *reinterpret_cast<const float4*>(a.mom + p0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      g = v[0];
 #pragma unroll
-    for (int q = 1; q < XG_MAX_WORLD; ++q)
-      if (q < x.world) {
-        g.x += v[q].x; g.y += v[q].y; g.z += v[q].z; g.w += v[q].w;
-      }
+      for (int q = 1; q < XG_MAX_WORLD; ++q)
+        if (q < x.world) {
+          g.x += v[q].x; g.y += v[q].y; g.z += v[q].z; g.w += v[q].w;
+        }
+    }
     const float ga[4] = {g.x, g.y, g.z, g.w}, wa[4] = {w4.x, w4.y, w4.z, w4.w}, ma[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -1611,7 +1660,7 @@ int sl_mlp_rows_bm(int batch) {
 
 int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_batches, int batch,
                 const uint16_t* w1h, const uint16_t* w2h, const uint16_t* w3h, const uint16_t* w2th,
-                const uint16_t* w3th, const float* params, float xa, float xb, float grad_scale,
+                const uint16_t* w3th, const float* params, float xa, float xb, float grad_scale, float dh1_scale,
                 uint16_t* h1, float* w3p, uint16_t* dh2, uint16_t* dh1,
                 float* loss, float* correct, float* logits, int train, hipStream_t stream) {
   if (batch <= 0 || batch % BM != 0) return -1;
@@ -1619,7 +1668,7 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.x = x; a.y = y; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
   a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th;
   a.b1 = params + P_B1; a.b2 = params + P_B2; a.b3 = params + P_B3;
-  a.xa = xa; a.xb = xb; a.grad_scale = grad_scale;
+  a.xa = xa; a.xb = xb; a.grad_scale = grad_scale; a.dh1_scale = dh1_scale;
   a.h1 = h1; a.w3p = w3p; a.dh2 = dh2; a.dh1 = dh1;
   a.loss = loss; a.correct = correct; a.logits = logits;
   a.stamps = g_stamps;
@@ -1728,15 +1777,16 @@ int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa
 
 int sl_mlp_sgd_xgmi(float* w, float* mom, float lr, float mu, float wd, uint16_t* w1h, uint16_t* w2h,
                     uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, char* const* bases, unsigned* ctl,
-                    long slot_bytes, int rank, int world, hipStream_t stream) {
+                    long slot_bytes, int rank, int world, long chunk4, hipStream_t stream) {
   if (!w || !bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return -1;
   if (slot_bytes < ((P_N + 3) / 4) * 16 || (slot_bytes & 255)) return -1;
+  if (chunk4 < 0 || (chunk4 > 0 && (chunk4 * world * 16 < slot_bytes || (chunk4 & 63)))) return -1;
   if (((uintptr_t)w | (uintptr_t)(mom ? mom : w)) & 15) return -2;
   SgdArgs a = {};
   a.w = w; a.mom = mom; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = 2;
   a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
   XgArgs x;
-  x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world;
+  x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world; x.chunk4 = chunk4;
   const long groups = (P_N + 3) / 4;
   hipLaunchKernelGGL(mlp_sgd_xgmi_kernel, dim3((groups + 255) / 256), dim3(256), 0, stream, a, x);
   SL_CHECK_LAUNCH();

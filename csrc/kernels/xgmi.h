@@ -8,9 +8,11 @@
 // whole exchange is capturable in a hipGraph.
 //
 // Buffer layout (bytes):
-//   [0, XG_HDR)                       inbox: flag of rank q at q * 64 -- the last step id q signalled
+//   [0, XG_HDR)                       inboxes: set b's flag of rank q at b * 1024 + q * 64 -- the last
+//                                     step id q signalled through barrier b (b = 0, 1)
 //   [XG_HDR, XG_HDR + slot)           payload slot 0 (even step ids)
 //   [XG_HDR + slot, XG_HDR + 2 slot)  payload slot 1 (odd step ids)
+//   [XG_HDR + 2 slot, + 4 slot)       reduced slots 0 / 1 (two-shot only; rank r fills its own chunk)
 //
 // Per step (step id s = completed steps + 1, kept on the device so graph
 // replays count on their own):
@@ -25,6 +27,19 @@
 // (s & 1) again only at step s + 2, which it reaches after passing barrier
 // s + 1 -- and every peer signals s + 1 only after its step-s consumer kernel
 // (the reader of that slot) has finished.
+//
+// Two-shot variant (chunk4 > 0; reduce-scatter + all-gather): one-shot moves W - 1
+// whole payloads into every GPU, (W - 1) x 1.08 MB over 7 links for the MLP at W = 8.
+// Two-shot moves 2 (W - 1) / W of one payload instead, for one more barrier:
+//   2'. barrier set 0 as above;
+//   3'. xgmi_rs_kernel: rank r sums float4 chunk [r chunk4, (r + 1) chunk4) of every
+//       rank's slot (s & 1), rank order, into the same offsets of ITS reduced slot (s & 1);
+//   4'. barrier set 1 (same step id s, second inbox set);
+//   5'. the consumer reads element i's reduced value from rank i / chunk4's reduced slot.
+// Each element is summed by exactly one rank, in rank order, and every replica applies
+// the same bits, so replicas stay identical.  Hazards are those of one-shot: a rank
+// rewrites reduced slot (s & 1) at step s + 2, after barrier set 0 of step s + 1, which
+// every peer signals only after its step-s consumer (the last reader) has finished.
 #pragma once
 #include "common.h"
 
@@ -39,11 +54,15 @@ struct XgArgs {
   unsigned* ctl;       // local: [0] completed steps, [1] finished-block counter, [2] error (1 = timeout)
   long slot_bytes;     // payload slot size, multiple of 256
   int rank, world;
+  long chunk4;         // two-shot: float4 elements reduced by each rank, multiple of 64 (0 = one-shot)
 };
 
-__device__ __forceinline__ unsigned* xg_inbox(char* base, int q) {
-  return reinterpret_cast<unsigned*>(base + (long)q * 64);
+__device__ __forceinline__ unsigned* xg_inbox(char* base, int q, int set) {
+  return reinterpret_cast<unsigned*>(base + (long)set * 1024 + (long)q * 64);
 }
+
+// Bytes of one exchange buffer (both payload slots, both reduced slots).
+__host__ __device__ constexpr long xg_buffer_bytes(long slot_bytes) { return XG_HDR + 4 * slot_bytes; }
 
 __device__ __forceinline__ char* xg_slot(const XgArgs& x, int q, unsigned s) {
   return x.bases[q] + XG_HDR + (long)(s & 1u) * x.slot_bytes;
@@ -54,7 +73,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t xg_rsrc(const XgArgs& x, int q
   const unsigned long long b = reinterpret_cast<unsigned long long>(x.bases[q]);
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b), hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
   char* base = reinterpret_cast<char*>(((unsigned long long)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(XG_HDR + 2 * x.slot_bytes), 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)xg_buffer_bytes(x.slot_bytes), 0x00020000);
 }
 
 // 16-byte payload load at system scope (sc0 sc1): served from memory, never from a line an
@@ -70,6 +89,19 @@ __device__ __forceinline__ unsigned xg_slot_off(const XgArgs& x, unsigned s) {
   return (unsigned)(XG_HDR + (long)(s & 1u) * x.slot_bytes);
 }
 
+// Byte offset of reduced slot (s & 1) (two-shot).
+__device__ __forceinline__ unsigned xg_red_off(const XgArgs& x, unsigned s) {
+  return (unsigned)(XG_HDR + (long)(2u + (s & 1u)) * x.slot_bytes);
+}
+
+// Two-shot consumer read: float4 element i of the all-reduced payload, from its owner's
+// reduced slot.  One-shot callers sum the W slots themselves.  chunk4 is a multiple of 64,
+// so the 64 consecutive elements of a wave share one owner (xg_rsrc is wave-uniform).
+__device__ __forceinline__ float4 xg_load_reduced(const XgArgs& x, unsigned s, long i) {
+  const int owner = (int)(i / x.chunk4);
+  return xg_load(xg_rsrc(x, owner), xg_red_off(x, s) + (unsigned)(i * 16));
+}
+
 // Step id of the step in flight (completed + 1), for producers that pick the slot.
 __device__ __forceinline__ unsigned xg_step(const unsigned* ctl) {
   return __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -83,13 +115,13 @@ __device__ __forceinline__ unsigned xg_step(const unsigned* ctl) {
 // matters: a consumer grid whose every block spun would hold every CU while it
 // waits, and ranks that share a GPU (tests) could then never run the peer's
 // producer kernels.
-__device__ __forceinline__ void xg_signal_wait(const XgArgs& x) {
+__device__ __forceinline__ void xg_signal_wait(const XgArgs& x, int set) {
   const int lane = threadIdx.x;
   const unsigned s = xg_step(x.ctl);
   if (lane < x.world)
-    __hip_atomic_store(xg_inbox(x.bases[lane], x.rank), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(xg_inbox(x.bases[lane], x.rank, set), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (lane < x.world) {
-    unsigned* f = xg_inbox(x.bases[x.rank], lane);
+    unsigned* f = xg_inbox(x.bases[x.rank], lane, set);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - s) < 0) {
       __builtin_amdgcn_s_sleep(2);

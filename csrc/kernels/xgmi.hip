@@ -19,25 +19,56 @@ __global__ __launch_bounds__(256) void xgmi_copyin_kernel(XgArgs x, const float4
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) dst[i] = src[i];
 }
 
-__global__ __launch_bounds__(64) void xgmi_barrier_kernel(XgArgs x) { xg_signal_wait(x); }
+__global__ __launch_bounds__(64) void xgmi_barrier_kernel(XgArgs x, int set) { xg_signal_wait(x, set); }
 
-// out = scale * sum_q slot_q (rank order); runs after xgmi_barrier_kernel.
-__global__ __launch_bounds__(256) void xgmi_sum_kernel(XgArgs x, float4* __restrict__ out, long n4, float scale) {
+// Two-shot reduce-scatter (after barrier set 0): this rank's chunk of the W slots,
+// summed in rank order into the same offsets of its own reduced slot.
+__global__ __launch_bounds__(256) void xgmi_rs_kernel(XgArgs x, long n4) {
   __shared__ unsigned s_step;
   const unsigned s = xg_block_step(x, &s_step);
   const unsigned off0 = xg_slot_off(x, s);
+  float4* red = reinterpret_cast<float4*>(x.bases[x.rank] + xg_red_off(x, s));
+  const long lo = (long)x.rank * x.chunk4;
+  const long hi = lo + x.chunk4 < n4 ? lo + x.chunk4 : n4;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  for (long i = lo + (long)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += stride) {
     float4 v[XG_MAX_WORLD];
 #pragma unroll
     for (int q = 0; q < XG_MAX_WORLD; ++q)
-      if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), off0 + (unsigned)(i * 16));  // all W loads in flight
+      if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), off0 + (unsigned)(i * 16));
     float4 acc = v[0];
 #pragma unroll
     for (int q = 1; q < XG_MAX_WORLD; ++q)
       if (q < x.world) {
         acc.x += v[q].x; acc.y += v[q].y; acc.z += v[q].z; acc.w += v[q].w;
       }
+    red[i] = acc;
+  }
+}
+
+// out = scale * sum_q slot_q (rank order); runs after xgmi_barrier_kernel (two-shot: after
+// xgmi_rs_kernel and barrier set 1, reading each chunk from its owner's reduced slot).
+__global__ __launch_bounds__(256) void xgmi_sum_kernel(XgArgs x, float4* __restrict__ out, long n4, float scale) {
+  __shared__ unsigned s_step;
+  const unsigned s = xg_block_step(x, &s_step);
+  const unsigned off0 = xg_slot_off(x, s);
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 acc;
+    if (x.chunk4 > 0) {
+      acc = xg_load_reduced(x, s, i);
+    } else {
+      float4 v[XG_MAX_WORLD];
+#pragma unroll
+      for (int q = 0; q < XG_MAX_WORLD; ++q)
+        if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), off0 + (unsigned)(i * 16));  // all W loads in flight
+      acc = v[0];
+#pragma unroll
+      for (int q = 1; q < XG_MAX_WORLD; ++q)
+        if (q < x.world) {
+          acc.x += v[q].x; acc.y += v[q].y; acc.z += v[q].z; acc.w += v[q].w;
+        }
+    }
     acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
     out[i] = acc;
   }
@@ -60,16 +91,21 @@ static int xg_grid(long n4) {
   return (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
 }
 
-static bool xg_args(XgArgs& x, char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world) {
+static bool xg_args(XgArgs& x, char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4) {
   if (!bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return false;
   if (slot_bytes <= 0 || (slot_bytes & 255)) return false;
-  x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world;
+  // two-shot: the W chunks must cover the slot, and be whole waves of float4 (a consumer wave
+  // then reads ONE owner's buffer: xg_rsrc makes the owner wave-uniform with readfirstlane)
+  if (chunk4 < 0 || (chunk4 > 0 && (chunk4 * world * 16 < slot_bytes || (chunk4 & 63)))) return false;
+  x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world; x.chunk4 = chunk4;
   return true;
 }
 
 extern "C" {
 
 int sl_xgmi_header_bytes() { return (int)XG_HDR; }
+
+long sl_xgmi_buffer_bytes(long slot_bytes) { return xg_buffer_bytes(slot_bytes); }
 
 // Uncached device allocation (the exchange buffer), zero-filled.
 int sl_xgmi_alloc(long bytes, void** out) {
@@ -102,10 +138,10 @@ int sl_ipc_open(const void* handle, void** out) {
 
 int sl_ipc_close(void* p) { return p ? (int)hipIpcCloseMemHandle(p) : 0; }
 
-int sl_xgmi_copyin(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, const float* src, long n,
+int sl_xgmi_copyin(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, const float* src, long n,
                    hipStream_t stream) {
   XgArgs x;
-  if (!xg_args(x, bases, ctl, slot_bytes, rank, world) || !src || (n & 3) || n * 4 > slot_bytes) return -1;
+  if (!xg_args(x, bases, ctl, slot_bytes, rank, world, chunk4) || !src || (n & 3) || n * 4 > slot_bytes) return -1;
   if ((uintptr_t)src & 15) return -2;
   hipLaunchKernelGGL(xgmi_copyin_kernel, dim3(xg_grid(n / 4)), dim3(256), 0, stream, x,
                      reinterpret_cast<const float4*>(src), n / 4);
@@ -113,18 +149,30 @@ int sl_xgmi_copyin(char* const* bases, unsigned* ctl, long slot_bytes, int rank,
   return 0;
 }
 
-int sl_xgmi_barrier(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, hipStream_t stream) {
+int sl_xgmi_barrier(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, int set,
+                    hipStream_t stream) {
   XgArgs x;
-  if (!xg_args(x, bases, ctl, slot_bytes, rank, world)) return -1;
-  hipLaunchKernelGGL(xgmi_barrier_kernel, dim3(1), dim3(64), 0, stream, x);
+  if (!xg_args(x, bases, ctl, slot_bytes, rank, world, chunk4) || set < 0 || set > 1) return -1;
+  hipLaunchKernelGGL(xgmi_barrier_kernel, dim3(1), dim3(64), 0, stream, x, set);
   SL_CHECK_LAUNCH();
   return 0;
 }
 
-int sl_xgmi_sum(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, float* out, long n,
+// Two-shot reduce-scatter of n floats (run between barrier sets 0 and 1).
+int sl_xgmi_rs(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, long n,
+               hipStream_t stream) {
+  XgArgs x;
+  if (!xg_args(x, bases, ctl, slot_bytes, rank, world, chunk4) || chunk4 <= 0 || (n & 3) || n * 4 > slot_bytes)
+    return -1;
+  hipLaunchKernelGGL(xgmi_rs_kernel, dim3(xg_grid(chunk4)), dim3(256), 0, stream, x, n / 4);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_xgmi_sum(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, float* out, long n,
                 float scale, hipStream_t stream) {
   XgArgs x;
-  if (!xg_args(x, bases, ctl, slot_bytes, rank, world) || !out || (n & 3) || n * 4 > slot_bytes) return -1;
+  if (!xg_args(x, bases, ctl, slot_bytes, rank, world, chunk4) || !out || (n & 3) || n * 4 > slot_bytes) return -1;
   if ((uintptr_t)out & 15) return -2;
   hipLaunchKernelGGL(xgmi_sum_kernel, dim3(xg_grid(n / 4)), dim3(256), 0, stream, x, reinterpret_cast<float4*>(out),
                      n / 4, scale);
@@ -132,10 +180,10 @@ int sl_xgmi_sum(char* const* bases, unsigned* ctl, long slot_bytes, int rank, in
   return 0;
 }
 
-int sl_xgmi_peek(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, int q, int parity,
+int sl_xgmi_peek(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, int q, int parity,
                  int mode, float* out, long n, hipStream_t stream) {
   XgArgs x;
-  if (!xg_args(x, bases, ctl, slot_bytes, rank, world) || !out || (n & 3) || n * 4 > slot_bytes) return -1;
+  if (!xg_args(x, bases, ctl, slot_bytes, rank, world, chunk4) || !out || (n & 3) || n * 4 > slot_bytes) return -1;
   if (q < 0 || q >= world) return -1;
   hipLaunchKernelGGL(xgmi_peek_kernel, dim3(xg_grid(n / 4)), dim3(256), 0, stream, x, q, (unsigned)parity, mode,
                      reinterpret_cast<float4*>(out), n / 4);

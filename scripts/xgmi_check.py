@@ -2,11 +2,11 @@
 """Multi-rank check of the xGMI exchange (parallel/xgmi.py, csrc/kernels/xgmi.*).
 
 Launched by tests/test_xgmi_gpu.py as
-``torchrun --nproc-per-node W scripts/xgmi_check.py [--same-device]``: every rank
+``torchrun --nproc-per-node W scripts/xgmi_check.py [--same-device] [--two-shot]``: every rank
 maps every other rank's exchange buffer over IPC (on one GPU the ranks share the
 device -- the same code path minus the xGMI links).  Checks, per rank:
 
-1. the generic one-shot all-reduce equals the rank-order fp32 sum, over several
+1. the generic all-reduce (one-shot, or reduce-scatter + all-gather with ``--two-shot``) equals the rank-order fp32 sum, over several
    calls (both slot parities, device-side step counter);
 2. the MLP step with the all-reduce fused into its update kernel gives exactly the
    parameters of the same step with gloo's all-reduce of the reduced gradient,
@@ -33,6 +33,7 @@ def _same(p, q, msg):
 
 def main() -> int:
     same = "--same-device" in sys.argv
+    two = "--two-shot" in sys.argv
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev = torch.device("cuda", 0 if same else int(os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(dev)
@@ -43,7 +44,7 @@ def main() -> int:
 
     # 1. generic all-reduce
     n = 100_000
-    ex = XgmiExchange(n, rank, world, dev, *dist_collectives())
+    ex = XgmiExchange(n, rank, world, dev, *dist_collectives(), two_shot=two)
     for it in range(5):
         gens = [torch.Generator().manual_seed(1000 * it + q) for q in range(world)]
         parts = [torch.randn(n, generator=g) for g in gens]
@@ -67,7 +68,7 @@ def main() -> int:
     b = FusedMLPTrainer(batch=B, device=dev, world_size=world, seed=0)
     a.load_shard(xt, yt)
     b.load_shard(xt, yt)
-    xa = XgmiExchange(a.n_pad, rank, world, dev, *dist_collectives())
+    xa = XgmiExchange(a.n_pad, rank, world, dev, *dist_collectives(), two_shot=two)
     a.enable_xgmi(xa)
 
     def host_allreduce(g):
@@ -125,7 +126,7 @@ def main() -> int:
     dist.barrier()
     torch.cuda.synchronize()
     xa.close()
-    print(f"XGMI_CHECK_OK rank={rank} steps={done} loss={a.stats().loss:.4f}", flush=True)
+    print(f"XGMI_CHECK_OK rank={rank} two_shot={two} steps={done} loss={a.stats().loss:.4f}", flush=True)
     dist.destroy_process_group()
     return 0
 

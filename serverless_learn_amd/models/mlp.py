@@ -318,10 +318,22 @@ class FusedMLPTrainer:
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
                None, n.stream_ptr())
 
+    @property
+    def dh1_scale(self) -> float:
+        """Power of two that brings grad_scale-sized dH1 values to O(1) before the rows kernel
+        stores them as fp16 for the weight gradient (fp16 would flush them to subnormals)."""
+        return 2.0 ** round(-math.log2(self.grad_scale))
+
+    @property
+    def dw1_coeffs(self) -> tuple:
+        """(a, b) with dW1 = a * slab + b * db1: the slab holds s dH1^T (X + 1024) (fp16 GEMM on
+        raw pixels), and dW1 of the normalised input xa X + xb is xa dH1^T X + xb db1."""
+        return self.xa / self.dh1_scale, self.xb - 1024.0 * self.xa
+
     def _launches(self):
         """Cached launches for the current buffers/hyper-parameters (rebuilt on change)."""
         key = (self.x.data_ptr() if self.x is not None else 0, self.n_batches, self.grad_scale, self.lr,
-               self.momentum, self.weight_decay, id(self.xgmi))
+               self.momentum, self.weight_decay, id(self.xgmi), bool(self.xgmi and self.xgmi.two_shot))
         if getattr(self, "_lkey", None) == key:
             return self._lc
         n, p = self._n, self._n.ptr
@@ -329,7 +341,7 @@ class FusedMLPTrainer:
         lc = {
             "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
                              p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
-                             p(self.params), self.xa, self.xb, self.grad_scale,
+                             p(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                              p(self.h1t), p(self.w3p), p(self.dh2t), p(self.dh1t),
                              p(self.loss), p(self.correct), None, 2 if self.l1_gemm else 1),
             "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
@@ -345,13 +357,13 @@ class FusedMLPTrainer:
             lc[name] = n.Launch("sl_mlp_sgd", p(self.params), p(self.mom),
                                 None if from_grad else p(self.slab), self.slices, self.n_pad,
                                 p(self.grad) if from_grad else None, p(self.grad) if grad_out else None,
-                                self.lr, self.momentum, self.weight_decay, self.xa, self.xb, mode, *ws,
+                                self.lr, self.momentum, self.weight_decay, *self.dw1_coeffs, mode, *ws,
                                 p(self.cursor) if bump else None)
         if self.xgmi is not None:
             xg = self.xgmi
-            lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.n_pad, self.xa, self.xb,
+            lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.n_pad, *self.dw1_coeffs,
                                      xg.slot_ptr(0), xg.slot_ptr(1), xg.ctl.data_ptr())
-            lc["xbarrier"] = n.Launch("sl_xgmi_barrier", *xg.args())
+            lc["xbarrier"] = [n.Launch(fn, *xg.args(), *extra) for fn, extra in xg.exchange_launches(self.n_pad)]
             lc["xupdate"] = n.Launch("sl_mlp_sgd_xgmi", p(self.params), p(self.mom), self.lr, self.momentum,
                                      self.weight_decay, *ws, p(self.cursor), *xg.args())
         self._lc, self._lkey = lc, key
@@ -366,7 +378,7 @@ class FusedMLPTrainer:
         n = self._n
         n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, self.grad_scale,
+               n.ptr(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                n.ptr(self.h1t), n.ptr(self.w3p), n.ptr(self.dh2t), n.ptr(self.dh1t),
                n.ptr(self.loss), n.ptr(self.correct), None, 0, n.stream_ptr())
 
@@ -421,7 +433,8 @@ class FusedMLPTrainer:
         if self.xgmi is not None:
             lc = self._launches()
             lc["xreduce"]()
-            lc["xbarrier"]()
+            for launch in lc["xbarrier"]:
+                launch()
             lc["xupdate"]()
         elif self.allreduce is None:
             self._sgd(2, from_grad=False, grad_out=False)
@@ -466,7 +479,7 @@ class FusedMLPTrainer:
         corr = torch.zeros(rows, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
                n.ptr(loss), n.ptr(corr), None, 0, n.stream_ptr())
         return StepStats(float(loss.mean()), float(corr.mean()), rows)
 
@@ -479,7 +492,7 @@ class FusedMLPTrainer:
         out = torch.empty(rows, CLASSES, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
                None, None, n.ptr(out), 0, n.stream_ptr())
         return out
 

@@ -30,7 +30,7 @@ F = ctypes.c_float
 # name -> argtypes (restype is always c_int unless listed in _RESTYPE)
 _SIGS: dict[str, list] = {
     "sl_mlp_param_count": [],
-    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, P, P, P, P, P, P, P, I, P],
+    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P],
     "sl_mlp_wgrad": [I, P, P, I, P, P, P, P, I, P, I, L, P],
     "sl_mlp_wgrad_slices": [I, I],
     "sl_mlp_l1": [P, P, I, I, P, P, F, F, P, P],
@@ -41,7 +41,7 @@ _SIGS: dict[str, list] = {
     "sl_mlp_set_stamps": [P],
     "sl_mlp_sgd": [P, P, P, I, L, P, P, F, F, F, F, F, I, P, P, P, P, P, P, P],
     "sl_mlp_reduce_xgmi": [P, I, L, F, F, P, P, P, P],
-    "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, P],
+    "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, L, P],
 }
 _RESTYPE = {"sl_mlp_param_count": ctypes.c_long}
 

@@ -1,4 +1,4 @@
-"""One-shot all-reduce over xGMI through IPC-mapped peer buffers.
+"""One-shot / two-shot all-reduce over xGMI through IPC-mapped peer buffers.
 
 Inside a node the 8 MI355X are fully connected by xGMI (7 links per GPU).  For
 the MLP's 1.08 MB gradient a ring all-reduce pays 2(W-1) latency-bound hops per
@@ -7,6 +7,11 @@ concurrent reads, one per link) and sums in rank order inside a kernel --
 protocol and memory-ordering argument in ``csrc/kernels/xgmi.h``.  The exchange
 needs no host synchronisation, so the whole multi-GPU step (forward, backward,
 all-reduce, optimizer) is captured in one hipGraph like the 1-GPU step.
+
+``two_shot=True`` switches to reduce-scatter + all-gather through the same buffers: each
+rank sums only its 1/W chunk of the W payloads, and consumers read every chunk from its
+owner -- 2(W-1)/W of a payload crosses each GPU's links instead of W-1 payloads, for one
+more barrier.  Which one wins depends on W and the links (``bench.py`` times both).
 
 Setup is collective: every rank allocates one uncached exchange buffer, exports
 it with ``hipIpcGetMemHandle``, the 64-byte handles are all-gathered over the
@@ -35,10 +40,12 @@ N.register("sl_ipc_get_handle", [N.P, N.P])
 N.register("sl_ipc_handle_size", [])
 N.register("sl_ipc_open", [N.P, ctypes.POINTER(ctypes.c_void_p)])
 N.register("sl_ipc_close", [N.P])
-N.register("sl_xgmi_copyin", [N.P, N.P, N.L, N.I, N.I, N.P, N.L, N.P])
-N.register("sl_xgmi_barrier", [N.P, N.P, N.L, N.I, N.I, N.P])
-N.register("sl_xgmi_sum", [N.P, N.P, N.L, N.I, N.I, N.P, N.L, N.F, N.P])
-N.register("sl_xgmi_peek", [N.P, N.P, N.L, N.I, N.I, N.I, N.I, N.I, N.P, N.L, N.P])
+N.register("sl_xgmi_buffer_bytes", [N.L], restype=ctypes.c_long)
+N.register("sl_xgmi_copyin", [N.P, N.P, N.L, N.I, N.I, N.L, N.P, N.L, N.P])
+N.register("sl_xgmi_barrier", [N.P, N.P, N.L, N.I, N.I, N.L, N.I, N.P])
+N.register("sl_xgmi_rs", [N.P, N.P, N.L, N.I, N.I, N.L, N.L, N.P])
+N.register("sl_xgmi_sum", [N.P, N.P, N.L, N.I, N.I, N.L, N.P, N.L, N.F, N.P])
+N.register("sl_xgmi_peek", [N.P, N.P, N.L, N.I, N.I, N.L, N.I, N.I, N.I, N.P, N.L, N.P])
 
 MAX_WORLD = 16
 
@@ -48,6 +55,19 @@ def enabled() -> bool:
     return os.environ.get("SL_XGMI", "1") != "0"
 
 
+def default_two_shot(world: int) -> bool:
+    """Protocol for a group that cannot time both (the worker runtime): ``SL_XGMI_TWO_SHOT``
+    = 1 / 0 forces it; by default two-shot from 4 ranks.  Bytes into each GPU for an n-byte
+    payload: one-shot (W-1) n, spread over W-1 links (n per link); two-shot 2 (W-1) n / W
+    (2 n / W per link) plus a second barrier -- at W = 8 and the MLP's 1.08 MB that is
+    1.08 MB against 0.27 MB per link, while at W = 2 both move one payload over one link
+    and the extra barrier only costs."""
+    v = os.environ.get("SL_XGMI_TWO_SHOT", "")
+    if v in ("0", "1"):
+        return v == "1"
+    return world >= 4
+
+
 class XgmiExchange:
     """IPC-mapped exchange buffers of a whole group (one per rank) + step counter.
 
@@ -55,7 +75,7 @@ class XgmiExchange:
     collectives (used only here, at setup)."""
 
     def __init__(self, payload_floats: int, rank: int, world: int, device: torch.device,
-                 allgather: Callable[[bytes], list], all_ok: Callable[[bool], bool]):
+                 allgather: Callable[[bytes], list], all_ok: Callable[[bool], bool], two_shot: bool = False):
         if not (1 <= world <= MAX_WORLD) or not (0 <= rank < world):
             raise ValueError(f"xgmi exchange needs 1 <= world <= {MAX_WORLD}, got rank {rank} of {world}")
         lib = N.lib()
@@ -63,13 +83,17 @@ class XgmiExchange:
         self.payload_floats = int(payload_floats)
         self.slot_bytes = (self.payload_floats * 4 + 255) // 256 * 256
         self.hdr = int(lib.sl_xgmi_header_bytes())
+        # float4 elements each rank reduces in two-shot mode: the W chunks cover the slot, and
+        # each is whole waves (64 float4) so a consumer wave reads from one owner
+        self.chunk4 = -(-(-(-(self.slot_bytes // 16) // world)) // 64) * 64
+        self.two_shot = bool(two_shot)
         self._own = ctypes.c_void_p()
         self._opened: list[int] = []
         self.table = None
         ok = True
         err = ""
         with torch.cuda.device(device):
-            rc = lib.sl_xgmi_alloc(self.hdr + 2 * self.slot_bytes, ctypes.byref(self._own))
+            rc = lib.sl_xgmi_alloc(int(lib.sl_xgmi_buffer_bytes(self.slot_bytes)), ctypes.byref(self._own))
             if rc != 0:
                 raise RuntimeError(f"xgmi exchange allocation failed ({rc})")
             hsize = int(lib.sl_ipc_handle_size())
@@ -109,8 +133,16 @@ class XgmiExchange:
         return self.own + self.hdr + (parity & 1) * self.slot_bytes
 
     def args(self):
-        """(table, ctl, slot_bytes, rank, world) -- the launcher's XgArgs fields."""
-        return self.table.data_ptr(), self.ctl.data_ptr(), self.slot_bytes, self.rank, self.world
+        """(table, ctl, slot_bytes, rank, world, chunk4) -- the launcher's XgArgs fields
+        (chunk4 = 0 selects one-shot)."""
+        return (self.table.data_ptr(), self.ctl.data_ptr(), self.slot_bytes, self.rank, self.world,
+                self.chunk4 if self.two_shot else 0)
+
+    def exchange_launches(self, n: int) -> list:
+        """Launch specs run between "payload written" and "consumer": [(fn, extra args)]."""
+        if not self.two_shot:
+            return [("sl_xgmi_barrier", (0,))]
+        return [("sl_xgmi_barrier", (0,)), ("sl_xgmi_rs", (n,)), ("sl_xgmi_barrier", (1,))]
 
     # ---- generic all-reduce ----------------------------------------------------
     def allreduce_(self, t: torch.Tensor, scale: float = 1.0) -> None:
@@ -121,7 +153,8 @@ class XgmiExchange:
             raise ValueError("tensor larger than the exchange slot")
         s = N.stream_ptr()
         N.call("sl_xgmi_copyin", *self.args(), t.data_ptr(), t.numel(), s)
-        N.call("sl_xgmi_barrier", *self.args(), s)
+        for fn, extra in self.exchange_launches(t.numel()):
+            N.call(fn, *self.args(), *extra, s)
         N.call("sl_xgmi_sum", *self.args(), t.data_ptr(), t.numel(), float(scale), s)
 
     def peek(self, q: int, parity: int, n: int, system: bool = True) -> torch.Tensor:

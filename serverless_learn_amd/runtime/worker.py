@@ -360,13 +360,14 @@ class Worker:
         hsize = int(xgmi.N.lib().sl_ipc_handle_size())
         try:
             ex = xgmi.XgmiExchange(t.n_pad, self.group.rank, self.group.world, self.device,
-                                   lambda b: self.group.allgather_fixed(b, hsize), self.group.all_true)
+                                   lambda b: self.group.allgather_fixed(b, hsize), self.group.all_true,
+                                   two_shot=xgmi.default_two_shot(self.group.world))
         except (RuntimeError, GroupBroken) as e:
             self.log.warn("xgmi_unavailable", error=str(e))
             return
         self.xgmi = ex
         t.enable_xgmi(ex)
-        self.log.info("xgmi_enabled", epoch=self.group.epoch, world=self.group.world)
+        self.log.info("xgmi_enabled", epoch=self.group.epoch, world=self.group.world, two_shot=ex.two_shot)
 
     def _drop_xgmi(self) -> None:
         ex, self.xgmi = self.xgmi, None

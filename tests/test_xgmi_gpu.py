@@ -20,11 +20,12 @@ def _port() -> int:
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_xgmi_exchange_ranks_on_one_gpu(world):
+@pytest.mark.parametrize("world,two_shot", [(2, False), (3, False), (2, True), (3, True)])
+def test_xgmi_exchange_ranks_on_one_gpu(world, two_shot):
+    """world 3 with two-shot: chunks of unequal fill (the last rank's chunk is short)."""
     cmd = ["timeout", "-k", "10", "100", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           os.path.join(ROOT, "scripts", "xgmi_check.py"), "--same-device"]
+           os.path.join(ROOT, "scripts", "xgmi_check.py"), "--same-device"] + (["--two-shot"] if two_shot else [])
     p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=115)
     assert p.returncode == 0, p.stdout[-4000:]
     assert p.stdout.count("XGMI_CHECK_OK") == world, p.stdout[-4000:]
