@@ -218,6 +218,19 @@ class CPUTrainer:
         self.params.copy_(flat.to(self.params))
 
 
+def dh1_scale(grad_scale: float) -> float:
+    """Power of two that brings grad_scale-sized dH1 values to O(1) before the rows kernel
+    stores them as fp16 for the weight gradient (fp16 would flush them to subnormals)."""
+    return 2.0 ** round(-math.log2(grad_scale))
+
+
+def dw1_coeffs(xa: float, xb: float, scale: float) -> tuple:
+    """(a, b) with dW1 = a * slab + b * db1.  The slab holds scale * dH1^T (X + 1024) (the fp16
+    GEMM on raw pixels, u -> 1024 + u exactly), and dW1 of the normalised input xa X + xb is
+    xa dH1^T X + xb db1 = (xa / scale) slab + (xb - 1024 xa) db1."""
+    return xa / scale, xb - 1024.0 * xa
+
+
 def default_slices(batch: int) -> int:
     """Split-K slices of the weight-gradient GEMM (the kernel's own choice: one workgroup per CU)."""
     from ..ops import _native
@@ -320,15 +333,11 @@ class FusedMLPTrainer:
 
     @property
     def dh1_scale(self) -> float:
-        """Power of two that brings grad_scale-sized dH1 values to O(1) before the rows kernel
-        stores them as fp16 for the weight gradient (fp16 would flush them to subnormals)."""
-        return 2.0 ** round(-math.log2(self.grad_scale))
+        return dh1_scale(self.grad_scale)
 
     @property
     def dw1_coeffs(self) -> tuple:
-        """(a, b) with dW1 = a * slab + b * db1: the slab holds s dH1^T (X + 1024) (fp16 GEMM on
-        raw pixels), and dW1 of the normalised input xa X + xb is xa dH1^T X + xb db1."""
-        return self.xa / self.dh1_scale, self.xb - 1024.0 * self.xa
+        return dw1_coeffs(self.xa, self.xb, self.dh1_scale)
 
     def _launches(self):
         """Cached launches for the current buffers/hyper-parameters (rebuilt on change)."""

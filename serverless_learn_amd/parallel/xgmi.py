@@ -55,6 +55,13 @@ def enabled() -> bool:
     return os.environ.get("SL_XGMI", "1") != "0"
 
 
+def two_shot_chunk4(slot_bytes: int, world: int) -> int:
+    """float4 elements each rank reduces in two-shot mode: the W chunks cover the slot, and
+    each is whole waves (64 float4), so a consumer wave reads from one owner's buffer."""
+    per_rank = -(-(slot_bytes // 16) // world)
+    return -(-per_rank // 64) * 64
+
+
 def default_two_shot(world: int) -> bool:
     """Protocol for a group that cannot time both (the worker runtime): ``SL_XGMI_TWO_SHOT``
     = 1 / 0 forces it; by default two-shot from 4 ranks.  Bytes into each GPU for an n-byte
@@ -83,9 +90,7 @@ class XgmiExchange:
         self.payload_floats = int(payload_floats)
         self.slot_bytes = (self.payload_floats * 4 + 255) // 256 * 256
         self.hdr = int(lib.sl_xgmi_header_bytes())
-        # float4 elements each rank reduces in two-shot mode: the W chunks cover the slot, and
-        # each is whole waves (64 float4) so a consumer wave reads from one owner
-        self.chunk4 = -(-(-(-(self.slot_bytes // 16) // world)) // 64) * 64
+        self.chunk4 = two_shot_chunk4(self.slot_bytes, world)
         self.two_shot = bool(two_shot)
         self._own = ctypes.c_void_p()
         self._opened: list[int] = []

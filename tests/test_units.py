@@ -217,3 +217,59 @@ def test_ps_reference_single_old_echoes_the_callers_delta():
     ps = ParameterServer(0.5, per_client=False)
     np.testing.assert_allclose(ps.exchange(np.full(3, 4.0), "A"), 2.0)
     np.testing.assert_allclose(ps.exchange(np.full(3, -2.0), "B"), -1.0)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5, 8, 16])
+def test_xgmi_two_shot_chunks_cover_payload_and_sum_like_one_shot(world):
+    """Two-shot partition (csrc/kernels/xgmi.h): wave-aligned chunks that cover the slot, one
+    owner per float4, and per-chunk rank-order sums equal to the one-shot rank-order sum."""
+    from serverless_learn_amd.models.mlp import N_PARAMS
+    from serverless_learn_amd.parallel.xgmi import two_shot_chunk4
+
+    n = (N_PARAMS + 3) // 4 * 4
+    slot_bytes = (n * 4 + 255) // 256 * 256
+    c4 = two_shot_chunk4(slot_bytes, world)
+    assert c4 % 64 == 0 and c4 * world * 16 >= slot_bytes
+    owners = np.arange(slot_bytes // 16) // c4
+    assert owners.max() < world
+    # the kernel's wave-uniform owner: every aligned group of 64 float4 has one owner
+    waves = np.arange(-(-owners.size // 64) * 64) // c4
+    assert (waves.reshape(-1, 64).min(1) == waves.reshape(-1, 64).max(1)).all()
+    rng = np.random.default_rng(world)
+    parts = [rng.standard_normal(n).astype(np.float32) for _ in range(world)]
+    one = parts[0].copy()
+    for q in range(1, world):
+        one += parts[q]
+    two = np.empty(n, dtype=np.float32)
+    for r in range(world):  # rank r reduces its chunk, in rank order
+        lo, hi = r * c4 * 4, min(n, (r + 1) * c4 * 4)
+        if lo >= hi:
+            continue
+        acc = parts[0][lo:hi].copy()
+        for q in range(1, world):
+            acc += parts[q][lo:hi]
+        two[lo:hi] = acc
+    assert np.array_equal(one, two)
+
+
+def test_mlp_dw1_fp16_coefficients_reproduce_normalised_gradient():
+    """The fp16 dW1 GEMM multiplies scale * dH1 by 1024 + u; the SGD coefficients must give
+    back xa dH1^T X + xb db1 for the normalised input xa X + xb."""
+    from serverless_learn_amd.models.mlp import dh1_scale, dw1_coeffs, norm_coeffs
+
+    rng = np.random.default_rng(0)
+    rows, feats, k = 512, 16, 24
+    gs = 1.0 / (65536 * 8)
+    dh = (rng.standard_normal((rows, feats)) * gs).astype(np.float64)
+    x = rng.integers(0, 256, (rows, k)).astype(np.float64)
+    xa, xb = norm_coeffs()
+    s = dh1_scale(gs)
+    assert s == 2.0 ** 19 and 0.25 < np.abs(dh * s).max() < 16  # O(1) in fp16
+    slab = (dh * s).T @ (x + 1024.0)
+    db1 = dh.sum(0)
+    a, b = dw1_coeffs(xa, xb, s)
+    got = a * slab + b * db1[:, None]
+    want = xa * dh.T @ x + xb * db1[:, None]
+    np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-18)
+    ref = dh.T @ (xa * x + xb)  # the gradient w.r.t. W1 of the normalised input
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-18)
