@@ -1513,6 +1513,10 @@ __device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p,
 #define SL_SGD_TPG 4
 #endif
 constexpr int SGD_TPG = SL_SGD_TPG;
+#ifndef SL_SGD_NT
+#define SL_SGD_NT 1024  // threads per mlp_sgd_kernel workgroup (1024: 9.8 us vs 11.5 us at 256, profiles/r02_sgdnt)
+#endif
+constexpr int SGD_NT = SL_SGD_NT;
 static_assert(SGD_TPG == 4 || SGD_TPG == 8, "4 or 8 threads per group");
 __device__ __forceinline__ float group_sum(float v) {
   v = quad_sum(v);
@@ -1520,7 +1524,7 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void mlp_sgd_kernel(SgdArgs a) {
+__global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
   if (SL_SGD_KO == 3) return;  // timing knockout 3: launch + kernel-boundary floor
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1757,7 +1761,7 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   if (mode == 1 && !grad_out) return -1;
   if (slab && (slab_stride & 3)) return -1;
   const long groups = (P_N + 3) / 4;
-  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + 255) / 256), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
@@ -1770,7 +1774,7 @@ int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa
   a.slab = slab; a.slices = slices; a.slab_stride = slab_stride; a.grad_out = slot0; a.grad_out_alt = slot1;
   a.ar_ctl = ctl; a.n = P_N; a.xa = xa; a.xb = xb; a.mode = 1;
   const long groups = (P_N + 3) / 4;
-  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + 255) / 256), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
