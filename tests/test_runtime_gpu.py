@@ -155,3 +155,38 @@ def test_bench_prints_the_driver_json_contract(argv, capsys):
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         with open(os.path.join(root, "BASELINE.json")) as f:
             assert out["metric"] == json.load(f)["metric"]
+
+
+def test_bench_two_ranks_autotune_and_replicas():
+    """bench.py with 2 ranks (gloo rehearsal on the one GPU): the xGMI exchange is set up, one-shot,
+    two-shot and the process group are timed before the timed region, the replicas end identical,
+    and the JSON reports the whole-job value for dp2."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = ["timeout", "-k", "10", "150", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "3", "--batch", "4096",
+           "--dist-backend", "gloo", "--ingest", "local"]
+    p = subprocess.run(cmd, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=170)
+    assert p.returncode == 0, p.stdout[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout[-4000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 8192
+    assert out["replicas_identical"] is True and "xgmi_fallback" not in out
+    at = out["allreduce_autotune"]
+    assert {"xgmi_ms", "xgmi_two_shot_ms", "pg_ms"} <= set(at), at
+    best = min(at["xgmi_ms"], at["xgmi_two_shot_ms"], at["pg_ms"])
+    names = {"xgmi_ms": "xgmi-ipc", "xgmi_two_shot_ms": "xgmi-ipc-two-shot", "pg_ms": "gloo"}
+    fastest = {names[k] for k in names if at[k] == best}  # (rounded values may tie)
+    assert out["config"]["collective_backend"] in fastest, (out["config"]["collective_backend"], at)
+    assert abs(out["value"] - 8192 / (out["ms_per_step"] / 1e3)) / out["value"] < 0.03
