@@ -1322,37 +1322,52 @@ int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w
   return sl_rsum_fold(stats, 2 * cout, stream);
 }
 
+// add_even: `add` holds values at the (even, even) output positions only (typically dx itself,
+// written there by sl_conv_dgrad_s2_even for the block's 1x1 stride-2 shortcut): in the
+// parity-class split only class (0, 0) adds it, the other classes overwrite their positions.
+// even_only: compute class (0, 0) alone (the other classes have no taps for a 1x1 stride-2
+// kernel and are left to the caller).
 static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt,
                         int cin, int KH, int KW, int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add,
-                        const BnBwdEpi* bn, hipStream_t stream) {
-  if (H == OH && W == OW && ldd == 64 && !(bn && bn->x2) &&
+                        const BnBwdEpi* bn, hipStream_t stream, bool add_even = false, bool even_only = false) {
+  if (!add_even && !even_only && H == OH && W == OW && ldd == 64 && !(bn && bn->x2) &&
       sl_conv3x3_c64_applicable(OH, OW, ldd, cin, KH, KW, stride, pad, ldd))
     return sl_conv3x3_c64_bn(dy, wt, 64, 1, N, OH, dx, cin, add, nullptr, bn, stream);
   ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr, {}};
   if (bn) e.bn = *bn;
-  if (g_conv_phase && stride == 2 && KH == 3 && KW == 3 && pad == 1 && (ldd & 63) == 0) {
-    // four parity classes of dX, each a dense GEMM over its own taps (1, 2, 2, 4 of the 9)
+  const bool phase_ok = stride == 2 && KH == KW && ((KH == 3 && pad == 1) || (KH == 1 && pad == 0)) &&
+                        (ldd & 63) == 0;
+  if ((add_even || even_only) && !phase_ok) return -5;
+  if (((g_conv_phase && KH == 3) || add_even || even_only) && phase_ok) {
+    // parity classes of dX, each a dense GEMM over its own taps: (ph + pad - kh) even, dy row
+    // (oh + pad - kh) / 2 = i + (ph + pad - kh) / 2 -- 1, 2, 2, 4 of the 9 taps of a 3x3/p1
+    // kernel; only class (0, 0) (its single tap) of a 1x1/p0 kernel
     ConvGeom qs[4];
     int nq = 0;
     for (int ph = 0; ph < 2; ++ph)
       for (int pw = 0; pw < 2; ++pw) {
+        if (even_only && (ph || pw)) continue;
         ConvGeom q = g;
         const int Hp = (H - ph + 1) / 2, Wp = (W - pw + 1) / 2;
         if (Hp <= 0 || Wp <= 0) continue;
         q.OH = Hp; q.OW = Wp; q.hw_shift = ilog2(Hp * Wp); q.w_shift = ilog2(Wp); q.M = N * Hp * Wp;
-        q.ph = ph; q.pw = pw; q.FH = H; q.FW = W; q.wld = 9 * ldd;
+        q.ph = ph; q.pw = pw; q.FH = H; q.FW = W; q.wld = KH * KW * ldd;
         int t = 0;
-        for (int kh = 1 - ph; kh < 3; kh += 2)
-          for (int kw = 1 - pw; kw < 3; kw += 2) {
-            q.dh[t] = (ph + 1 - kh) / 2; q.dw[t] = (pw + 1 - kw) / 2; q.tapw[t] = kh * 3 + kw;
+        for (int kh = 0; kh < KH; ++kh)
+          for (int kw = 0; kw < KW; ++kw) {
+            if (((ph + pad - kh) & 1) || ((pw + pad - kw) & 1)) continue;
+            q.dh[t] = (ph + pad - kh) / 2; q.dw[t] = (pw + pad - kw) / 2; q.tapw[t] = kh * KW + kw;
             ++t;
           }
+        if (t == 0) return -6;  // a class with no taps would have to be zero-filled
         q.ntaps = t;
         q.K = t * ldd;
         qs[nq++] = q;
       }
     for (int i = 0; i < nq; ++i) {
-      const int rc = launch_gemm<true>(qs[i], e, stream);
+      ConvEpi ei = e;
+      if (add_even && (qs[i].ph || qs[i].pw)) ei.add = nullptr;
+      const int rc = launch_gemm<true>(qs[i], ei, stream);
       if (rc) return rc;
     }
     return 0;
@@ -1366,7 +1381,7 @@ static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, in
 // that BN's backward sums are accumulated in the epilogue (bn_bwd_epi.h).
 int sl_conv_dgrad_bn(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int KH, int KW,
                      int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add, const BnBwdEpi* bn,
-                     hipStream_t stream) {
+                     hipStream_t stream, int add_even) {
   ConvGeom g;
   if (fill_geom(g, dy, N, OH, OW, ldd, H, W, KH, KW, stride, pad)) return -1;
   if (cin & 7) return -2;
@@ -1375,8 +1390,9 @@ int sl_conv_dgrad_bn(const uint16_t* dy, int N, int OH, int OW, int ldd, const u
   if (fuse && (!bn->sums || (bn->x2 && !bn->sums2) || (bn->ymask && bn->mcoef) ||
                (((uintptr_t)bn->x | (uintptr_t)bn->x2 | (uintptr_t)dx) & 15)))
     return -4;
+  if (add_even && !add) return -5;
   int rc = dgrad_launch(g, dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, fuse ? bn : nullptr,
-                        stream);
+                        stream, add_even != 0);
   if (rc || !fuse) return rc;
   if ((rc = sl_rsum_fold(bn->sums, 2 * cin, stream))) return rc;
   return bn->x2 ? sl_rsum_fold(bn->sums2, 2 * cin, stream) : 0;
@@ -1384,17 +1400,30 @@ int sl_conv_dgrad_bn(const uint16_t* dy, int N, int OH, int OW, int ldd, const u
 
 int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int KH, int KW,
                   int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add, hipStream_t stream) {
-  return sl_conv_dgrad_bn(dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, nullptr, stream);
+  return sl_conv_dgrad_bn(dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, nullptr, stream, 0);
+}
+
+// Data gradient of a 1x1 / stride-2 / pad-0 convolution (a downsample shortcut), written to the
+// (even, even) positions of dx only -- its other positions get no contribution, and the block's
+// strided 3x3 conv1 data gradient then writes them and adds these (add_even).  Against the
+// full-resolution launch this skips the three tap-less parity classes (3/4 of the output rows)
+// and the full-size temporary the conv1 gradient used to re-read.
+int sl_conv_dgrad_s2_even(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int H, int W,
+                          uint16_t* dx, hipStream_t stream) {
+  ConvGeom g;
+  if (fill_geom(g, dy, N, OH, OW, ldd, H, W, 1, 1, 2, 0)) return -1;
+  if ((cin & 7) || (((uintptr_t)dy | (uintptr_t)wt | (uintptr_t)dx) & 15)) return -2;
+  return dgrad_launch(g, dy, N, OH, OW, ldd, wt, cin, 1, 1, 2, 0, H, W, dx, nullptr, nullptr, stream, false, true);
 }
 
 // ctypes entry: the BnBwdEpi fields as scalars
 int sl_conv_dgrad_bnx(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int KH, int KW,
                       int stride, int pad, int H, int W, uint16_t* dx, const uint16_t* add, const uint16_t* bx,
                       const uint8_t* ymask, const float* mcoef, float* sums, const uint16_t* x2, float* sums2,
-                      hipStream_t stream) {
+                      int add_even, hipStream_t stream) {
   BnBwdEpi b{bx, ymask, mcoef, sums, x2, sums2};
   return sl_conv_dgrad_bn(dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, bx ? &b : nullptr,
-                          stream);
+                          stream, add_even);
 }
 
 // Weight gradient: dw[cout][KH][KW][C] += sum over pixels of dy x im2col(x)

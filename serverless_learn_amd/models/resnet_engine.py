@@ -88,6 +88,7 @@ class FusedResNetTrainer:
         self.world_size = world_size
         self.grad_scale = 1.0 / (batch * world_size)
         self.bn_momentum = bn_momentum
+        self.shortcut_even_on = os.environ.get("SL_SHORTCUT_EVEN", "1") != "0"
         n = spec.n_flat
         self.params = torch.zeros(n, dtype=torch.float32, device=dev)
         self.params.copy_((flat if flat is not None else init_params(spec, seed)).to(dev))
@@ -141,7 +142,8 @@ class FusedResNetTrainer:
             if blk.down is not None:
                 st["cs"] = torch.empty(shp, **bf)
                 st["dcs"] = torch.empty(shp, **bf)
-                st["dxs"] = torch.empty_like(cur)
+                if not self._shortcut_even(blk):  # else the shortcut gradient goes straight into dx
+                    st["dxs"] = torch.empty_like(cur)
             st["dx"] = torch.empty_like(cur)
             self.blocks.append(st)
             cur = st["y"]
@@ -169,6 +171,15 @@ class FusedResNetTrainer:
         items.append((self.fc_w, self.fc_wt, classes, 1, 512, LOGIT_LD))
         self.wt = K.WeightTransposer(items, dev)
         self.refresh_shadows()
+
+    def _shortcut_even(self, blk) -> bool:
+        """A 1x1 / stride-2 shortcut beside a 3x3 / stride-2 conv1 (every ResNet-18 downsample
+        block): its data gradient is written straight into the (even, even) positions of the block's
+        input gradient, and conv1's parity-class data gradient adds there (ops.cnn.conv_dgrad_s2_even).
+        SL_SHORTCUT_EVEN=0 keeps the full-resolution shortcut gradient + add (A/B, tests)."""
+        d, c1 = blk.down, blk.conv1
+        return (self.shortcut_even_on and d is not None and d.k == 1 and d.stride == 2 and d.pad == 0
+                and c1.k == 3 and c1.stride == 2 and c1.pad == 1 and d.cout % 64 == 0 and c1.cout % 64 == 0)
 
     @property
     def n_params(self) -> int:
@@ -281,15 +292,32 @@ class FusedResNetTrainer:
                 bo = block_out_bn(st)
                 K.bn_bwd_reduce(dy, None, bo["x"], bo["sums"], dz_out=st["dz"], y_mask=bo["y_mask"],
                                 x2=bo.get("x2"), sums2=bo.get("sums2"))
-            add = st["dz"]
+            # the input gradient is the previous block's output gradient (its dz, stored masked
+            # with that block's BN sums) or, for the first block, the stem BN's
+            nxt = None
+            if fuse and i + 1 < len(rblocks):
+                nxt = block_out_bn(rblocks[i + 1])
+                dx = rblocks[i + 1]["dz"]
+            elif fuse and spec.stem != "imagenet":
+                nxt = dict(x=self.c0, sums=sbn.sums_buf, mask_coef=sbn.coef)
+                dx = st["dx"]
+            else:
+                dx = st["dx"]
+            add, add_even = st["dz"], False
             if down:
                 cd = self.conv[blk.down.name]
                 # dc2 and dcs from one read of dz
                 K.bn_bwd_apply_dual(st["dz"], st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"],
                                     st["cs"], bd.sums, bd.coef, bd.ggamma, bd.gbeta, st["dcs"])
                 K.conv_wgrad(st["x"], st["dcs"], blk.down.cout, 1, blk.down.stride, 0, cd.g, ws=self.wgws)
-                K.conv_dgrad(st["dcs"], cd.wt, blk.down.cin, 1, blk.down.stride, 0, st["dxs"])
-                add = st["dxs"]
+                if self._shortcut_even(blk):
+                    # 1x1/s2 shortcut: only the (even, even) positions of dx get a gradient; write
+                    # them into dx now, and conv1's parity-class data gradient adds there
+                    K.conv_dgrad_s2_even(st["dcs"], cd.wt, blk.down.cin, dx)
+                    add, add_even = dx, True
+                else:
+                    K.conv_dgrad(st["dcs"], cd.wt, blk.down.cin, 1, blk.down.stride, 0, st["dxs"])
+                    add = st["dxs"]
             else:
                 K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
             K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g, ws=self.wgws)
@@ -303,18 +331,8 @@ class FusedResNetTrainer:
             K.bn_bwd_apply_sums(st["da1"], None, st["c1"], b1.sums, b1.coef, b1.ggamma, b1.gbeta, st["dc1"],
                                 mask_coef=b1.coef)
             K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g, ws=self.wgws)
-            # the input gradient is the previous block's output gradient (its dz, stored masked
-            # with that block's BN sums) or, for the first block, the stem BN's
-            nxt = None
-            if fuse and i + 1 < len(rblocks):
-                nxt = block_out_bn(rblocks[i + 1])
-                dx = rblocks[i + 1]["dz"]
-            elif fuse and spec.stem != "imagenet":
-                nxt = dict(x=self.c0, sums=sbn.sums_buf, mask_coef=sbn.coef)
-                dx = st["dx"]
-            else:
-                dx = st["dx"]
-            K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, dx, add=add, bn=nxt)
+            K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, dx, add=add, bn=nxt,
+                         add_even=add_even)
             dy = dx
             maybe_bucket(blk.conv1.off)
         # stem

@@ -19,7 +19,8 @@ P, I, L, F = N.P, N.I, N.L, N.F
 
 N.register("sl_conv_fwd", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, I, P, P, P, P])
 N.register("sl_conv_dgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, P, P])
-N.register("sl_conv_dgrad_bnx", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P])
+N.register("sl_conv_dgrad_bnx", [P, I, I, I, I, P, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P])
+N.register("sl_conv_dgrad_s2_even", [P, I, I, I, I, P, I, I, I, P, P])
 N.register("sl_conv_wgrad", [P, I, I, I, I, P, I, I, I, I, I, I, I, I, P, I, P, L, P])
 N.register("sl_conv_wgrad_ws_need", [], ctypes.c_long)
 N.register("sl_conv_wt", [P, I, L, P])
@@ -85,8 +86,22 @@ def conv_fwd(x, w, cout: int, k: int, stride: int, pad: int, y=None, yf=None, bi
     return oh, ow
 
 
-def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None, bn=None):
+def conv_dgrad_s2_even(dy, wt, cin: int, dx):
+    """Data gradient of a 1x1 / stride-2 / pad-0 convolution written to the (even, even) positions of
+    dx [N,H,W,cin] only; the other positions are left as they are.  A downsample block passes dx
+    on as ``add`` with ``add_even=True`` to its strided 3x3 conv1 data gradient, which writes every
+    position and adds the shortcut's part at the even ones (csrc/kernels/conv.hip)."""
+    n, oh, ow, cd = dy.shape
+    _, h, wd, ci = dx.shape
+    assert ci == cin and (h + 1) // 2 == oh and (wd + 1) // 2 == ow
+    N.call("sl_conv_dgrad_s2_even", _bf16(dy), n, oh, ow, cd, _bf16(wt), cin, h, wd, _bf16(dx), N.stream_ptr())
+
+
+def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None, bn=None, add_even: bool = False):
     """dy [N,OH,OW,Cd] bf16 (Cd channels, zero beyond cout), wt [cin, k*k*Cd] -> dx [N,H,W,cin] (+ add).
+
+    ``add_even`` (3x3 stride-2 only): ``add`` holds values at the (even, even) positions only and
+    may be dx itself (see :func:`conv_dgrad_s2_even`).
 
     ``bn``: dx is the gradient at the input of ``relu(bn(x))`` (or of a block output
     ``relu(bn(x) + shortcut)``): a dict with ``x`` (the BN input, dx's shape), ``sums``
@@ -99,7 +114,12 @@ def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None, bn
     assert ci == cin
     if add is not None:
         assert add.shape == dx.shape and add.dtype == torch.bfloat16
+    assert not add_even or (add is not None and k == 3 and stride == 2 and pad == 1)
     if bn is None:
+        if add_even:
+            N.call("sl_conv_dgrad_bnx", _bf16(dy), n, oh, ow, cd, _bf16(wt), cin, k, k, stride, pad, h, wd,
+                   _bf16(dx), _bf16(add), None, None, None, None, None, None, 1, N.stream_ptr())
+            return
         N.call("sl_conv_dgrad", _bf16(dy), n, oh, ow, cd, _bf16(wt), cin, k, k, stride, pad, h, wd, _bf16(dx),
                _bf16(add) if add is not None else None, N.stream_ptr())
         return
@@ -111,7 +131,7 @@ def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None, bn
     N.call("sl_conv_dgrad_bnx", _bf16(dy), n, oh, ow, cd, _bf16(wt), cin, k, k, stride, pad, h, wd, _bf16(dx),
            _bf16(add) if add is not None else None, _bf16(x), p(ym) if ym is not None else None,
            _f32(mc) if mc is not None else None, _f32(bn["sums"]), _bf16(x2) if x2 is not None else None,
-           _f32(bn["sums2"]) if x2 is not None else None, N.stream_ptr())
+           _f32(bn["sums2"]) if x2 is not None else None, 1 if add_even else 0, N.stream_ptr())
 
 
 # split-K target for the implicit-GEMM weight gradient (workgroups per launch);

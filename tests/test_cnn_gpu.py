@@ -153,6 +153,61 @@ def test_dgrad_fused_bn_backward_matches_separate_reduce(case, mode):
         assert rel(f2, r2) < 1e-4
 
 
+@pytest.mark.parametrize("n,h,c,cout", [(8, 32, 64, 128), (4, 16, 128, 256), (2, 8, 256, 512)])
+@pytest.mark.parametrize("fused_bn", [False, True])
+def test_shortcut_gradient_into_even_positions(n, h, c, cout, fused_bn):
+    """Downsample block input gradient: the 1x1/s2 shortcut data gradient written straight into
+    the (even, even) positions of dx (conv_dgrad_s2_even) + conv1's 3x3/s2 parity-class data
+    gradient with add_even equals the full-resolution shortcut gradient passed as ``add``."""
+    from serverless_learn_amd.ops import cnn as K
+
+    torch.manual_seed(11)
+    oh = h // 2
+    dy1 = bf(torch.randn(n, oh, oh, cout, device=DEV))
+    dys = bf(torch.randn(n, oh, oh, cout, device=DEV))
+    w1 = bf(torch.randn(c, 9, cout, device=DEV) / math.sqrt(9 * cout)).reshape(-1)
+    ws = bf(torch.randn(c, 1, cout, device=DEV) / math.sqrt(cout)).reshape(-1)
+    xb = bf(torch.randn(n, h, h, c, device=DEV))
+    coef = torch.randn(4 * c, device=DEV)
+    nf = K.rsum_floats(2 * c)
+
+    def bn_of():
+        return dict(x=xb, mask_coef=coef, sums=torch.zeros(nf, device=DEV)) if fused_bn else None
+
+    dxs = torch.empty(n, h, h, c, dtype=torch.bfloat16, device=DEV)
+    K.conv_dgrad(dys, ws, c, 1, 2, 0, dxs)
+    ref = torch.empty_like(dxs)
+    bn_ref = bn_of()
+    K.conv_dgrad(dy1, w1, c, 3, 2, 1, ref, add=dxs, bn=bn_ref)
+    got = torch.full_like(dxs, float("nan"))  # every position must be written
+    K.conv_dgrad_s2_even(dys, ws, c, got)
+    # the shortcut part alone: even positions = the full-resolution result there
+    assert torch.equal(got[:, ::2, ::2], dxs[:, ::2, ::2])
+    bn_got = bn_of()
+    K.conv_dgrad(dy1, w1, c, 3, 2, 1, got, add=got, bn=bn_got, add_even=True)
+    torch.cuda.synchronize()
+    assert not torch.isnan(got.float()).any()
+    assert torch.equal(got, ref), float((got.float() - ref.float()).abs().max())
+    if fused_bn:
+        r, f = K.rsum_result(bn_ref["sums"], 2 * c), K.rsum_result(bn_got["sums"], 2 * c)
+        assert rel(f, r) < 1e-4
+
+
+def test_resnet_engine_shortcut_even_matches_full_resolution(monkeypatch):
+    """The engine with the even-position shortcut gradient (default) against the full-resolution
+    shortcut gradient + add (SL_SHORTCUT_EVEN=0), within the engine's run-to-run noise (see
+    test_resnet_engine_fused_bn_backward_matches_unfused)."""
+    monkeypatch.setenv("SL_SHORTCUT_EVEN", "1")
+    tr, g, _, _ = _engine("cifar", 32, 32)
+    assert tr.shortcut_even_on and "dxs" not in tr.blocks[2]
+    monkeypatch.setenv("SL_SHORTCUT_EVEN", "0")
+    tr0, g0, _, _ = _engine("cifar", 32, 32)
+    _, g1, _, _ = _engine("cifar", 32, 32)
+    assert not tr0.shortcut_even_on and "dxs" in tr0.blocks[2]
+    noise = float(F.cosine_similarity(g0, g1, dim=0))
+    assert float(F.cosine_similarity(g, g0, dim=0)) > min(noise, 0.995) - 0.01
+
+
 def test_stats_fold_fresh_across_repeated_launches():
     """The cross-workgroup statistics fold (replicas + last-arriver) must see this
     launch's values, not lines cached by an earlier launch's fold: run the conv
