@@ -603,6 +603,7 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict
 
 // ---------------------------------------------------------------------------
 extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream);  // conv.hip
+extern "C" int sl_rsum_fold2(float* buf, float* buf2, int n, hipStream_t stream);  // conv.hip
 
 extern "C" {
 
@@ -668,8 +669,7 @@ int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, ymask, dz_out, sums, x2, sums2, rows,
                      C);
   SL_CHECK_LAUNCH();
-  if (int rc = sl_rsum_fold(sums, 2 * C, stream)) return rc;
-  if (x2) return sl_rsum_fold(sums2, 2 * C, stream);
+  if (int rc = sl_rsum_fold2(sums, x2 ? sums2 : nullptr, 2 * C, stream)) return rc;
   return 0;
 }
 

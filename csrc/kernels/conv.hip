@@ -1267,8 +1267,15 @@ static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) 
 // Fold of the rsum replicas into the result row (common.h): one launch after the producers.
 // 64 threads per block, all SL_REP loads of a thread in flight at once: the launch is
 // latency-bound (2C <= 1024 values), so keep it to one round trip and spread it over CUs.
-__global__ __launch_bounds__(64) void rsum_fold_kernel(float* buf, int n) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
+// buf2 (nullable): a second buffer of the same n folded by the same launch (blocks past the
+// first buffer's take it), for producers that accumulate two sets (a downsample block's BNs).
+__global__ __launch_bounds__(64) void rsum_fold_kernel(float* buf, int n, float* buf2) {
+  int i = blockIdx.x * 64 + threadIdx.x;
+  const int nb = (n + 63) / 64;
+  if ((int)blockIdx.x >= nb) {
+    buf = buf2;
+    i -= nb * 64;
+  }
   if (i >= n) return;
   float v[SL_REP];
 #pragma unroll
@@ -1279,12 +1286,15 @@ __global__ __launch_bounds__(64) void rsum_fold_kernel(float* buf, int n) {
   rsum_result(buf, n)[i] = acc;
 }
 
-extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream) {
+extern "C" int sl_rsum_fold2(float* buf, float* buf2, int n, hipStream_t stream) {
   if (!buf || n <= 0) return -1;
-  hipLaunchKernelGGL(rsum_fold_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, buf, n);
+  const int nb = (n + 63) / 64;
+  hipLaunchKernelGGL(rsum_fold_kernel, dim3(buf2 ? 2 * nb : nb), dim3(64), 0, stream, buf, n, buf2);
   SL_CHECK_LAUNCH();
   return 0;
 }
+
+extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream) { return sl_rsum_fold2(buf, nullptr, n, stream); }
 
 static int g_conv_phase = 1;  // stride-2 dgrad by parity classes (sl_conv_set_phase)
 
@@ -1394,8 +1404,7 @@ int sl_conv_dgrad_bn(const uint16_t* dy, int N, int OH, int OW, int ldd, const u
   int rc = dgrad_launch(g, dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, fuse ? bn : nullptr,
                         stream, add_even != 0);
   if (rc || !fuse) return rc;
-  if ((rc = sl_rsum_fold(bn->sums, 2 * cin, stream))) return rc;
-  return bn->x2 ? sl_rsum_fold(bn->sums2, 2 * cin, stream) : 0;
+  return sl_rsum_fold2(bn->sums, bn->x2 ? bn->sums2 : nullptr, 2 * cin, stream);
 }
 
 int sl_conv_dgrad(const uint16_t* dy, int N, int OH, int OW, int ldd, const uint16_t* wt, int cin, int KH, int KW,
