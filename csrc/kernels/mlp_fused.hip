@@ -861,7 +861,7 @@ __global__ __launch_bounds__(L1_NT, 2) void mlp_l1_kernel(L1Args a) {
 
 // ---------------------------------------------------------------------------
 // Weight-gradient grouped split-K GEMM:  G[m][n] = sum_b A[b][m] * Bop[b][n],
-// A = dH1 / dH2 ([batch][256] bf16), Bop = raw u8 X / bf16 H1, row-major over b.
+// A = dH1 / dH2 ([batch][256]; dH1 fp16 scaled, dH2 bf16), Bop = raw u8 X / bf16 H1, row-major over b.
 //
 // Workgroup tile 256 (m: all of dH) x 128 (n); 8 waves as 4 (m) x 2 (n) of
 // 64 x 64, every wave over the whole 64-row stage: 32 MFMAs per wave per
@@ -980,25 +980,9 @@ __device__ __forceinline__ short8_t wg_tr8(uint32_t a) {
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
-// 8 u8 -> 8 bf16, exact (integers < 256 have <= 8 significant bits):
-// v_cvt_f32_ubyteN per byte, then one v_perm_b32 keeps the high halves of two floats.
-__device__ __forceinline__ short8_t u8x8_exact_bf16(uint2v_t v) {
-  uint32_t w[4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t x = v[h];
-    const uint32_t f0 = __float_as_uint((float)(x & 0xffu)), f1 = __float_as_uint((float)((x >> 8) & 0xffu));
-    const uint32_t f2 = __float_as_uint((float)((x >> 16) & 0xffu)), f3 = __float_as_uint((float)(x >> 24));
-    w[2 * h] = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
-    w[2 * h + 1] = __builtin_amdgcn_perm(f3, f2, 0x07060302u);
-  }
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  return __builtin_bit_cast(short8_t, u32x4{w[0], w[1], w[2], w[3]});
-}
-
 // 8 u8 -> 8 fp16 of (1024 + u), exact: fp16 steps by 1 over [1024, 2048), so the bits are
-// 0x6400 | u and one v_perm_b32 builds two of them (the bf16 form above costs 1.5 VALU per
-// element).  dW1 is then dH1^T (X + 1024); mlp_sgd_kernel removes the 1024 db1 term.
+// 0x6400 | u and one v_perm_b32 builds two of them (widening each byte exactly to bf16 took
+// a v_cvt_f32_ubyteN per byte + a v_perm per pair, 1.5 VALU per element).  dW1 is then dH1^T (X + 1024); mlp_sgd_kernel removes the 1024 db1 term.
 __device__ __forceinline__ short8_t u8x8_f16_biased(uint2v_t v) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   return __builtin_bit_cast(short8_t, u32x4{__builtin_amdgcn_perm(0x64646464u, v[0], 0x04010400u),
