@@ -69,6 +69,9 @@ def parse(argv=None):
     ap.add_argument("--autotune", type=int, default=6,
                     help="--allreduce auto with N>1: untimed steps per candidate (xGMI one-shot, xGMI two-shot, "
                          "the process group) before the timed region; the fastest is timed (0 = keep one-shot xGMI)")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="allow --gpus N on fewer than N visible devices (ranks share GPUs: rehearsal only, "
+                         "needs --dist-backend gloo)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     mlp = a.model == "mlp"
@@ -85,8 +88,61 @@ def parse(argv=None):
     return a
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_devices() -> int:
+    """GPUs this process could use.  ``torch.cuda.device_count()`` does not initialise the
+    GPU on this image, so the launcher parent stays GPU-free before it spawns its ranks."""
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def launch_ranks(args, argv) -> int:
+    """``--gpus N`` without a launcher: spawn N rank processes (one per GPU, the same
+    command line under ``torch.distributed.run``) and exit with their status.  Nothing
+    here touches the GPU, so the children are started from a parent that never
+    initialised HIP.  Rank 0 prints the one JSON line; it reaches our stdout unchanged.
+
+    The reference starts one ``worker ADDR`` process per worker by hand
+    (/root/reference/src/worker.cc:233-258); this is the benchmark's equivalent."""
+    import subprocess
+
+    n_dev = visible_devices()
+    if n_dev < args.gpus and not args.oversubscribe:
+        print(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) visible; refusing to report a "
+              f"{args.gpus}-GPU number (pass --oversubscribe --dist-backend gloo to rehearse ranks "
+              "sharing GPUs)", file=sys.stderr)
+        return 2
+    if n_dev < args.gpus and args.dist_backend != "gloo":
+        print("bench.py: --oversubscribe needs --dist-backend gloo (RCCL refuses ranks sharing a device)",
+              file=sys.stderr)
+        return 2
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    env["SL_BENCH_LAUNCHED"] = "1"
+    p = subprocess.run(cmd, env=env)
+    return p.returncode
+
+
 def main(argv=None) -> int:
     args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
+
     import torch
     import torch.distributed as dist
 
@@ -95,9 +151,18 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
-    local_dev = local_rank % max(1, torch.cuda.device_count()) if args.dist_backend == "gloo" else local_rank
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+        return 2
+    n_dev = visible_devices()
+    if n_dev < 1:
+        print("bench.py: no GPU visible", file=sys.stderr)
+        return 2
+    if local_rank >= n_dev and not (args.oversubscribe and args.dist_backend == "gloo"):
+        print(f"bench.py: local rank {local_rank} but only {n_dev} GPU(s) visible (ranks would share a "
+              "device; pass --oversubscribe --dist-backend gloo to rehearse that)", file=sys.stderr)
+        return 2
+    local_dev = local_rank % n_dev
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     if world > 1:
@@ -314,6 +379,14 @@ def main(argv=None) -> int:
         "train_acc_last": round(st.accuracy, 4),
         "ingest_s": round(t_ingest, 3),
         "replicas_identical": replicas_identical,
+        "dist": {
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
+            "collective_backend": collective,
+            "devices_visible": n_dev,
+            "ranks_share_gpus": world > n_dev,
+            "launcher": "bench.py" if os.environ.get("SL_BENCH_LAUNCHED") else ("torchrun" if world > 1 else None),
+        },
     }
     if xgmi_fallback:
         out["xgmi_fallback"] = xgmi_fallback

@@ -111,7 +111,8 @@ __device__ __forceinline__ unsigned xg_step(const unsigned* ctl) {
 // consumer kernels: lane q < world stores s into inbox[rank] of rank q's buffer (a
 // system-scope store over xGMI), then polls inbox[q] of this rank's own buffer until
 // rank q has signalled s (bounded: after XG_TIMEOUT_TICKS it records the error word
-// and gives up, so a lost peer never hangs the GPU).  Keeping the spin in one wave
+// and gives up, so a lost peer never hangs the GPU; with the error word set, later barriers
+// skip the wait).  Keeping the spin in one wave
 // matters: a consumer grid whose every block spun would hold every CU while it
 // waits, and ranks that share a GPU (tests) could then never run the peer's
 // producer kernels.
@@ -120,7 +121,11 @@ __device__ __forceinline__ void xg_signal_wait(const XgArgs& x, int set) {
   const unsigned s = xg_step(x.ctl);
   if (lane < x.world)
     __hip_atomic_store(xg_inbox(x.bases[lane], x.rank, set), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (lane < x.world) {
+  // once a barrier has timed out the group is void until the host re-forms it: later
+  // barriers (steps already queued in a graph) signal but do not wait again, so draining
+  // them costs microseconds instead of XG_TIMEOUT_TICKS each
+  const bool failed = __hip_atomic_load(x.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (lane < x.world && !failed) {
     unsigned* f = xg_inbox(x.bases[x.rank], lane, set);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - s) < 0) {

@@ -10,6 +10,13 @@ load the file server's latest checkpoint and join the group.  Prints one JSON
 summary line; exit code 0 iff every phase happened.
 
     python scripts/elastic_demo.py [--device cpu|cuda] [--model mlp|resnet18] [--timeout 240]
+        [--scenario kill2|all] [--dp-backend gloo] [--xgmi-gloo]
+
+``--scenario all`` kills EVERY original worker and starts fresh ones, which must resume
+from the file server's checkpoint (``PeerList.resume_file``) -- the whole-group
+replacement case.  ``--device cuda --dp-backend gloo --xgmi-gloo`` runs the workers as
+GPU processes sharing one GPU with the MLP's xGMI exchange live (IPC maps dropped and
+re-made on every regroup), the GPU rehearsal of BASELINE config 5.
 
 The reference has leave-unhandled, log-only failure detection
 (/root/reference/src/master.cc:240-266) and no checkpoints; this exercises the
@@ -68,6 +75,11 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--timeout", type=float, default=240.0)
     ap.add_argument("--logdir", default=None)
+    ap.add_argument("--scenario", choices=["kill2", "all"], default="kill2")
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--dp-backend", default="auto")
+    ap.add_argument("--dp-timeout-s", type=float, default=20.0)
+    ap.add_argument("--xgmi-gloo", action="store_true", help="SL_XGMI_GLOO=1: xGMI exchange on a gloo group")
     args = ap.parse_args(argv)
 
     logdir = args.logdir or tempfile.mkdtemp(prefix="sl_elastic_")
@@ -77,7 +89,8 @@ def main(argv=None) -> int:
               "--checkup-interval-ms", "300", "--push-interval-ms", "300", "--max-misses", "2",
               "--rpc-timeout-s", "2.0", "--log-every", "5", "--checkpoint-every", "20",
               "--shard-records", "4096", "--model", args.model, "--batch", str(args.batch),
-              "--device", args.device, "--sync", "allreduce"]
+              "--device", args.device, "--sync", "allreduce", "--dp-backend", args.dp_backend,
+              "--dp-timeout-s", str(args.dp_timeout_s)]
     if args.model == "resnet18":
         common += ["--dataset", "synthetic-cifar"]
     procs: dict[str, subprocess.Popen] = {}
@@ -86,6 +99,8 @@ def main(argv=None) -> int:
     def spawn(name, role_args):
         path = os.path.join(logdir, name + ".log")
         env = dict(os.environ, SL_LOG_FILE=path, PYTHONPATH=ROOT)
+        if args.xgmi_gloo:
+            env["SL_XGMI_GLOO"] = "1"
         env.setdefault("OMP_NUM_THREADS", "2")
         procs[name] = subprocess.Popen([sys.executable, "-m", "serverless_learn_amd.cli", *role_args, *common],
                                        env=env, stdout=subprocess.DEVNULL, stderr=open(path + ".err", "w"))
@@ -105,45 +120,71 @@ def main(argv=None) -> int:
         tr = last(ev, "train")
         return (tr or {}).get("step", 0), (tr or {}).get("epoch", -1), ev
 
+    def replicas_agree(group):
+        """Parameter checksums the workers logged at the newest step they all logged: lock-step
+        replicas must match (one value)."""
+        per = {n: {e["step"]: e.get("param_sum") for e in read_events(logs[n])
+                   if e.get("event") == "train" and "param_sum" in e} for n in group}
+        common = set.intersection(*(set(v) for v in per.values())) if per else set()
+        if not common:
+            return None
+        st = max(common)
+        vals = {per[n][st] for n in group}
+        return {"step": st, "distinct": len(vals), "sums": sorted(vals)}
+
     summary = {"ok": False, "logdir": logdir, "phases": {}}
     try:
         spawn("file_server", ["file-server"])
         spawn("master", ["master"])
         time.sleep(1.0)
-        names = [f"w{i}" for i in range(4)]
+        names = [f"w{i}" for i in range(args.workers)]
         for i, n in enumerate(names):
             spawn(n, ["worker", f"127.0.0.1:{free_port()}"])
         budget = args.timeout
 
-        # phase 1: all four train together, a checkpoint exists
+        # phase 1: all train together, a checkpoint exists
         ok = wait(lambda: all(worker_state(n)[0] >= 30 for n in names)
                   and last(read_events(logs["master"]), "checkpoint_reported") is not None, budget / 3,
-                  "4 workers training + checkpoint")
-        summary["phases"]["train4"] = {n: worker_state(n)[:2] for n in names}
+                  f"{len(names)} workers training + checkpoint")
+        summary["phases"]["train_all"] = {n: worker_state(n)[:2] for n in names}
+        summary["replicas_before"] = replicas_agree(names)
         if not ok:
             return 1
-        # phase 2: SIGKILL two workers (no Deregister)
-        for n in names[2:]:
+        # phase 2: SIGKILL workers (no Deregister: the master must notice missed heartbeats)
+        victims = names[2:] if args.scenario == "kill2" else list(names)
+        survivors = [n for n in names if n not in victims]
+        t_kill = time.time()
+        for n in victims:
             procs[n].send_signal(signal.SIGKILL)
             procs[n].wait()
-        killed_at = {n: worker_state(n)[0] for n in names[:2]}
-        ok = wait(lambda: sum(1 for e in read_events(logs["master"]) if e.get("event") == "evicted") >= 2,
-                  budget / 4, "eviction of 2 workers")
-        ok = ok and wait(lambda: all(worker_state(n)[0] >= killed_at[n] + 15 for n in names[:2]), budget / 4,
-                         "survivors training after regroup")
-        summary["phases"]["survivors"] = {n: worker_state(n)[:2] for n in names[:2]}
+        killed_at = {n: worker_state(n)[0] for n in names}
+        ok = wait(lambda: sum(1 for e in read_events(logs["master"]) if e.get("event") == "evicted") >= len(victims),
+                  budget / 4, f"eviction of {len(victims)} workers")
+        if survivors:
+            ok = ok and wait(lambda: all(worker_state(n)[0] >= killed_at[n] + 15 for n in survivors), budget / 4,
+                             "survivors training after regroup")
+            summary["survivor_regroup_s"] = round(time.time() - t_kill, 2)
+        summary["phases"]["survivors"] = {n: worker_state(n)[:2] for n in survivors}
         if not ok:
             return 1
-        # phase 3: two fresh workers join, load the checkpoint, and train with the group
-        fresh = ["w4", "w5"]
+        # phase 3: fresh workers join, load the checkpoint, and train with the group
+        fresh = [f"w{len(names) + i}" for i in range(len(victims))]
         for n in fresh:
             spawn(n, ["worker", f"127.0.0.1:{free_port()}"])
+        base = max(killed_at.values()) if survivors else 0
         ok = wait(lambda: all(last(read_events(logs[n]), "checkpoint_loaded") is not None or
-                              last(read_events(logs[n]), "state_synced") is not None for n in fresh)
-                  and all(worker_state(n)[0] >= killed_at[names[0]] + 20 for n in fresh), budget / 3,
+                              last(read_events(logs[n]), "state_synced") is not None or bool(survivors)
+                              for n in fresh)
+                  and all(worker_state(n)[0] >= base + 20 for n in fresh), budget / 3,
                   "fresh workers resumed and training")
-        summary["phases"]["rejoined"] = {n: worker_state(n)[:2] for n in names[:2] + fresh}
+        group = survivors + fresh
+        summary["phases"]["rejoined"] = {n: worker_state(n)[:2] for n in group}
         summary["resumed_from_checkpoint"] = {n: last(read_events(logs[n]), "checkpoint_loaded") for n in fresh}
+        summary["resume_pulled"] = {n: last(read_events(logs[n]), "resume_pulled") for n in fresh}
+        summary["replicas_after"] = replicas_agree(group)
+        summary["xgmi"] = {n: [(e.get("event"), e.get("epoch")) for e in read_events(logs[n])
+                               if e.get("event") in ("xgmi_enabled", "xgmi_closed")] for n in group}
+        summary["graph"] = {n: bool((last(read_events(logs[n]), "train") or {}).get("graph")) for n in group}
         summary["ok"] = bool(ok)
         return 0 if ok else 1
     finally:

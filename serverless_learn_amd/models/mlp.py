@@ -23,6 +23,7 @@ import math
 import os
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -216,6 +217,16 @@ class CPUTrainer:
 
     def set_flat(self, flat: torch.Tensor) -> None:
         self.params.copy_(flat.to(self.params))
+
+    def state_extra(self) -> dict:
+        return {"cursor": np.array([self.cursor], dtype=np.float64)}
+
+    def load_state_extra(self, d: dict) -> None:
+        if "cursor" in d:
+            self.cursor = int(d["cursor"][0])
+
+    def buffers(self) -> list:
+        return []
 
 
 def dh1_scale(grad_scale: float) -> float:
@@ -511,3 +522,16 @@ class FusedMLPTrainer:
     def set_flat(self, flat: torch.Tensor) -> None:
         self.params[:N_PARAMS].copy_(flat.to(self.params))
         self.refresh_shadows()
+
+    # ---- exact-resume state beyond the flat vectors (ckpt format v2) ----
+    def state_extra(self) -> dict:
+        """The device batch cursor: a resumed run continues with the batch the saved run
+        would have taken next, so save-at-k + resume + m steps equals k + m steps."""
+        return {"cursor": self.cursor.double().cpu().numpy()}
+
+    def load_state_extra(self, d: dict) -> None:
+        if "cursor" in d:
+            self.cursor.fill_(int(d["cursor"][0]))
+
+    def buffers(self) -> list:
+        return []

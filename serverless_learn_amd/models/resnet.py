@@ -24,6 +24,7 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -310,3 +311,35 @@ class CPUResNetTrainer:
 
     def set_flat(self, flat: torch.Tensor) -> None:
         self.params.copy_(flat.to(self.params))
+
+    # ---- exact-resume state beyond the flat vectors (ckpt format v2) ----
+    def state_extra(self) -> dict:
+        d = {"cursor": np.array([self.cursor], dtype=np.float64)}
+        for name, (rm, rv) in self.running.items():
+            d[f"bn/{name}/mean"] = rm.double().numpy()
+            d[f"bn/{name}/var"] = rv.double().numpy()
+        return d
+
+    def load_state_extra(self, d: dict) -> None:
+        if "cursor" in d:
+            self.cursor = int(d["cursor"][0])
+        for name, (rm, rv) in self.running.items():
+            if f"bn/{name}/mean" in d:
+                rm.copy_(torch.from_numpy(np.asarray(d[f"bn/{name}/mean"])).to(rm.dtype))
+                rv.copy_(torch.from_numpy(np.asarray(d[f"bn/{name}/var"])).to(rv.dtype))
+
+    def buffers(self) -> list:
+        """Non-parameter state every replica must agree on (broadcast after a regroup)."""
+        return [t for pair in self.running.values() for t in pair]
+
+    def evaluate(self, x_u8: torch.Tensor, y_u8: torch.Tensor):
+        """Inference with the BatchNorm running statistics (eval mode)."""
+        from .mlp import StepStats
+
+        with torch.no_grad():
+            logits = ref_forward(self.spec, self.params, x_u8.reshape(-1, self.spec.in_hw, self.spec.in_hw, 3),
+                                 False, self.running)
+            y = y_u8.reshape(-1).long()
+            loss = F.cross_entropy(logits, y, reduction="mean")
+            acc = (logits.argmax(1) == y).float().mean()
+        return StepStats(float(loss), float(acc), int(y.numel()))

@@ -401,3 +401,82 @@ class FusedResNetTrainer:
 
     def running_stats(self) -> dict:
         return {name: (b.run_mean, b.run_var) for name, b in self.bn.items()}
+
+    # ---- exact-resume state beyond the flat vectors (ckpt format v2) ----
+    def state_extra(self) -> dict:
+        d = {"cursor": self.cursor.double().cpu().numpy()}
+        for name, b in self.bn.items():
+            d[f"bn/{name}/mean"] = b.run_mean.double().cpu().numpy()
+            d[f"bn/{name}/var"] = b.run_var.double().cpu().numpy()
+        return d
+
+    def load_state_extra(self, d: dict) -> None:
+        if "cursor" in d:
+            self.cursor.fill_(int(d["cursor"][0]))
+        for name, b in self.bn.items():
+            if f"bn/{name}/mean" in d:
+                b.run_mean.copy_(torch.as_tensor(d[f"bn/{name}/mean"], dtype=torch.float32))
+                b.run_var.copy_(torch.as_tensor(d[f"bn/{name}/var"], dtype=torch.float32))
+
+    def buffers(self) -> list:
+        """BN running statistics: broadcast with the parameters after a regroup, so every
+        replica evaluates identically (each rank's statistics come from its own batches)."""
+        return [t for b in self.bn.values() for t in (b.run_mean, b.run_var)]
+
+    # ---- inference with running statistics ----
+    def _eval_coef(self, bn: _BN, eps: float = 1e-5) -> torch.Tensor:
+        sc = bn.gamma * torch.rsqrt(bn.run_var + eps)
+        return torch.cat([sc, bn.beta - bn.run_mean * sc, bn.run_mean, torch.rsqrt(bn.run_var + eps)])
+
+    def forward_eval(self) -> None:
+        """Eval-mode forward of the current batch: every BatchNorm normalises with its running
+        statistics (no batch statistics are computed, none are updated), then loss / correct
+        / logits.  Same kernels as training -- conv_fwd without the statistics epilogue and
+        bn_apply with coefficients folded from (gamma, beta, running mean, running var)."""
+        K, spec = self.K, self.spec
+        co = {name: self._eval_coef(b) for name, b in self.bn.items()}
+        K.input_norm(self.x, self.y, self.cursor, self.batch, self.x0, self.labels, CIFAR_MEAN, CIFAR_STD)
+        sc = spec.stem_conv
+        K.conv_fwd(self.x0, self.conv["stem"].w, sc.cout, sc.k, sc.stride, sc.pad, y=self.c0)
+        K.bn_apply(self.c0, co[spec.stem_bn.name], self.a0, relu=True)
+        if spec.stem == "imagenet":
+            K.maxpool_fwd(self.a0, self.p0, self.p0_arg)
+        for st in self.blocks:
+            blk: BlockSpec = st["spec"]
+            c1, c2 = blk.conv1, blk.conv2
+            K.conv_fwd(st["x"], self.conv[c1.name].w, c1.cout, c1.k, c1.stride, c1.pad, y=st["c1"])
+            K.bn_apply(st["c1"], co[blk.bn1.name], st["a1"], relu=True)
+            K.conv_fwd(st["a1"], self.conv[c2.name].w, c2.cout, c2.k, c2.stride, c2.pad, y=st["c2"])
+            if blk.down is not None:
+                d = blk.down
+                K.conv_fwd(st["x"], self.conv[d.name].w, d.cout, d.k, d.stride, d.pad, y=st["cs"])
+                K.bn_apply(st["c2"], co[blk.bn2.name], st["y"], relu=True, res=st["cs"], rcoef=co[blk.dbn.name])
+            else:
+                K.bn_apply(st["c2"], co[blk.bn2.name], st["y"], relu=True, res=st["x"])
+        K.avgpool_fwd(self.feat_in, self.feat)
+        K.conv_fwd(self.feat, self.fc_w, spec.classes, 1, 1, 0, yf=self.logits, bias=self.fc_b)
+        K.softmax_ce(self.logits, self.labels, self.loss, self.correct, self.dlogits.view(self.batch, LOGIT_LD),
+                     None, self.grad_scale)
+
+    def evaluate(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> StepStats:
+        """Eval-mode loss / accuracy over every whole batch of (x, y) with the running
+        statistics; the training shard, cursor and statistics are left untouched."""
+        hw = self.spec.in_hw
+        x = x_u8.reshape(-1, hw, hw, 3).to(self.device).contiguous()
+        y = y_u8.reshape(-1).to(self.device).to(torch.uint8).contiguous()
+        nb = x.shape[0] // self.batch
+        if nb < 1:
+            raise ValueError("evaluation set smaller than one batch")
+        saved = (self.x, self.y, self.cursor)
+        self.x, self.y, self.cursor = x, y, torch.zeros(1, dtype=torch.int32, device=self.device)
+        loss = corr = 0.0
+        try:
+            for _ in range(nb):
+                self.forward_eval()
+                loss += float(self.loss.sum())
+                corr += float(self.correct.sum())
+                self.K.cursor_bump(self.cursor)
+        finally:
+            self.x, self.y, self.cursor = saved
+        n = nb * self.batch
+        return StepStats(loss / n, corr / n, n)

@@ -154,10 +154,22 @@ class ElasticGroup:
             raise GroupBroken(repr(e)) from e
         self._run(work)
 
-    def allreduce_async(self, t: torch.Tensor):
+    def allreduce_async(self, t: torch.Tensor, op=None):
         if self.pg is None:
             return None
-        return self.pg.allreduce([t])
+        if op is None:
+            return self.pg.allreduce([t])
+        o = dist.AllreduceOptions()
+        o.reduceOp = op
+        try:
+            return self.pg.allreduce([t], o)
+        except Exception as e:
+            self.broken = True
+            raise GroupBroken(repr(e)) from e
+
+    def wait(self, work) -> None:
+        if work is not None:
+            self._run(work)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
         if self.pg is None:

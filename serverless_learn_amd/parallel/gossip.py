@@ -84,7 +84,11 @@ class GossipState:
         exchange in the meantime, that serve already set ``o = m`` (its reply carried
         everything, ``sent`` included), so only ``a*r`` is added.  With no concurrent
         steps both rules give ``o = m``, so the exchange math of SURVEY.md §3.4 is
-        unchanged."""
+        unchanged.
+
+        ``compat`` keeps the reference's ``o = m`` (worker.cc:215) exactly, so progress made
+        while the RPC was in flight is dropped from later exchanges there too -- compat mode
+        reproduces the reference, including that loss."""
         with self.lock:
             r = torch.from_numpy(np.asarray(reply, dtype=np.float64))
             self._grow(r.numel())
@@ -108,6 +112,8 @@ class GossipState:
                     o[:s.numel()] += s
                 o[:n] += a * r
                 self.old.copy_(o.to(self.old.dtype))
+            if self.compat:
+                self.old.copy_(self.model)  # worker.cc:215, o = m
             self.exchanges += 1
 
     # -- server side -----------------------------------------------------------

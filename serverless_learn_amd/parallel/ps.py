@@ -46,6 +46,8 @@ class ParameterServer:
         self.base = np.zeros(0, np.float64)         # what a client that never exchanged has seen
         self.lock = threading.Lock()
         self.exchanges = 0
+        self.incarnations: dict[str, int] = {}      # client addr -> incarnation its ``old`` belongs to
+        self.max_anonymous = 64                     # bound on per-connection entries (peer() strings)
 
     def _grow(self, n: int) -> None:
         self.model = _grown(self.model, n)
@@ -56,9 +58,33 @@ class ParameterServer:
             return self.old
         o = self.olds.get(client)
         # a new client has seen nothing yet: everything the PS holds is news to it
+        if o is None and client not in self.incarnations:
+            self._evict_anonymous()
         o = _grown(self.base.copy() if o is None else o, self.model.size)
         self.olds[client] = o
         return o
+
+    def _evict_anonymous(self) -> None:
+        """Reference-style clients are keyed by their connection (``context.peer()``), a new
+        key per connection: keep at most ``max_anonymous`` of them (oldest dropped first)."""
+        anon = [k for k in self.olds if k not in self.incarnations]
+        for k in anon[:max(0, len(anon) - self.max_anonymous + 1)]:
+            del self.olds[k]
+
+    def client_joined(self, client: str, incarnation: int = 0) -> None:
+        """A worker (re-)registered.  A new incarnation at a known address is a different
+        process: it has seen none of the PS model, so its ``old`` restarts from ``base``
+        instead of inheriting its predecessor's (which would hide everything the PS had
+        accumulated before the restart from the echo-free client)."""
+        with self.lock:
+            if self.incarnations.get(client) != incarnation:
+                self.olds.pop(client, None)
+            self.incarnations[client] = incarnation
+
+    def client_left(self, client: str) -> None:
+        with self.lock:
+            self.olds.pop(client, None)
+            self.incarnations.pop(client, None)
 
     def _set_old(self, client: str | None) -> None:
         if not self.per_client or client is None:
@@ -83,10 +109,15 @@ class ParameterServer:
             return self.model - self._old_for(client)
 
     def absorb_reply(self, reply: np.ndarray, sent: np.ndarray | None = None, client: str | None = None) -> None:
-        """Master-side mixing of a worker's reply to a broadcast; then o[client] = m.
+        """Master-side mixing of a worker's reply to a broadcast.
 
         With ``sent`` given (echo-free), the echo ``alpha*sent`` is removed first, as the
-        worker-side client does (parallel/gossip.py)."""
+        worker-side client does (parallel/gossip.py).  ``o[client]`` then advances by exactly
+        what was shared with that client -- ``sent`` plus what its reply brought in -- not to
+        the whole model: another client's exchange that landed while the broadcast RPC was in
+        flight was never sent to ``client`` and must stay pending for it (the in-flight race
+        ``GossipState.absorb`` handles on the worker side).  The single shared ``old`` of the
+        reference rule keeps ``o = m``."""
         with self.lock:
             r = np.asarray(reply, np.float64)
             self._grow(r.size)
@@ -95,7 +126,12 @@ class ParameterServer:
                 r = r.copy()
                 r[:s.size] -= self.alpha * s
             self.model[:r.size] += self.alpha * r
-            self._set_old(client)
+            if not self.per_client or client is None or sent is None:
+                self._set_old(client)
+                return
+            o = self._old_for(client)
+            o[:s.size] += s
+            o[:r.size] += self.alpha * r
 
     def set_model(self, flat: np.ndarray) -> None:
         with self.lock:

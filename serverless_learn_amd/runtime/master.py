@@ -90,6 +90,7 @@ class Master:
                                                       info.incarnation, self.clock())
         with self._lock:
             self.incarnation[info.addr] = info.incarnation
+        self.ps.client_joined(info.addr, info.incarnation)
         self.log.info("register_birth", worker=info.addr, epoch=epoch, changed=changed, gpus=info.num_gpus,
                       world=len(self.registry.members()))
         if changed:
@@ -103,6 +104,7 @@ class Master:
             with self._lock:
                 self.delivered.pop(info.addr, None)
                 self.ckpt_delivered.pop(info.addr, None)
+            self.ps.client_left(info.addr)
         self.log.info("deregister", worker=info.addr, existed=existed, epoch=self.registry.epoch(),
                       world=len(self.registry.members()))
         if existed:
@@ -167,6 +169,7 @@ class Master:
                     self.delivered.pop(addr, None)
                     self.ckpt_delivered.pop(addr, None)
                     self.feedback.pop(addr, None)
+                self.ps.client_left(addr)
                 self.log.info("evicted", worker=addr, epoch=self.registry.epoch(), world=len(self.registry.members()))
                 self._notify()
 

@@ -14,7 +14,9 @@ deadline; message caps are raised so a full-model ``Update`` fits.
 """
 from __future__ import annotations
 
+import random
 import threading
+import time
 from concurrent import futures
 
 import grpc
@@ -22,6 +24,16 @@ import grpc
 from ..proto import messages as pb
 
 _RETRYABLE = {grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.DEADLINE_EXCEEDED}
+
+# Unary RPCs that may be re-sent after a transient failure: re-delivery has no extra effect
+# (CheckUp replaces the receiver's view, the others read state or set it to the same value).
+# ExchangeUpdates mixes models and DoPush re-streams a whole shard: never retried here.  The
+# reference only logs a failed call (master.cc:156-158, :192-194).
+IDEMPOTENT = frozenset({
+    ("Worker", "CheckUp"), ("FileServer", "CheckUp"), ("MasterControl", "GetMembership"),
+    ("FileStore", "ListFiles"), ("MasterControl", "ReportCheckpoint"), ("MasterControl", "Deregister"),
+    ("Master", "RegisterBirth"),
+})
 
 
 class RpcFailure(RuntimeError):
@@ -88,11 +100,19 @@ class RpcServer:
 class Channels:
     """Per-address channel cache with deadlines (fixes master.cc:257's TODO(PERF))."""
 
-    def __init__(self, max_message_bytes: int = 256 << 20, default_timeout: float = 5.0):
+    def __init__(self, max_message_bytes: int = 256 << 20, default_timeout: float = 5.0, retries: int = 4,
+                 backoff_s: float = 0.05):
+        self.retries = retries      # extra attempts for idempotent unary RPCs
+        self.backoff_s = backoff_s  # first back-off; doubles per attempt, +-50 % jitter
+        self.retried = 0            # attempts re-sent (metrics / tests)
         self._lock = threading.Lock()
         self._channels: dict[str, grpc.Channel] = {}
         self._stubs: dict[tuple, object] = {}
-        self._opts = _options(max_message_bytes)
+        # reconnect quickly: gRPC's default first reconnect back-off is 1 s, during which every
+        # call on the channel fails at once (a retry could never see a restarted listener)
+        self._opts = _options(max_message_bytes) + [
+            ("grpc.initial_reconnect_backoff_ms", 100), ("grpc.min_reconnect_backoff_ms", 100),
+            ("grpc.max_reconnect_backoff_ms", 2000)]
         self.default_timeout = default_timeout
 
     def channel(self, addr: str) -> grpc.Channel:
@@ -116,12 +136,32 @@ class Channels:
         return s
 
     def unary(self, addr: str, service: str, method: str, request: bytes, timeout: float | None = None,
-              metadata=None) -> bytes:
+              metadata=None, idempotent: bool | None = None) -> bytes:
+        """One unary call with a deadline.  Idempotent methods (``IDEMPOTENT``, or
+        ``idempotent=True``) are re-sent with bounded exponential back-off on UNAVAILABLE /
+        DEADLINE_EXCEEDED, all attempts inside the ONE deadline ``timeout`` -- so a caller's
+        failure-detection timing (the master's miss counting) is unchanged: a peer that is
+        really gone still fails within ``timeout``, while a dropped connection or a restarting
+        listener no longer costs a miss."""
         stub = self._stub(addr, service, method, "uu")
-        try:
-            return stub(request, timeout=timeout or self.default_timeout, metadata=metadata)
-        except grpc.RpcError as e:  # pragma: no cover - exercised by failure tests
-            raise RpcFailure(pb.method_path(service, method), addr, e.code(), e.details() or "") from None
+        budget = timeout or self.default_timeout
+        deadline = time.monotonic() + budget
+        retry = (service, method) in IDEMPOTENT if idempotent is None else idempotent
+        attempt = 0
+        while True:
+            left = deadline - time.monotonic()
+            try:
+                return stub(request, timeout=max(0.001, left), metadata=metadata)
+            except grpc.RpcError as e:
+                fail = RpcFailure(pb.method_path(service, method), addr, e.code(), e.details() or "")
+            wait = self.backoff_s * (2 ** attempt) * (0.5 + random.random())
+            if not (retry and fail.retryable and attempt < self.retries
+                    and deadline - time.monotonic() > wait + 0.01):
+                raise fail
+            attempt += 1
+            with self._lock:
+                self.retried += 1
+            time.sleep(wait)
 
     def stream_unary(self, addr: str, service: str, method: str, requests, timeout: float | None = None,
                      metadata=None) -> bytes:

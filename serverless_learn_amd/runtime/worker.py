@@ -81,11 +81,18 @@ class Worker:
         self.trainer = None
         self.xgmi = None  # parallel.xgmi.XgmiExchange while an RCCL group of MLP workers is live
         self.gossip: GossipState | None = None
-        self.group = ElasticGroup(device=self.device, timeout_s=float(self.cfg.extra.get("dp_timeout_s", 30.0)))
+        backend = None if self.cfg.dp_backend == "auto" else self.cfg.dp_backend
+        timeout = float(self.cfg.extra.get("dp_timeout_s", self.cfg.dp_timeout_s))
+        self.group = ElasticGroup(backend=backend, device=self.device, timeout_s=timeout)
         self.step = 0
         self.samples = 0
         self.loss = float("nan")
         self.rate = 0.0
+        self.group_metrics = {"samples_per_sec": 0.0, "loss": 0.0, "accuracy": 0.0, "world": 0}
+        self.resumed_step = -1
+        self._resume_pulled = 0   # PeerList.resume_file already pulled from the file server
+        self.graph_chunks = 0     # graph replays run (tests / feedback)
+        self._agreed_epoch = -1   # newest membership epoch the whole lock-step group has agreed to see
         self.bytes_ingested = 0
         self.files_received: list[int] = []
         self.state = "idle"
@@ -207,10 +214,12 @@ class Worker:
         with self.view_lock:
             self.view = {"epoch": pl.epoch, "peers": list(pl.peer_addrs), "rank": pl.rank,
                          "world": pl.world_size, "rendezvous": pl.rendezvous, "resume_file": pl.resume_file}
+        gm = self.group_metrics
         fb = pb.FlowFeedback(step=self.step, samples_per_sec=self.rate,
                              loss=self.loss if self.loss == self.loss else 0.0,
                              bytes_ingested=self.bytes_ingested, epoch=self.group.epoch if self.group.epoch >= 0 else 0,
-                             state=self.state)
+                             state=self.state, group_samples_per_sec=gm["samples_per_sec"],
+                             group_loss=gm["loss"], group_accuracy=gm["accuracy"], group_world=gm["world"])
         return fb.SerializeToString()
 
     def _exchange_updates(self, request: bytes, context) -> bytes:
@@ -227,7 +236,7 @@ class Worker:
 
     # ---- checkpoints -----------------------------------------------------------
     def _load_checkpoint(self, data: bytes) -> None:
-        meta, params, mom = ckfmt.decode(data)
+        meta, params, mom, extra = ckfmt.decode_full(data)
         with self.train_lock:
             self._ensure_trainer()
             if self.trainer is None:
@@ -241,10 +250,14 @@ class Worker:
             self.trainer.set_flat(torch.from_numpy(params))
             if mom is not None and self.trainer.mom is not None:
                 self.trainer.mom[:self.trainer.n_params].copy_(torch.from_numpy(mom))
+            if extra and hasattr(self.trainer, "load_state_extra"):
+                self.trainer.load_state_extra(extra)  # batch cursor, BN running statistics
+            self.trainer.graph = None  # a captured graph holds the old state's launches
             self.step = int(meta.get("step", 0))
+            self.resumed_step = self.step
             if self.gossip is not None:
                 self.gossip.old.copy_(self._flat_view())
-        self.log.info("checkpoint_loaded", step=self.step, epoch=meta.get("epoch"))
+        self.log.info("checkpoint_loaded", step=self.step, epoch=meta.get("epoch"), extra=sorted(extra))
 
     def save_checkpoint(self) -> int:
         with self.train_lock:
@@ -254,7 +267,8 @@ class Worker:
             meta = {"model": self.trainer.model_name, "step": self.step, "epoch": self.group.epoch,
                     "layout": self.trainer.layout(),
                     "optimizer": {"lr": self.cfg.lr, "momentum": self.cfg.momentum}}
-        data = ckfmt.encode(flat, meta, mom)
+            extra = self.trainer.state_extra() if hasattr(self.trainer, "state_extra") else {}
+        data = ckfmt.encode(flat, meta, mom, extra)
         file_num = ckfmt.CKPT_BASE + self.ckpt_slot
         self.ckpt_slot ^= 1  # two alternating slots: never overwrite one being served
         raw = self.channels.stream_unary(self.cfg.file_server_addr, "FileStore", "StoreFile", iter_chunks(data),
@@ -309,15 +323,68 @@ class Worker:
                     self.view = dict(self.view, epoch=0, rank=-1)
                 self.registered.clear()
 
+    def _ensure_resumed(self, resume_file: int) -> None:
+        """Consume ``PeerList.resume_file``: a worker that has not trained yet (a fresh join,
+        or a whole replacement group after every original member died) pulls the group's
+        latest checkpoint from the file server before the group syncs state, so rank 0 never
+        broadcasts untrained weights over a checkpoint the job already has.  The pull is the
+        ordinary DoPush -> ReceiveFile path (the file server streams it into our ring and
+        ``_load_checkpoint`` applies it); it does not depend on the master having pushed
+        the checkpoint before the data."""
+        if (not resume_file or resume_file == self._resume_pulled or self.step > 0
+                or self.resumed_step >= 0 or self.cfg.model == "simulate"):
+            return
+        self._resume_pulled = resume_file
+        req = pb.Push(recipient_addr=self.addr, file_num=resume_file).SerializeToString()
+        try:
+            raw = self.channels.unary(self.cfg.file_server_addr, "FileServer", "DoPush", req,
+                                      timeout=max(60.0, self.cfg.rpc_timeout_s))
+            ok = pb.PushOutcome.FromString(raw).ok
+        except RpcFailure as e:
+            ok = False
+            self.log.warn("resume_pull_failed", file_num=resume_file, error=str(e))
+        self.log.info("resume_pulled", file_num=resume_file, ok=ok, step=self.step)
+
+    def _needs_regroup(self, v: dict) -> bool:
+        """A live lock-step group (world > 1) switches epochs only at a step boundary every
+        member agreed on (``_agree``): members learn of a join from their CheckUps at
+        different times, and one that left while the others still ran steps would stall
+        theirs (the xGMI barrier, RCCL) until a timeout.  A broken group, or a worker
+        with no group, re-forms as soon as its view changes."""
+        if v["epoch"] == 0 or v["rank"] < 0:
+            return False
+        if self.group.broken:
+            return True
+        if v["epoch"] == self.group.epoch:
+            return False
+        if self.group.active and self.group.world > 1:
+            return self._agreed_epoch > self.group.epoch and v["epoch"] >= self._agreed_epoch
+        return True
+
+    def _agree(self, have_data: bool | None = None):
+        """One MAX all-reduce over the live group of [view epoch, -have_data]: returns
+        (newest epoch any member sees, every member has data).  Posted asynchronously
+        right after a step chunk is queued, so it overlaps the GPU work."""
+        with self.view_lock:
+            ep = float(self.view["epoch"])
+        dev = self.device if self.group.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([ep, -1.0 if (have_data is None or have_data) else 0.0], dtype=torch.float64, device=dev)
+        work = self.group.allreduce_async(t, torch.distributed.ReduceOp.MAX)
+
+        def result():
+            self.group.wait(work)
+            v = t.cpu()
+            return int(v[0]), bool(v[1] < -0.5)
+        return result
+
     def _maybe_regroup(self) -> None:
         with self.view_lock:
             v = dict(self.view)
-        if v["epoch"] == 0 or v["rank"] < 0:
-            return
-        if v["epoch"] == self.group.epoch and not self.group.broken:
+        if not self._needs_regroup(v):
             return
         self.state = "regrouping"
-        self._drop_xgmi()
+        self._drop_xgmi(healthy=not self.group.broken)
+        self._ensure_resumed(v.get("resume_file", 0))
         with trace.span("regroup", epoch=v["epoch"], world=v["world"]):
             ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"])
             if not ok:
@@ -332,7 +399,8 @@ class Worker:
                     self._set_world(max(1, v["world"]))
                     t = self.trainer
                     try:
-                        self.group.sync_state([t.params, t.mom])
+                        bufs = t.buffers() if hasattr(t, "buffers") else []
+                        self.group.sync_state([t.params, t.mom, *bufs])
                         step = torch.tensor([self.step], dtype=torch.int64, device=t.params.device)
                         self.group.broadcast_(step, 0)
                         self.step = int(step.item())
@@ -347,16 +415,27 @@ class Worker:
         self.state = "training"
 
     # ---- xGMI exchange (parallel/xgmi.py) -----------------------------------------
-    def _setup_xgmi(self) -> None:
-        """MLP on an RCCL group: aggregate through IPC-mapped exchange buffers over xGMI
-        instead of an RCCL all-reduce per step.  Collective over the group; any rank that
-        cannot map its peers makes every rank keep RCCL."""
+    def _xgmi_wanted(self) -> bool:
+        """GPU MLP groups aggregate over xGMI.  RCCL groups always may; a gloo group of GPU
+        workers (ranks sharing one GPU: the elastic rehearsal) only when ``SL_XGMI_GLOO=1``,
+        as ``bench.py`` rehearses it."""
         from ..parallel import xgmi
 
         t = self.trainer
-        if (t is None or not hasattr(t, "enable_xgmi") or self.group.backend != "nccl" or self.group.world < 2
-                or self.group.world > xgmi.MAX_WORLD or not xgmi.enabled()):
+        if not (self.cfg.xgmi and t is not None and hasattr(t, "enable_xgmi") and self.device.type == "cuda"
+                and 2 <= self.group.world <= xgmi.MAX_WORLD and xgmi.enabled()):
+            return False
+        return self.group.backend == "nccl" or os.environ.get("SL_XGMI_GLOO", "0") == "1"
+
+    def _setup_xgmi(self) -> None:
+        """MLP on a GPU group: aggregate through IPC-mapped exchange buffers over xGMI
+        instead of an RCCL all-reduce per step.  Collective over the group; any rank that
+        cannot map its peers makes every rank keep the process group's all-reduce."""
+        from ..parallel import xgmi
+
+        if not self._xgmi_wanted():
             return
+        t = self.trainer
         hsize = int(xgmi.N.lib().sl_ipc_handle_size())
         try:
             ex = xgmi.XgmiExchange(t.n_pad, self.group.rank, self.group.world, self.device,
@@ -369,34 +448,124 @@ class Worker:
         t.enable_xgmi(ex)
         self.log.info("xgmi_enabled", epoch=self.group.epoch, world=self.group.world, two_shot=ex.two_shot)
 
-    def _drop_xgmi(self) -> None:
+    def _drop_xgmi(self, healthy: bool = False) -> None:
+        """Leave the exchange.  A peer may still have queued steps that read this rank's
+        buffer or signal into it, so on a healthy group every member first drains its GPU
+        and meets the others at a group barrier before unmapping; on a broken group (a peer
+        died: its barrier timed out, later ones skip their wait) the local drain is all that
+        can be done -- the survivors' queued steps finish within microseconds, and a dead
+        peer's mapping keeps the freed memory alive until its process is gone."""
         ex, self.xgmi = self.xgmi, None
         if ex is None:
             return
         with self.train_lock:
             if self.trainer is not None and hasattr(self.trainer, "enable_xgmi"):
                 self.trainer.enable_xgmi(None)
-        ex.close()
+        torch.cuda.synchronize(self.device)
+        closed_with_barrier = False
+        if healthy and self.group.active:
+            try:
+                closed_with_barrier = self.group.all_true(not ex.error())
+            except GroupBroken:
+                pass
+        ex.close(sync=False)
+        self.log.info("xgmi_closed", epoch=self.group.epoch, barrier=closed_with_barrier)
 
     def _install_allreduce(self) -> None:
-        """Gradient hook follows the group: set whenever a >1 group is live, cleared otherwise.
-
-        Called after every re-form and before every step, so a trainer created after the
-        group formed (first shard arriving late) still reduces its gradients.  With the
-        xGMI exchange live the update kernel aggregates by itself: no hook."""
-        if self.trainer is None:
+        """Gradient aggregation follows the group: set whenever a >1 group is live, cleared
+        otherwise.  Called after every re-form and before every step chunk, so a trainer
+        created after the group formed (first shard arriving late) still reduces its
+        gradients.  With the xGMI exchange live the update kernel aggregates by itself: no
+        hook.  Trainers with bucket hooks (the ResNet engine) launch one async all-reduce
+        per bucket during backward instead of one blocking all-reduce after it."""
+        t = self.trainer
+        if t is None:
             return
-        live = self.group.active and self.group.world > 1
-        want = self.group.allreduce_ if live and self.xgmi is None else None
-        if self.trainer.allreduce != want:
-            self.trainer.allreduce = want
-            self._set_world(max(1, self.group.world) if live else 1)
+        live = self.group.active and self.group.world > 1 and self.xgmi is None
+        bucketed = hasattr(t, "bucket_hook")
+        want = self.group.allreduce_ if live and not bucketed else None
+        want_hook = self._bucket_hook if live and bucketed else None
+        changed = t.allreduce != want or (bucketed and t.bucket_hook != want_hook)
+        if changed:
+            t.allreduce = want
+            if bucketed:
+                t.bucket_hook = want_hook
+                t.bucket_wait = self._bucket_wait if want_hook else None
+                t.graph = None
+            self._set_world(max(1, self.group.world) if self.group.active and self.group.world > 1 else 1)
+
+    def _bucket_hook(self, view: torch.Tensor):
+        return self.group.allreduce_async(view)
+
+    def _bucket_wait(self, works) -> None:
+        for w in works:
+            if w is None:
+                continue
+            try:
+                w.wait()
+            except Exception as e:
+                self.group.broken = True
+                raise GroupBroken(repr(e)) from e
+
+    # ---- training ------------------------------------------------------------------
+    def _use_graph(self) -> bool:
+        """hipGraph replay of whole steps: the fused GPU engines, with no host-side collective
+        inside the step (world 1, or the xGMI exchange, which is itself captured)."""
+        t = self.trainer
+        return (self.cfg.graph and self.device.type == "cuda" and hasattr(t, "capture")
+                and t.allreduce is None and getattr(t, "bucket_hook", None) is None)
+
+    def _run_chunk(self, n: int) -> int:
+        """Run up to ``n`` steps; returns how many ran.  Graph mode replays a captured
+        k-step graph (re-captured whenever load_shard / set_world / enable_xgmi / a
+        checkpoint load dropped it); eager mode runs one step."""
+        t = self.trainer
+        if not self._use_graph():
+            t.step()
+            return 1
+        k = max(1, self.cfg.graph_steps)
+        if t.graph is None:
+            # one eager step first (sizes lazily-grown workspaces), then capture
+            t.step()
+            if hasattr(t, "steps"):
+                t.capture(warmup=0, unroll=k)
+            else:
+                t.capture(warmup=0)
+            self.log.info("graph_captured", steps=k, step=self.step + 1)
+            return 1
+        n = min(n, k)
+        if hasattr(t, "steps"):
+            t.steps(n)
+        else:
+            for _ in range(n):
+                t.step()
+        self.graph_chunks += 1
+        return n
+
+    def _group_metrics_update(self, dt: float, samples: int, st) -> None:
+        """N3: all-reduce [loss_sum, correct_sum, samples] (SUM) and the interval (MAX) over
+        the group every log_every steps: the job-level samples/s is total samples over the
+        slowest rank's time.  Every member of a lock-step group calls this at the same step."""
+        if not (self.group.active and self.group.world > 1):
+            self.group_metrics = {"samples_per_sec": samples / max(dt, 1e-9), "loss": st.loss,
+                                  "accuracy": st.accuracy, "world": 1}
+            return
+        dev = self.device if self.group.backend == "nccl" else torch.device("cpu")
+        b = float(self.trainer.batch)
+        v = torch.tensor([st.loss * b, st.accuracy * b, b, float(samples)], dtype=torch.float64, device=dev)
+        m = torch.tensor([dt], dtype=torch.float64, device=dev)
+        self.group.allreduce_(v)
+        self.group.allreduce_(m, torch.distributed.ReduceOp.MAX)
+        v, m = v.cpu(), float(m.item())
+        self.group_metrics = {"samples_per_sec": float(v[3]) / max(m, 1e-9), "loss": float(v[0] / v[2]),
+                              "accuracy": float(v[1] / v[2]), "world": self.group.world}
 
     def _train_loop(self) -> None:
         if self.cfg.model == "simulate":
             return self._simulate_loop()
         t_last, s_last = time.perf_counter(), 0
         ready_epoch = -1
+        inflight = None  # event recorded after the previous chunk: at most two chunks queued
         while not self._stop.is_set():
             with self.train_lock:
                 if self._pending_shard is not None:
@@ -409,21 +578,30 @@ class Worker:
             if self.cfg.sync == "allreduce":
                 self._maybe_regroup()
                 self._install_allreduce()
+                if self.group.active and self._agreed_epoch > self.group.epoch:
+                    # the group agreed to move to a newer epoch that this worker's view has
+                    # not reached yet: no more steps on the old group, wait for the CheckUp
+                    self.state = "regrouping"
+                    self._stop.wait(0.05)
+                    continue
                 if self.view["world"] > 1:
                     if not self.group.active:
                         self._stop.wait(0.05)
                         continue
                     if ready_epoch != self.group.epoch:
-                        # every member must have data before the first lock-step collective
-                        flag = torch.ones(1) if have_data else torch.zeros(1)
-                        if self.group.backend == "nccl":
-                            flag = flag.to(self.device)
+                        # every member must have data before the first lock-step collective;
+                        # the same all-reduce agrees on the newest epoch any member has seen
                         try:
-                            self.group.allreduce_(flag)
+                            agreed, all_data = self._agree(have_data)()
                         except GroupBroken:
                             continue
-                        if int(flag.item()) == self.group.world:
+                        self._agreed_epoch = max(self._agreed_epoch, agreed)
+                        if agreed > self.group.epoch:
+                            self._drop_xgmi(healthy=True)
+                            continue
+                        if all_data:
                             ready_epoch = self.group.epoch
+                            t_last, s_last = time.perf_counter(), self.samples
                         else:
                             self.state = "waiting_for_data"
                             self._stop.wait(0.1)
@@ -433,30 +611,73 @@ class Worker:
                 self.has_data.wait(0.2)
                 self.has_data.clear()
                 continue
+            want = self.cfg.max_steps - self.step if self.cfg.max_steps else 1 << 30
+            # chunks end on log / checkpoint boundaries, so every member of a lock-step group
+            # runs its group collectives (metrics) at the same step
+            for every in (self.cfg.log_every, self.cfg.checkpoint_every):
+                if every:
+                    want = min(want, every - self.step % every)
+            prev = self.step
             try:
-                with self.train_lock, trace.span("step", step=self.step):
-                    self.trainer.step()
+                with self.train_lock, trace.span("steps", step=self.step):
+                    ran = self._run_chunk(want)
             except GroupBroken as e:
                 self.log.warn("collective_failed", error=str(e), epoch=self.group.epoch)
                 continue
-            self.step += 1
-            self.samples += self.trainer.batch
+            self.step += ran
+            self.samples += ran * self.trainer.batch
             self.state = "training"
-            self.fault.on_step(self.step)
-            if self.cfg.log_every and self.step % self.cfg.log_every == 0:
-                if self.xgmi is not None and self.xgmi.error():
-                    # a peer stopped answering the step barrier: results since are void,
-                    # re-form (the master's next epoch) and resync from rank 0
-                    self.log.warn("xgmi_barrier_timeout", epoch=self.group.epoch)
-                    self.group.broken = True
+            for s_i in range(prev + 1, self.step + 1):
+                self.fault.on_step(s_i)
+            lockstep = self.cfg.sync == "allreduce" and self.group.active and self.group.world > 1
+            agreement = None
+            if lockstep:
+                try:
+                    agreement = self._agree()
+                except GroupBroken as e:
+                    self.log.warn("collective_failed", error=str(e), epoch=self.group.epoch)
+                    continue
+            if self.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record()
+                if inflight is not None:
+                    inflight.synchronize()
+                inflight = ev
+            if agreement is not None:
+                try:
+                    agreed, _ = agreement()
+                except GroupBroken as e:
+                    self.log.warn("collective_failed", error=str(e), epoch=self.group.epoch)
+                    continue
+                if agreed > self.group.epoch:
+                    # every member is at this same step boundary: leave the exchange together
+                    self._agreed_epoch = max(self._agreed_epoch, agreed)
+                    self._drop_xgmi(healthy=True)
+            if self.xgmi is not None and self.xgmi.error():
+                # a peer stopped answering the step barrier (checked at every chunk boundary,
+                # i.e. every graph replay): results since are void -- re-form (the master's
+                # next epoch) and resync from rank 0
+                self.log.warn("xgmi_barrier_timeout", epoch=self.group.epoch, step=self.step)
+                self.group.broken = True
+                continue
+            if self.cfg.log_every and self.step // self.cfg.log_every != prev // self.cfg.log_every:
                 st = self.trainer.stats()
                 now = time.perf_counter()
-                self.rate = (self.samples - s_last) / max(1e-9, now - t_last)
-                t_last, s_last = now, self.samples
+                dt = max(1e-9, now - t_last)
+                self.rate = (self.samples - s_last) / dt
+                try:
+                    self._group_metrics_update(dt, self.samples - s_last, st)
+                except GroupBroken as e:
+                    self.log.warn("group_metrics_failed", error=str(e))
+                t_last, s_last = time.perf_counter(), self.samples
                 self.loss = st.loss
+                gm = self.group_metrics
                 self.log.info("train", step=self.step, loss=round(st.loss, 4), acc=round(st.accuracy, 4),
-                              samples_per_sec=round(self.rate, 1), epoch=self.group.epoch)
-            if (self.cfg.checkpoint_every and self.step % self.cfg.checkpoint_every == 0
+                              samples_per_sec=round(self.rate, 1), epoch=self.group.epoch,
+                              group_samples_per_sec=round(gm["samples_per_sec"], 1), group_world=gm["world"],
+                              group_loss=round(gm["loss"], 4), graph=self._use_graph(),
+                              param_sum=float(self.trainer.params.double().sum()))
+            if (self.cfg.checkpoint_every and self.step // self.cfg.checkpoint_every != prev // self.cfg.checkpoint_every
                     and (self.group.rank <= 0)):
                 try:
                     self.save_checkpoint()
@@ -542,7 +763,7 @@ class Worker:
         self.has_data.set()
         for t in self._threads:
             t.join(timeout=10)
-        self._drop_xgmi()
+        self._drop_xgmi(healthy=False)
         self.group.teardown()
         if self.server:
             self.server.stop()

@@ -46,6 +46,10 @@ class Metrics:
         self.rate = Gauge("sl_samples_per_second", "training throughput (samples/s)", ["role"], registry=r)
         self.epoch = Gauge("sl_membership_epoch", "membership epoch", ["role"], registry=r)
         self.world = Gauge("sl_world_size", "members of the data-parallel group", ["role"], registry=r)
+        self.job_rate = Gauge("sl_job_samples_per_second", "whole-job training throughput (samples/s) "
+                              "derived by the master from the workers' feedback", ["role"], registry=r)
+        self.group_rate = Gauge("sl_group_samples_per_second", "data-parallel group throughput (samples/s, "
+                                "all-reduced over the group)", ["role"], registry=r)
         self.ingested = Counter("sl_ingested_bytes", "bytes landed by ReceiveFile", ["role"], registry=r)
         self.ingest_s = Histogram("sl_ingest_seconds", "ReceiveFile duration", ["role"], buckets=_BUCKETS,
                                   registry=r)
@@ -67,6 +71,11 @@ class Metrics:
                 for k, g in (("step", self.step), ("loss", self.loss), ("samples_per_sec", self.rate)):
                     if isinstance(fields.get(k), (int, float)):
                         g.labels(role).set(fields[k])
+                if isinstance(fields.get("group_samples_per_sec"), (int, float)):
+                    self.group_rate.labels(role).set(fields["group_samples_per_sec"])
+            elif event == "job":
+                if isinstance(fields.get("samples_per_sec"), (int, float)):
+                    self.job_rate.labels(role).set(fields["samples_per_sec"])
             elif event == "received_file":
                 if isinstance(fields.get("bytes"), (int, float)):
                     self.ingested.labels(role).inc(fields["bytes"])

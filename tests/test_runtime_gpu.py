@@ -175,7 +175,7 @@ def test_bench_two_ranks_autotune_and_replicas():
     cmd = ["timeout", "-k", "10", "150", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "3", "--batch", "4096",
-           "--dist-backend", "gloo", "--ingest", "local"]
+           "--dist-backend", "gloo", "--oversubscribe", "--ingest", "local"]
     p = subprocess.run(cmd, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=170)
     assert p.returncode == 0, p.stdout[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
@@ -190,3 +190,37 @@ def test_bench_two_ranks_autotune_and_replicas():
     fastest = {names[k] for k in names if at[k] == best}  # (rounded values may tie)
     assert out["config"]["collective_backend"] in fastest, (out["config"]["collective_backend"], at)
     assert abs(out["value"] - 8192 / (out["ms_per_step"] / 1e3)) / out["value"] < 0.03
+
+
+def _bench_self_launch(extra, timeout=240):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = ["timeout", "-k", "10", str(timeout), sys.executable, os.path.join(root, "bench.py"), *extra]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(cmd, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=timeout + 20, env=env)
+    assert p.returncode == 0, p.stdout[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout[-4000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("model,extra", [
+    ("mlp", ["--batch", "4096", "--steps", "8", "--warmup", "3", "--ingest", "local"]),
+    ("resnet18", ["--batch", "64", "--steps", "3", "--warmup", "2", "--ingest", "device", "--bucket-mb", "4"]),
+])
+def test_bench_self_launches_two_ranks(model, extra):
+    """``bench.py --gpus 2`` with no launcher spawns the two rank processes itself (here sharing the
+    one GPU over gloo, --oversubscribe) and reports a real dp2 number: both models, replicas
+    identical after the timed steps (the ResNet path through the async bucket hooks)."""
+    out = _bench_self_launch(["--gpus", "2", "--oversubscribe", "--dist-backend", "gloo", "--model", model, *extra])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["dist"]["world_size"] == 2 and out["dist"]["launcher"] == "bench.py"
+    assert out["dist"]["ranks_share_gpus"] is True
+    assert out["replicas_identical"] is True, out
+    b = int(extra[extra.index("--batch") + 1])
+    assert out["config"]["global_batch"] == 2 * b

@@ -169,3 +169,43 @@ def test_receive_file_short_stream_is_rejected(ch):
         assert full.ok and w._pending_shard is not None
     finally:
         w.stop(leave=False)
+
+
+def test_idempotent_rpc_retries_until_listener_is_back(ch):
+    """An idempotent unary RPC (FileServer.CheckUp) to a server that is restarting is
+    re-sent with back-off inside its one deadline and succeeds once the listener is up;
+    a non-idempotent one (ExchangeUpdates) fails at once; a dead peer still fails within
+    the deadline."""
+    import socket
+    import threading
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    addr = f"127.0.0.1:{port}"
+    started = {}
+
+    def start_later():
+        time.sleep(0.4)
+        started["fs"] = FileServer(fast_config(shard_records=256), addr=addr).start()
+
+    th = threading.Thread(target=start_later)
+    th.start()
+    try:
+        t0 = time.monotonic()
+        raw = ch.unary(addr, "FileServer", "CheckUp", pb.Empty().SerializeToString(), timeout=4.0)
+        pb.LoadFeedback.FromString(raw)
+        assert ch.retried >= 1 and time.monotonic() - t0 < 4.0
+    finally:
+        th.join()
+        started["fs"].stop()
+    # nothing listens any more: fails within the deadline, never hangs past it
+    t0 = time.monotonic()
+    with pytest.raises(RpcFailure):
+        ch.unary(addr, "FileServer", "CheckUp", pb.Empty().SerializeToString(), timeout=0.8)
+    assert time.monotonic() - t0 < 2.0
+    before = ch.retried
+    with pytest.raises(RpcFailure):
+        ch.unary(addr, "Worker", "ExchangeUpdates", codec.encode_update(np.zeros(2)), timeout=0.8)
+    assert ch.retried == before

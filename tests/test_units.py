@@ -273,3 +273,80 @@ def test_mlp_dw1_fp16_coefficients_reproduce_normalised_gradient():
     np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-18)
     ref = dh.T @ (xa * x + xb)  # the gradient w.r.t. W1 of the normalised input
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-18)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """``bench.py --gpus 8`` on a machine with fewer devices exits non-zero and prints no
+    JSON line: it never reports an N-GPU number measured on fewer GPUs (here: 0 visible)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--steps", "2"],
+                       cwd=root, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=120, env=env)
+    assert p.returncode != 0
+    assert '"metric"' not in p.stdout
+    assert "refusing" in p.stderr
+    # a torchrun-style rank whose WORLD_SIZE disagrees with --gpus is refused too
+    env2 = dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8"], cwd=root,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=120, env=env2)
+    assert p.returncode == 2 and '"metric"' not in p.stdout
+
+
+def test_ps_new_incarnation_restarts_old_and_anonymous_entries_are_bounded():
+    from serverless_learn_amd.parallel.ps import ParameterServer
+
+    ps = ParameterServer(alpha=0.5)
+    ps.client_joined("w1", 1)
+    ps.exchange(np.ones(4), "w1")
+    ps.exchange(2 * np.ones(4), "w2")
+    # w1 restarts at the same address: the new process has seen nothing of the PS model
+    ps.client_joined("w1", 2)
+    r = ps.exchange(np.zeros(4), "w1")
+    np.testing.assert_allclose(r, ps.model)  # everything the PS holds is news to it
+    # the same incarnation re-registering (eviction + re-join) keeps its history
+    ps.client_joined("w1", 2)
+    assert "w1" in ps.olds
+    ps.max_anonymous = 4
+    for i in range(20):
+        ps.exchange(np.zeros(4), f"ipv4:127.0.0.1:{1000 + i}")
+    assert sum(1 for k in ps.olds if k.startswith("ipv4")) <= 4
+    ps.client_left("w1")
+    assert "w1" not in ps.olds
+
+
+def test_ps_broadcast_keeps_exchanges_that_land_in_flight():
+    """absorb_reply advances o[target] by what was shared, so another client's exchange that
+    lands while the broadcast RPC is in flight stays pending for the broadcast's target."""
+    from serverless_learn_amd.parallel.ps import ParameterServer
+
+    ps = ParameterServer(alpha=0.5)
+    ps.set_model(np.zeros(3))
+    ps.exchange(np.array([1.0, 0, 0]), "a")
+    sent = ps.pending_delta("b")               # broadcast to b starts
+    ps.exchange(np.array([0, 4.0, 0]), "c")     # lands while the RPC is in flight
+    reply = 0.5 * sent                          # b had no progress of its own: pure echo
+    ps.absorb_reply(reply, sent, "b")
+    pending = ps.pending_delta("b")
+    np.testing.assert_allclose(pending, [0, 2.0, 0])  # c's contribution is still news to b
+
+
+def test_gossip_compat_absorb_sets_old_to_model():
+    """compat mode keeps the reference's o = m after the client absorbs (worker.cc:215), even
+    when training stepped while the exchange was in flight."""
+    A = GossipState(torch.zeros(3, dtype=torch.float64), alpha=0.5, compat=True)
+    A.model += 1.0
+    d = A.make_delta()
+    A.model += 1.0  # a step lands while the RPC is in flight
+    A.absorb(np.full(3, 0.25), d)
+    torch.testing.assert_close(A.old, A.model)
+    B = GossipState(torch.zeros(3, dtype=torch.float64), alpha=0.5, compat=False)
+    B.model += 1.0
+    d = B.make_delta()
+    B.model += 1.0
+    B.absorb(np.full(3, 0.5), d)
+    # echo-free: the in-flight step stays unshared
+    torch.testing.assert_close(B.model - B.old, torch.ones(3, dtype=torch.float64))
