@@ -75,6 +75,9 @@ using namespace sl;
 #ifndef SL_MLP_APF
 #define SL_MLP_APF 1  // rows kernel: prefetch the next k-step's A fragments (3-slot X ring)
 #endif
+#ifndef SL_ROWS_KO
+#define SL_ROWS_KO 0  // timing knockouts of mlp_rows_kernel (1: every wave streams wave 0's weight columns, 2: no X loads)
+#endif
 #ifndef SL_MLP_XQ
 #define SL_MLP_XQ 4  // X prefetch distance in 64-column chunks (4 measured +1% over 2)
 #endif
@@ -329,6 +332,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
   // ROCm 7.2 emits a packed FMA that breaks the gfx950 constant-bus limit.
   const float nxa = a.xa + 0.f * (float)lane, nxb = a.xb + 0.f * (float)lane;
   auto xload = [&](int c) -> uint4 {
+    if (SL_ROWS_KO == 2) return make_uint4(c, xrow, 7, 9);
     return (c * 64 + xcol < D_IN) ? *reinterpret_cast<const uint4*>(xg + c * 64) : make_uint4(0, 0, 0, 0);
   };
   auto xstore = [&](int c, uint4 v) {
@@ -418,9 +422,10 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
     }
   };
 
-  const FragSrc f_w1(a.w1h, HID * D_INP * 2, NF * wng, KS1, lane);
-  const FragSrc f_w2(a.w2h, HID * HID * 2, NF * wng, KS2, lane);
-  const FragSrc f_w2t(a.w2th, HID * HID * 2, NF * wng, KS2, lane);
+  const int wcol = SL_ROWS_KO == 1 ? 0 : NF * wng;
+  const FragSrc f_w1(a.w1h, HID * D_INP * 2, wcol, KS1, lane);
+  const FragSrc f_w2(a.w2h, HID * HID * 2, wcol, KS2, lane);
+  const FragSrc f_w2t(a.w2th, HID * HID * 2, wcol, KS2, lane);
   const FragSrc f_w3(a.w3h, 16 * HID * 2, 0, KS2, lane);
   const FragSrc f_w3t(a.w3th, HID * 32 * 2, NF * wng, 1, lane);
 

@@ -93,6 +93,7 @@ class Worker:
         self._resume_pulled = 0   # PeerList.resume_file already pulled from the file server
         self.graph_chunks = 0     # graph replays run (tests / feedback)
         self._agreed_epoch = -1   # newest membership epoch the whole lock-step group has agreed to see
+        self._broken_since = None  # when the live group was first seen broken (monotonic s)
         self.bytes_ingested = 0
         self.files_received: list[int] = []
         self.state = "idle"
@@ -354,6 +355,15 @@ class Worker:
         if v["epoch"] == 0 or v["rank"] < 0:
             return False
         if self.group.broken:
+            if v["epoch"] == self.group.epoch and self.group.world > 1:
+                # a collective failed but the view has not changed yet: most likely a member
+                # died and the master will evict it within its miss window -- re-forming the
+                # same membership now would only wait out the rendezvous timeout on the dead
+                # peer.  Re-form the same epoch only once that window has passed.
+                if self._broken_since is None:
+                    self._broken_since = time.monotonic()
+                window = (self.cfg.max_misses + 1) * self.cfg.checkup_interval + self.cfg.rpc_timeout_s
+                return time.monotonic() - self._broken_since > window
             return True
         if v["epoch"] == self.group.epoch:
             return False
@@ -383,6 +393,7 @@ class Worker:
         if not self._needs_regroup(v):
             return
         self.state = "regrouping"
+        self._broken_since = None
         self._drop_xgmi(healthy=not self.group.broken)
         self._ensure_resumed(v.get("resume_file", 0))
         with trace.span("regroup", epoch=v["epoch"], world=v["world"]):
@@ -578,6 +589,10 @@ class Worker:
             if self.cfg.sync == "allreduce":
                 self._maybe_regroup()
                 self._install_allreduce()
+                if self.group.broken:
+                    self.state = "regrouping"  # waiting for the master's next view (see _needs_regroup)
+                    self._stop.wait(0.05)
+                    continue
                 if self.group.active and self._agreed_epoch > self.group.epoch:
                     # the group agreed to move to a newer epoch that this worker's view has
                     # not reached yet: no more steps on the old group, wait for the CheckUp

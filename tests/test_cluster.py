@@ -179,3 +179,27 @@ def test_master_ps_broadcast_loop():
         assert {a.addr, b.addr} & set(c.master.ps.olds)
     finally:
         c.stop()
+
+
+def test_group_metrics_are_allreduced_and_master_reports_job_rate(cluster):
+    """N3: every member of an all-reduce group reports the SAME group samples/s / loss (an
+    all-reduce over the group every log_every steps) in FlowFeedback; the master counts each
+    group once in its whole-job rate and exports it as a Prometheus gauge."""
+    a = cluster.add_worker(sync="allreduce", batch=256)
+    b = cluster.add_worker(sync="allreduce", batch=256)
+    assert cluster.wait_for(lambda: a.group_metrics["world"] == 2 and b.group_metrics["world"] == 2
+                            and a.step >= 60, 120), (a.group_metrics, b.group_metrics)
+
+    def agree():
+        f = cluster.master.feedback
+        if a.addr not in f or b.addr not in f:
+            return False
+        x, y = f[a.addr], f[b.addr]
+        return (x["group_world"] == 2 and y["group_world"] == 2
+                and x["group_samples_per_sec"] == y["group_samples_per_sec"] > 0)
+    assert cluster.wait_for(agree, 30), cluster.master.feedback
+    job = cluster.master.job_metrics()
+    f = cluster.master.feedback
+    assert job["groups"] == 1
+    assert job["samples_per_sec"] == pytest.approx(f[a.addr]["group_samples_per_sec"], rel=1e-3)
+    assert cluster.wait_for(lambda: "sl_job_samples_per_second" in cluster.master.metrics.text(), 15)
