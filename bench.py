@@ -6,9 +6,11 @@ MLP on synthetic MNIST, 1/2/4/8 workers").  One process per GPU (torchrun sets
 RANK/LOCAL_RANK/WORLD_SIZE); each rank is one worker that
 
   1. receives its data shard (default: over the real gRPC data plane -- an
-     in-process file server streams it as 1 MB ``Chunk``s to the worker's
-     ``ReceiveFile`` handler, which lands it in a pinned host buffer and
-     hipMemcpyAsync's it into HBM; ``--ingest local`` skips gRPC),
+     in-process file server streams it as 1 MB ``Chunk``s to a ``ReceiveFile``
+     handler, which parses each chunk in place into a pinned (hipHostMalloc) ring
+     slot and hipMemcpyAsync's it into HBM, the worker's own ingest path; the
+     JSON reports that stream's GB/s as ``ingest_gbps``, shard synthesis timed
+     apart; ``--ingest local`` skips gRPC),
   2. trains the model with the hand-written HIP kernels (bf16 MFMA, fp32
      master weights, momentum SGD) -- every timed step is a full forward +
      backward + (RCCL all-reduce) + optimizer step,
@@ -178,19 +180,27 @@ def main(argv=None) -> int:
     n_records = B * args.shard_batches
 
     # ---- 1. shard delivery -------------------------------------------------
+    ingest_stats: dict = {}
     t_ingest = time.perf_counter()
     if args.ingest == "device":
         from serverless_learn_amd.data.device_synth import synth_on_device
 
         x, y = synth_on_device("mnist" if mlp else "cifar", n_records, seed=rank, device=dev)
-    else:
-        if args.ingest == "grpc":
-            from serverless_learn_amd.runtime.local_cluster import fetch_shard_via_grpc
+    elif args.ingest == "grpc":
+        # the north-star data plane: the file server streams the shard as 1 MB Chunks, the
+        # receiving handler parses each in place into a pinned ring slot and hipMemcpyAsync's
+        # it into HBM (csrc/core/ingest.cpp); x / y are views of that device buffer
+        from serverless_learn_amd.data.synthetic import HEADER_SIZE, decode_header
+        from serverless_learn_amd.runtime.local_cluster import fetch_shard_via_grpc
 
-            host_buf = fetch_shard_via_grpc(n_records=n_records, shard_index=rank, num_shards=world, seed=0,
-                                            dataset=dataset)
-        else:
-            host_buf = make_shard(n_records, shard_index=rank, num_shards=world, seed=0, dataset=dataset)
+        buf = fetch_shard_via_grpc(n_records=n_records, shard_index=rank, num_shards=world, seed=0,
+                                   dataset=dataset, device=local_dev, stats=ingest_stats)
+        hdr = decode_header(buf[:HEADER_SIZE].cpu().numpy().tobytes())
+        n, d = hdr["n"], hdr["height"] * hdr["width"] * hdr["channels"]
+        x = buf[HEADER_SIZE:HEADER_SIZE + n * d].view(n, d)
+        y = buf[HEADER_SIZE + n * d:HEADER_SIZE + n * d + n]
+    else:
+        host_buf = make_shard(n_records, shard_index=rank, num_shards=world, seed=0, dataset=dataset)
         hdr, images, labels = decode_shard(bytearray(host_buf))
         x = torch.from_numpy(images).pin_memory().to(dev, non_blocking=True)
         y = torch.from_numpy(labels.copy()).pin_memory().to(dev, non_blocking=True)
@@ -378,6 +388,8 @@ def main(argv=None) -> int:
         "train_loss_last": round(st.loss, 4),
         "train_acc_last": round(st.accuracy, 4),
         "ingest_s": round(t_ingest, 3),
+        "ingest": ingest_stats or None,
+        "ingest_gbps": ingest_stats.get("gbps"),
         "replicas_identical": replicas_identical,
         "dist": {
             "world_size": dist.get_world_size() if world > 1 else 1,

@@ -7,6 +7,7 @@
 
 #include "ingest.h"
 #include "membership.h"
+#include "synth.h"
 #include "wire.h"
 
 namespace py = pybind11;
@@ -113,6 +114,20 @@ PYBIND11_MODULE(_slcore, m) {
   m.def("encode_chunk", &encode_chunk_py);
   m.def("chunk_payload", &chunk_payload_py, "(offset, length) of Chunk.data inside the message");
   m.def("reference_dummy_file", &reference_dummy, "the reference file server's file 0 bytes");
+  m.def(
+      "synth_images",
+      [](py::buffer images, py::buffer labels, long n, int pixels, py::array_t<float, py::array::c_style> protos,
+         int classes, float noise, float scale, float offset, unsigned long long seed, long first, int threads) {
+        py::buffer_info im = contiguous(images), lb = contiguous(labels);
+        if ((long)(im.size * im.itemsize) < n * pixels || (long)(lb.size * lb.itemsize) < n)
+          throw std::invalid_argument("output buffers too small");
+        if (protos.size() < (ssize_t)classes * pixels) throw std::invalid_argument("prototypes too small");
+        const float* pr = protos.data();
+        py::gil_scoped_release r;
+        synth_images((uint8_t*)im.ptr, (uint8_t*)lb.ptr, n, pixels, pr, classes, noise, scale, offset, seed, first,
+                     threads);
+      },
+      "Philox synthetic records (the K8 device generator's math) into writable buffers, multithreaded");
 
   py::register_exception<WireError>(m, "WireError", PyExc_ValueError);
 

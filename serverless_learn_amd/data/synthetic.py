@@ -136,8 +136,40 @@ def decode_shard(buf) -> tuple[dict, np.ndarray, np.ndarray]:
     return hdr, images, labels
 
 
-def make_shard(n: int, shard_index: int = 0, num_shards: int = 1, seed: int = 0, dataset: str = "synthetic-mnist") -> bytes:
-    """Shard ``shard_index`` of a seeded synthetic dataset (``synthetic-mnist`` or ``synthetic-cifar``)."""
+def make_shard_philox(n: int, shard_index: int = 0, num_shards: int = 1, seed: int = 0,
+                      dataset: str = "synthetic-mnist", threads: int | None = None) -> bytes:
+    """Shard ``shard_index`` = records [shard_index * n, (shard_index + 1) * n) of the Philox
+    dataset keyed by ``seed``: the same records the on-device generator K8 produces
+    (data/device_synth.py), synthesised by the native core on ``threads`` CPU threads straight
+    into the encoded shard buffer (no intermediate arrays)."""
+    import os
+
+    from .._core import core
+    from .device_synth import KINDS, prototypes
+
+    kind = "cifar" if dataset == "synthetic-cifar" else "mnist"
+    h, w, c, noise, scale, offset = KINDS[kind]
+    pixels = h * w * c
+    buf = bytearray(HEADER_SIZE + n * pixels + n)
+    buf[:HEADER_SIZE] = HEADER.pack(MAGIC, 1, 1 if c == 1 else 2, n, h, w, 10, shard_index, num_shards,
+                                    c if c > 1 else 0, seed, 0)
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    images = arr[HEADER_SIZE:HEADER_SIZE + n * pixels]
+    labels = arr[HEADER_SIZE + n * pixels:]
+    threads = threads or max(1, min(16, (os.cpu_count() or 4)))
+    core().synth_images(images, labels, n, pixels, prototypes(kind), 10, noise, scale, offset,
+                        seed & ((1 << 64) - 1), shard_index * n, threads)
+    return bytes(buf)
+
+
+def make_shard(n: int, shard_index: int = 0, num_shards: int = 1, seed: int = 0, dataset: str = "synthetic-mnist",
+               generator: str = "philox") -> bytes:
+    """Shard ``shard_index`` of a seeded synthetic dataset (``synthetic-mnist`` or ``synthetic-cifar``).
+
+    ``generator="philox"`` (default): the native multithreaded Philox generator (the K8
+    records); ``"numpy"``: the original numpy generator (kept for comparisons and tests)."""
+    if generator == "philox":
+        return make_shard_philox(n, shard_index, num_shards, seed, dataset)
     if dataset == "synthetic-cifar":
         images, labels = make_cifar_like(n, seed=seed * 1000003 + shard_index)
         return encode_shard(images.reshape(n, -1), labels, shard_index, num_shards, seed, h=32, w=32, channels=3)

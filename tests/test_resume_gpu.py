@@ -77,11 +77,17 @@ def test_resnet_resume_restores_running_stats_and_cursor():
     # the stats are real (moved away from the (0, 1) init) and keep evolving identically
     rm0, rv0 = a.running_stats()["stem_bn"] if "stem_bn" in a.running_stats() else next(iter(a.running_stats().values()))
     assert float(rm0.abs().sum()) > 0 and float((rv0 - 1).abs().sum()) > 0
+    w0 = a.get_flat()
     a.step()
     b.step()
     torch.cuda.synchronize()
-    # the engine's BN sums use cross-workgroup atomics (not bit-reproducible): close, not equal
-    torch.testing.assert_close(b.get_flat(), a.get_flat(), rtol=1e-3, atol=1e-4)
+    # the engine's BN / weight-gradient sums use cross-workgroup atomics, so two runs of the
+    # same step are not bit-equal (test_cnn_gpu.py: cosine ~0.99 run to run): the resumed
+    # step must move the weights the same way
+    da, db = (a.get_flat() - w0).double(), (b.get_flat() - w0).double()
+    cos = float(torch.dot(da, db) / (da.norm() * db.norm()))
+    assert cos > 0.95, cos
+    assert int(a.cursor.item()) == int(b.cursor.item()) == 4
 
 
 def test_resnet_eval_uses_running_statistics():
