@@ -79,7 +79,8 @@ using namespace sl;
 #define SL_ROWS_KO 0  // timing knockouts of mlp_rows_kernel (1: every wave streams wave 0's weight columns, 2: no X loads)
 #endif
 #ifndef SL_MLP_XQ
-#define SL_MLP_XQ 4  // X prefetch distance in 64-column chunks (4 measured +1% over 2)
+#define SL_MLP_XQ 13  // X prefetch distance in 64-column chunks: 13 = every chunk's load issued up front
+                      // (+1.5 % MLP over 4, profiles/r03_xq; 4 measured +1 % over 2 in round 1)
 #endif
 namespace {
 constexpr int D_IN = 784;   // input features (28x28)

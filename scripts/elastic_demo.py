@@ -196,6 +196,17 @@ def main(argv=None) -> int:
                 p.wait(10)
             except subprocess.TimeoutExpired:
                 p.kill()
+        if not summary.get("ok"):
+            tails = {}
+            for n, path in logs.items():
+                try:
+                    with open(path + ".err") as f:
+                        tails[n] = f.read()[-1500:]
+                except OSError:
+                    pass
+            summary["stderr_tails"] = tails
+            summary["last_events"] = {n: [(e.get("event"), e.get("step"), e.get("epoch")) for e in read_events(path)[-8:]]
+                                      for n, path in logs.items()}
         print(json.dumps(summary, default=str))
 
 

@@ -16,9 +16,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_gpu_workers_kill_one_respawn_with_xgmi(tmp_path):
     dp_timeout = 20.0
+    logdir = os.path.join(ROOT, "gpurun_out", "elastic_gpu")  # merged back from the GPU box for post-mortems
     cmd = ["timeout", "-k", "10", "220", sys.executable, os.path.join(ROOT, "scripts", "elastic_demo.py"),
            "--device", "cuda:0", "--dp-backend", "gloo", "--xgmi-gloo", "--workers", "3", "--batch", "1024",
-           "--timeout", "200", "--dp-timeout-s", str(dp_timeout), "--logdir", str(tmp_path)]
+           "--timeout", "200", "--dp-timeout-s", str(dp_timeout), "--logdir", logdir]
     proc = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
     lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
     assert lines, proc.stderr[-3000:]
