@@ -298,7 +298,12 @@ class FusedMLPTrainer:
         self.w3p = torch.empty(batch // 64, W3P_LD, dtype=torch.float32, device=dev)
         self.loss = torch.zeros(batch, dtype=torch.float32, device=dev)
         self.correct = torch.zeros(batch, dtype=torch.float32, device=dev)
-        self.slab = torch.empty(self.slices, self.n_pad, dtype=torch.float32, device=dev)
+        # per-slice stride of the weight-gradient slab (the kernel library's layout: tiled in the
+        # wgrad kernel's register order, larger than the parameter count)
+        lib = _native.lib()
+        # (older kernel builds, kept for A/B runs, have no tiled layout and no stride query)
+        self.slab_stride = int(lib.sl_mlp_slab_stride()) if hasattr(lib, "sl_mlp_slab_stride") else self.n_pad
+        self.slab = torch.empty(self.slices, self.slab_stride, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         # layer 1 of the train step as a separate 128-row-tile GEMM (mlp_l1_kernel) when SL_MLP_L1=1.
@@ -366,7 +371,7 @@ class FusedMLPTrainer:
                              p(self.loss), p(self.correct), None, 2 if self.l1_gemm else 1),
             "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
-                              self.slices, self.n_pad),
+                              self.slices, self.slab_stride),
         }
         if self.l1_gemm:
             lc["l1"] = n.Launch("sl_mlp_l1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1h),
@@ -375,13 +380,13 @@ class FusedMLPTrainer:
                                                         "reduce": (1, False, True, False),
                                                         "update": (2, True, False, True)}.items():
             lc[name] = n.Launch("sl_mlp_sgd", p(self.params), p(self.mom),
-                                None if from_grad else p(self.slab), self.slices, self.n_pad,
+                                None if from_grad else p(self.slab), self.slices, self.slab_stride,
                                 p(self.grad) if from_grad else None, p(self.grad) if grad_out else None,
                                 self.lr, self.momentum, self.weight_decay, *self.dw1_coeffs, mode, *ws,
                                 p(self.cursor) if bump else None)
         if self.xgmi is not None:
             xg = self.xgmi
-            lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.n_pad, *self.dw1_coeffs,
+            lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.slab_stride, *self.dw1_coeffs,
                                      xg.slot_ptr(0), xg.slot_ptr(1), xg.ctl.data_ptr())
             lc["xbarrier"] = [n.Launch(fn, *xg.args(), *extra) for fn, extra in xg.exchange_launches(self.n_pad)]
             lc["xupdate"] = n.Launch("sl_mlp_sgd_xgmi", p(self.params), p(self.mom), self.lr, self.momentum,

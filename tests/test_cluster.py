@@ -203,3 +203,36 @@ def test_group_metrics_are_allreduced_and_master_reports_job_rate(cluster):
     assert job["groups"] == 1
     assert job["samples_per_sec"] == pytest.approx(f[a.addr]["group_samples_per_sec"], rel=1e-3)
     assert cluster.wait_for(lambda: "sl_job_samples_per_second" in cluster.master.metrics.text(), 15)
+
+
+def test_join_switches_epoch_at_an_agreed_step_without_failed_collectives(cluster):
+    """A worker joining a training all-reduce group: the members see the new epoch from their
+    CheckUps at different times, but switch together at a step boundary the whole group agreed
+    on (Worker._agree), so no member runs a collective on the old group alone -- no
+    collective_failed -- and all three then train in lock-step with identical weights."""
+    a = cluster.add_worker(sync="allreduce", batch=256)
+    b = cluster.add_worker(sync="allreduce", batch=256)
+    assert cluster.wait_for(lambda: a.group.world == 2 and b.group.world == 2 and a.step > 30, 60)
+    fails = []
+    for w in (a, b):
+        orig = w.log.warn
+
+        def spy(event, _orig=orig, **f):
+            if event == "collective_failed":
+                fails.append(f)
+            return _orig(event, **f)
+        w.log.warn = spy
+    c = cluster.add_worker(sync="allreduce", batch=256)
+    ws = (a, b, c)
+    assert cluster.wait_for(lambda: all(w.group.world == 3 for w in ws) and min(w.step for w in ws) > 0
+                            and len({w.group.epoch for w in ws}) == 1, 60), \
+        [(w.group.world, w.group.epoch, w.step, w.state) for w in ws]
+    s0 = max(w.step for w in ws)
+    assert cluster.wait_for(lambda: min(w.step for w in ws) > s0 + 20, 60)
+    assert not fails, fails
+    # lock-step replicas: stop the group at a boundary and compare
+    for w in ws:
+        w.cfg.max_steps = max(x.step for x in ws) + 40
+    assert cluster.wait_for(lambda: all(w.state == "done" for w in ws), 60), [(w.step, w.state) for w in ws]
+    assert a.step == b.step == c.step
+    assert torch.equal(a.trainer.params, b.trainer.params) and torch.equal(a.trainer.params, c.trainer.params)
