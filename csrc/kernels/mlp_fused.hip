@@ -895,6 +895,19 @@ __global__ __launch_bounds__(L1_NT, 2) void mlp_l1_kernel(L1Args a) {
 // band of those columns over its slice's stages into the slice's slab, so the
 // slab carries every gradient and mlp_sgd_kernel needs no special case.
 // ---------------------------------------------------------------------------
+#ifndef SL_WG_TILED
+#define SL_WG_TILED 1  // slab in the weight-gradient kernel's register order (contiguous 1 KB per store)
+#endif
+// Tiled slab layout (SL_WG_TILED): per slice, the 9 weight-gradient tiles in the order the
+// accumulators sit in the waves' registers -- tile t, wave w, store instruction (i, j), lane l,
+// 4 floats -- so every epilogue store is 1 KB of contiguous memory, then the rows kernel's
+// partial-row sums in their own layout [dW3 | db3 | pad | db1 | db2].  The row-major form wrote
+// 16 rows x 64 B per store instruction; that tail took ~16 us (knockout, profiles/r03_wgrad).
+constexpr long TL_TILE = 256L * 128;            // floats per 256 x 128 tile
+constexpr long TL_W2 = 7L * TL_TILE;            // dW2 tiles (dW1: tiles 0..6, tile 6 = 16 real columns)
+constexpr long TL_SMALL = 9L * TL_TILE;         // [dW3 | db3 | pad | db1 | db2]
+constexpr long TL_STRIDE = (TL_SMALL + W3P_LD + 63) / 64 * 64;
+
 struct WgProblem {
   const void* a;  // [batch][256] bf16: dH1 / dH2
   const void* b;  // [batch][ldb]: u8 X (problem 0) / bf16 H1
@@ -1092,45 +1105,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     for (int st = 0; st < wg_ns<true>() - 1 && st < nst; ++st) issue(st, T_{});
   } else {
     for (int st = 0; st < wg_ns<false>() - 1 && st < nst; ++st) issue(st, F_{});
-  }
-
-  // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
-  // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
-  // a fixed-order sum through LDS (deterministic).  Scratch in the last ring slot, whose
-  // first LDS-DMA (stage NS-1) is issued after the main loop's first barrier. ----
-  {
-    constexpr int NC4 = W3P_LD / 4;
-    const int per = (NC4 + A.total_tiles - 1) / A.total_tiles;
-    const int c0 = t * per, nc = min(NC4, c0 + per) - c0;
-    float4* red = reinterpret_cast<float4*>(smem + (u8b ? (WG_NSLOT8 - 1) * WG_SLOT8 : (WG_NSLOT - 1) * WG_SLOT));
-    const int G = WG_NT / nc, col = tid % nc, g = tid / nc;
-    if (g < G) {
-      const float4* src = reinterpret_cast<const float4*>(A.w3p + (long)st0 * W3P_LD) + c0 + col;
-      float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 4
-      for (int k = g; k < nst; k += G) {
-        const float4 v = src[(long)k * NC4];
-        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
-      }
-      red[g * nc + col] = sum;
-    }
-    __syncthreads();
-    if (g == 0) {
-      float4 tot = red[col];
-      for (int i = 1; i < G; ++i) {
-        const float4 v = red[i * nc + col];
-        tot.x += v.x; tot.y += v.y; tot.z += v.z; tot.w += v.w;
-      }
-      const float tv[4] = {tot.x, tot.y, tot.z, tot.w};
-      float* out = A.slab + (long)s * A.slab_stride;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = 4 * (c0 + col) + j;
-        if (q < W3P_N) out[P_W3 + q] = tv[j];
-        else if (q >= W3P_DB1 && q < W3P_DB2) out[P_B1 + q - W3P_DB1] = tv[j];
-        else if (q >= W3P_DB2) out[P_B2 + q - W3P_DB2] = tv[j];
-      }
-    }
   }
 
   floatx4_t acc[WG_MI][WG_NJ];
@@ -1413,18 +1387,93 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
+  // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
+  // a fixed-order sum through LDS (deterministic).  Done HERE, around the slab stores: the
+  // loads are issued first (every row of the band at once, clamped indices so no branch
+  // splits them), the accumulator stores go out while they are in flight, and the sum
+  // waits only for the loads.  As a prologue this cost 6 us of load latency before the
+  // main loop; the store tail is issue-bound (~16 us, profiles/r03_wgrad) and hides it. ----
+  constexpr int NC4 = W3P_LD / 4;
+  constexpr int PR_MAX = 12;  // partial rows per thread held in registers (else a plain loop)
+  const int per = (NC4 + A.total_tiles - 1) / A.total_tiles;
+  const int c0 = t * per, nc = min(NC4, c0 + per) - c0;
+  const int G = WG_NT / nc, col = tid % nc, g = tid / nc;
+  const float4* psrc = reinterpret_cast<const float4*>(A.w3p + (long)st0 * W3P_LD) + c0 + col;
+  const bool pr_regs = (nst + G - 1) / G <= PR_MAX;
+  float4 pv[PR_MAX];
+  if (g < G && pr_regs) {
+#pragma unroll
+    for (int i = 0; i < PR_MAX; ++i) pv[i] = psrc[(long)min(g + i * G, nst - 1) * NC4];
+  }
+
   // ---- epilogue: the MFMAs took their operands swapped (B first), so each lane holds
   // 4 consecutive n of one m row: float4 stores straight from registers into slab slice
   // s (no LDS staging, no barriers) ----
+#if SL_WG_TILED
+  static_assert(SL_WG_W128 && WG_MI == 8 && WG_NJ == 2, "tiled slab assumes 2 x 4 waves of 128 x 32");
+  float* out = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096 + lane * 4;
+#else
   float* out = A.slab + (long)s * A.slab_stride + P.w_off;
+#endif
 #pragma unroll
   for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
     for (int j = 0; j < WG_NJ; ++j) {
       const int n = n0 + wn * 16 * WG_NJ + j * 16 + 4 * lg;
+#if SL_WG_KO == 7  // 7: epilogue stores knocked out; asm keeps every accumulator (and its MFMAs) live
+      asm volatile("" ::"v"(acc[i][j]));
+#else
+#if SL_WG_TILED
+      if (n < P.n_real) *reinterpret_cast<floatx4_t*>(out + (i * WG_NJ + j) * 256) = acc[i][j];
+#else
       if (n < P.n_real)
         *reinterpret_cast<floatx4_t*>(out + (long)(wm * 16 * WG_MI + i * 16 + lr) * P.n_real + n) = acc[i][j];
+#endif
+#endif
     }
+
+#if SL_WG_KO != 6  // 6: no partial-row sums
+  float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g < G) {
+    if (pr_regs) {
+#pragma unroll
+      for (int i = 0; i < PR_MAX; ++i) {
+        const float w = g + i * G < nst ? 1.f : 0.f;  // select after the load, not around it
+        sum.x += w * pv[i].x; sum.y += w * pv[i].y; sum.z += w * pv[i].z; sum.w += w * pv[i].w;
+      }
+    } else {
+      for (int k = g; k < nst; k += G) {
+        const float4 v = psrc[(long)k * NC4];
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+      }
+    }
+  }
+  float4* red = reinterpret_cast<float4*>(smem);
+  __syncthreads();  // every wave is done with the ring
+  if (g < G) red[g * nc + col] = sum;
+  __syncthreads();
+  if (g == 0) {
+    float4 tot = red[col];
+    for (int i = 1; i < G; ++i) {
+      const float4 v = red[i * nc + col];
+      tot.x += v.x; tot.y += v.y; tot.z += v.z; tot.w += v.w;
+    }
+    const float tv[4] = {tot.x, tot.y, tot.z, tot.w};
+    float* srow = A.slab + (long)s * A.slab_stride;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = 4 * (c0 + col) + j;
+#if SL_WG_TILED
+      if (q < W3P_N || q >= W3P_DB1) srow[TL_SMALL + q] = tv[j];
+#else
+      if (q < W3P_N) srow[P_W3 + q] = tv[j];
+      else if (q >= W3P_DB1 && q < W3P_DB2) srow[P_B1 + q - W3P_DB1] = tv[j];
+      else if (q >= W3P_DB2) srow[P_B2 + q - W3P_DB2] = tv[j];
+#endif
+    }
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1514,11 +1563,92 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
+#if SL_WG_TILED
+// Slab reduction + update over a tiled slab (SL_WG_TILED): the threads walk the slab in its
+// own order (float4 unit u of every slice: coalesced 1 KB per wave and slice), each unit's 4
+// floats map back to 4 consecutive parameters of one weight row (or, in the small region, to
+// single parameters).  w / mom / the shadows are then touched in a scattered order, but they
+// are 1 MB arrays that stay in L2.
+__device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
+  const long off = u * 4;
+  if (off >= TL_SMALL + W3P_LD) return;
+  long pe = -1;       // this thread's parameter (part < 4)
+  int w1row = -1;     // dW1 row (output feature) of the unit, for the db1 term
+  if (off < TL_SMALL) {
+    const int tile = (int)(off / TL_TILE), within = (int)(off % TL_TILE);
+    const int wave = within >> 12, rem = within & 4095;
+    const int ins = rem >> 8, lane = (rem & 255) >> 2;
+    const int m = (wave & 1) * 128 + (ins >> 1) * 16 + (lane & 15);
+    const int nn = (wave >> 1) * 32 + (ins & 1) * 16 + (lane >> 4) * 4;
+    if (tile < 7) {
+      const int n = tile * 128 + nn;
+      if (n >= D_IN) return;  // dW1's last tile: 16 real columns (whole group exits together)
+      pe = P_W1 + (long)m * D_IN + n + part;
+      w1row = m;
+    } else {
+      pe = P_W2 + (long)m * HID + (tile - 7) * 128 + nn + part;
+    }
+  } else {
+    const int q = (int)(off - TL_SMALL) + part;
+    if (q < W3P_N) pe = P_W3 + q;
+    else if (q >= W3P_DB1 && q < W3P_DB2) pe = P_B1 + q - W3P_DB1;
+    else if (q >= W3P_DB2 && q < W3P_LD) pe = P_B2 + q - W3P_DB2;
+  }
+  const bool mine = part < 4 && pe >= 0;
+  const bool upd = mine && a.mode != 1;
+  const float w0 = upd ? a.w[pe] : 0.f;
+  const float m0 = upd && a.mom ? a.mom[pe] : 0.f;
+  float g[4] = {0.f, 0.f, 0.f, 0.f};
+  float db = 0.f;
+  const float* src = a.slab + off;
+  const float* dbs = a.slab + TL_SMALL + W3P_DB1 + (w1row >= 0 ? w1row : 0);
+  constexpr int U = 8;
+  for (int s0 = part; s0 < a.slices; s0 += SGD_TPG * U) {
+    float4 v[U];
+    float d[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int sidx = s0 + k * SGD_TPG;
+      v[k] = sidx < a.slices ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      d[k] = (w1row >= 0 && sidx < a.slices) ? dbs[(long)sidx * a.slab_stride] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      g[0] += v[k].x; g[1] += v[k].y; g[2] += v[k].z; g[3] += v[k].w;
+      db += d[k];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) g[j] = group_sum(g[j]);
+  float gme = g[part & 3];
+  if (w1row >= 0) {
+    db = group_sum(db);
+    gme = a.xa * gme + a.xb * db;
+  }
+  if (!mine) return;
+  float* gout = a.grad_out;
+  if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
+  sgd_apply(a, gout, pe, gme, w0, m0);
+}
+#endif
+
+// float4 units a launch of mlp_sgd_kernel walks: the slab's (tiled) or the parameters'
+__host__ __device__ constexpr long sgd_units(bool slab) {
+  return (SL_WG_TILED && slab) ? TL_STRIDE / 4 : (P_N + 3) / 4;
+}
+
 __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
   if (SL_SGD_KO == 3) return;  // timing knockout 3: launch + kernel-boundary floor
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int part = (int)(t % SGD_TPG);
+#if SL_WG_TILED
+  if (a.slab && a.mode != 0) {
+    sgd_tiled(a, t / SGD_TPG, part);
+    return;
+  }
+#endif
   const long p0 = (t / SGD_TPG) * 4;
   if (p0 >= a.n) return;  // whole groups exit together (n groups are group-aligned in t)
   const long p = p0 + part;
@@ -1632,6 +1762,9 @@ extern "C" {
 
 long sl_mlp_param_count() { return P_N; }
 
+// floats per slice of the weight-gradient slab (the tiled layout is larger than the parameters)
+long sl_mlp_slab_stride() { return SL_WG_TILED ? TL_STRIDE : (P_N + 3) / 4 * 4; }
+
 static unsigned long long* g_stamps = nullptr;
 int sl_mlp_set_stamps(unsigned long long* p) {
   g_stamps = p;
@@ -1713,6 +1846,7 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
                  const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
                  long slab_stride, hipStream_t stream) {
   if (!w3p || n_w3p != batch / 64) return -1;
+  if (SL_WG_TILED && slab_stride < TL_STRIDE) return -1;
   const int s_eff = sl_mlp_wgrad_slices(batch, slices);
   if (s_eff <= 0 || s_eff != slices) return -1;
   WgArgs a;
@@ -1750,7 +1884,8 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   if (mode != 0 && !slab && !grad_in) return -1;
   if (mode == 1 && !grad_out) return -1;
   if (slab && (slab_stride & 3)) return -1;
-  const long groups = (P_N + 3) / 4;
+  if (SL_WG_TILED && slab && slab_stride < TL_STRIDE) return -1;
+  const long groups = sgd_units(slab != nullptr && mode != 0);
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
@@ -1763,7 +1898,8 @@ int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa
   SgdArgs a = {};
   a.slab = slab; a.slices = slices; a.slab_stride = slab_stride; a.grad_out = slot0; a.grad_out_alt = slot1;
   a.ar_ctl = ctl; a.n = P_N; a.xa = xa; a.xb = xb; a.mode = 1;
-  const long groups = (P_N + 3) / 4;
+  if (SL_WG_TILED && slab_stride < TL_STRIDE) return -1;
+  const long groups = sgd_units(true);
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;

@@ -30,6 +30,7 @@ F = ctypes.c_float
 # name -> argtypes (restype is always c_int unless listed in _RESTYPE)
 _SIGS: dict[str, list] = {
     "sl_mlp_param_count": [],
+    "sl_mlp_slab_stride": [],
     "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P],
     "sl_mlp_wgrad": [I, P, P, I, P, P, P, P, I, P, I, L, P],
     "sl_mlp_wgrad_slices": [I, I],
@@ -43,7 +44,7 @@ _SIGS: dict[str, list] = {
     "sl_mlp_reduce_xgmi": [P, I, L, F, F, P, P, P, P],
     "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, L, P],
 }
-_RESTYPE = {"sl_mlp_param_count": ctypes.c_long}
+_RESTYPE = {"sl_mlp_param_count": ctypes.c_long, "sl_mlp_slab_stride": ctypes.c_long}
 
 
 def register(name: str, argtypes: list, restype=ctypes.c_int) -> None:
