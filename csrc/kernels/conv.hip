@@ -771,6 +771,29 @@ __device__ __forceinline__ void wgrad_out(const WgradArgs& a, int s, int co, int
   else a.dw[(long)co * a.g.K + k] += v;
 }
 
+// Epilogue of the weight-gradient kernels: the fp32 tile (BMO x 128, staged in LDS with row
+// stride LD) goes out to the slab as 16-B stores -- four times fewer store instructions than one
+// float per lane, and the end-of-kernel store tail is issue-bound (profiles/r03_wgrad for the
+// MLP's analogue).  Atomic mode (no slab) keeps the per-element path.
+template <int BMO, int LD, int NTH>
+__device__ __forceinline__ void wgrad_store_tile(const WgradArgs& a, int s, int co0, int k0, const float* Os, int tid) {
+  if (a.ws && (a.g.K & 3) == 0) {
+    for (int q = tid; q < BMO * 32; q += NTH) {
+      const int rl = q >> 5, cl = (q & 31) * 4;
+      const int co = co0 + rl, k = k0 + cl;
+      if (co < a.cout && k < a.g.K)  // K % 4 == 0 and k % 4 == 0: the whole float4 is in range
+        *reinterpret_cast<float4*>(a.ws + ((long)s * a.cout + co) * a.g.K + k) =
+            *reinterpret_cast<const float4*>(Os + rl * LD + cl);
+    }
+    return;
+  }
+  for (int q = tid; q < BMO * 128; q += NTH) {
+    const int rl = q >> 7, cl = q & 127;
+    const int co = co0 + rl, k = k0 + cl;
+    if (co < a.cout && k < a.g.K) wgrad_out(a, s, co, k, Os[rl * LD + cl]);
+  }
+}
+
 // dw[i] += sum_s ws[s][i] (a fixed summation tree: deterministic, unlike the atomics).  8 lanes
 // per float4 group each sum every 8th slice with all their loads in flight, then combine by
 // shuffles: one thread per group was latency-bound (1.9 TB/s on 57 slices).
@@ -979,11 +1002,8 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
     }
   }
   __syncthreads();
-  for (int q = tid; q < BMO * BNO; q += NTW) {
-    const int rl = q >> 7, cl = q & 127;
-    const int co = co0 + rl, k = k0 + cl;
-    if (co < a.cout && k < g.K) wgrad_out(a, s, co, k, Os[rl * OUT_LD + cl]);
-  }
+  static_assert(BNO == 128, "wgrad_store_tile writes 128-column tiles");
+  wgrad_store_tile<BMO, OUT_LD, NTW>(a, s, co0, k0, Os, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -1116,11 +1136,8 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
       for (int r = 0; r < 4; ++r)
         Os[(wm * 64 + i * 16 + 4 * (lane >> 4) + r) * OUT_LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
-  for (int q = tid; q < BMO * BNO; q += 512) {
-    const int rl = q >> 7, cl = q & 127;
-    const int co = co0 + rl, k = k0 + cl;
-    if (co < a.cout && k < g.K) wgrad_out(a, s, co, k, Os[rl * OUT_LD + cl]);
-  }
+  static_assert(BNO == 128, "wgrad_store_tile writes 128-column tiles");
+  wgrad_store_tile<BMO, OUT_LD, 512>(a, s, co0, k0, Os, tid);
 }
 
 // ---------------------------------------------------------------------------
