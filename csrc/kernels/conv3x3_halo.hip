@@ -430,6 +430,54 @@ __device__ __forceinline__ void wgrad_tile_mfmas(uint32_t xb, uint32_t yb, float
   kstep(std::integral_constant<int, 7>{});
 }
 
+// Slab layout of one workgroup's partial dW (register order): wave w's accumulators, tile
+// (i, t) of NTAP(w) per i, 64 lanes x float4; waves 0-3 hold taps 0-4 (20 tiles), 4-7 taps 5-8 (16).
+__host__ __device__ constexpr int halo_wgrad_wave_base(int w) { return w < 4 ? w * 20 * 256 : 80 * 256 + (w - 4) * 16 * 256; }
+
+// dw[co][tap][ci] += sum over slices of the register-order slab (a fixed order: deterministic).
+// SLAB_G lanes per float4 unit split the slices; the unit's 4 floats are 4 consecutive co.
+constexpr int HSLAB_G = 8;
+__global__ __launch_bounds__(256) void halo_wgrad_reduce_kernel(const float4* __restrict__ ws, int slices,
+                                                                float* __restrict__ dw) {
+  constexpr int UNITS = 64 * 9 * HC / 4;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int part = (int)(t % HSLAB_G);
+  const int u = (int)(t / HSLAB_G);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (u < UNITS) {
+    for (int s0 = part; s0 < slices; s0 += HSLAB_G * 8) {
+      float4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int sl = s0 + k * HSLAB_G;
+        v[k] = sl < slices ? ws[(long)sl * UNITS + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < HSLAB_G; m <<= 1) {
+    acc.x += __shfl_xor(acc.x, m);
+    acc.y += __shfl_xor(acc.y, m);
+    acc.z += __shfl_xor(acc.z, m);
+    acc.w += __shfl_xor(acc.w, m);
+  }
+  if (u >= UNITS || part != 0) return;
+  const int off = u * 4;
+  const int w = off < 80 * 256 ? off / (20 * 256) : 4 + (off - 80 * 256) / (16 * 256);
+  const int ntap = w < 4 ? 5 : 4, t0 = w < 4 ? 0 : 5;
+  const int rem = off - halo_wgrad_wave_base(w);
+  const int tile = rem >> 8, lane = (rem & 255) >> 2;
+  const int i = tile / ntap, tp = t0 + tile % ntap;
+  const int co = 16 * i + 4 * (lane >> 4), ci = 16 * (w & 3) + (lane & 15);
+  const float v4[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dw[((long)(co + r) * 9 + tp) * HC + ci] += v4[r];
+}
+
 __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[WX_BYTES + WY_BYTES];
   uint8_t* Xs = smem;
@@ -502,6 +550,15 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
     }
     // acc[i][t]: lane (lg, lr) holds dW[co = 16 i + 4 lg + r][tap T0 + t][ci = 16 cb + lr]
     const int lr = lane & 15;
+    if (a.ws) {
+      // slab in register order (halo_wgrad_slab_off): one contiguous 1 KB per store instruction
+      float* base = a.ws + (long)blockIdx.x * (64 * 9 * HC) + halo_wgrad_wave_base(wave) + lane * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t) *reinterpret_cast<floatx4_t*>(base + (i * NTAP + t) * 256) = acc[i][t];
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -548,7 +605,12 @@ int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, 
   a.ws = (ws && need <= ws_floats && !((uintptr_t)ws & 15) && !((uintptr_t)dw & 15)) ? ws : nullptr;
   hipLaunchKernelGGL(conv3x3_wgrad_c64_kernel, dim3(grid), dim3(WNT), 0, stream, a);
   SL_CHECK_LAUNCH();
-  if (a.ws) return sl_wgrad_slab_reduce(a.ws, grid, 64L * 9 * HC, dw, stream);
+  if (a.ws) {
+    constexpr long units = 64L * 9 * HC / 4;
+    hipLaunchKernelGGL(halo_wgrad_reduce_kernel, dim3((int)((units * HSLAB_G + 255) / 256)), dim3(256), 0, stream,
+                       reinterpret_cast<const float4*>(a.ws), grid, dw);
+    SL_CHECK_LAUNCH();
+  }
   return 0;
 }
 

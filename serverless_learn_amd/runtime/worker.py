@@ -94,6 +94,7 @@ class Worker:
         self.graph_chunks = 0     # graph replays run (tests / feedback)
         self._agreed_epoch = -1   # newest membership epoch the whole lock-step group has agreed to see
         self._broken_since = None  # when the live group was first seen broken (monotonic s)
+        self._agree_stream = None  # side stream of the epoch agreement on RCCL groups
         self.bytes_ingested = 0
         self.files_received: list[int] = []
         self.state = "idle"
@@ -377,13 +378,28 @@ class Worker:
         right after a step chunk is queued, so it overlaps the GPU work."""
         with self.view_lock:
             ep = float(self.view["epoch"])
-        dev = self.device if self.group.backend == "nccl" else torch.device("cpu")
-        t = torch.tensor([ep, -1.0 if (have_data is None or have_data) else 0.0], dtype=torch.float64, device=dev)
-        work = self.group.allreduce_async(t, torch.distributed.ReduceOp.MAX)
+        flags = [ep, -1.0 if (have_data is None or have_data) else 0.0]
+        if self.group.backend != "nccl":
+            t = torch.tensor(flags, dtype=torch.float64)
+            work = self.group.allreduce_async(t, torch.distributed.ReduceOp.MAX)
+        else:
+            # RCCL: on a side stream of its own, so the collective does not queue behind the
+            # step chunk just enqueued on the compute stream (it would then only complete when
+            # the GPU has drained, and the next chunk could not be queued behind the current one)
+            if self._agree_stream is None:
+                self._agree_stream = torch.cuda.Stream(device=self.device)
+            with torch.cuda.stream(self._agree_stream):
+                t = torch.tensor(flags, dtype=torch.float64, device=self.device)
+                work = self.group.allreduce_async(t, torch.distributed.ReduceOp.MAX)
 
         def result():
-            self.group.wait(work)
-            v = t.cpu()
+            if self.group.backend == "nccl":
+                with torch.cuda.stream(self._agree_stream):  # the side stream waits for RCCL, then we read
+                    self.group.wait(work)
+                    v = t.cpu()
+            else:
+                self.group.wait(work)
+                v = t
             return int(v[0]), bool(v[1] < -0.5)
         return result
 
