@@ -78,6 +78,9 @@ using namespace sl;
 #ifndef SL_ROWS_KO
 #define SL_ROWS_KO 0  // timing knockouts of mlp_rows_kernel (1: every wave streams wave 0's weight columns, 2: no X loads)
 #endif
+#ifndef SL_MLP_XW
+#define SL_MLP_XW 64  // rows kernel layer 1: X chunk width (128 = one barrier per 4 k-steps, ring over R0+R1)
+#endif
 #ifndef SL_MLP_XQ
 #define SL_MLP_XQ 13  // X prefetch distance in 64-column chunks: 13 = every chunk's load issued up front
                       // (+1.5 % MLP over 4, profiles/r03_xq; 4 measured +1 % over 2 in round 1)
@@ -442,7 +445,58 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
     stamp(1);
   } else {
   zero_acc();
-  {
+  constexpr bool XWIDE = SL_MLP_XW == 128 && SL_MLP_APF && !ONE;
+  if constexpr (XWIDE) {
+    // 128-column X chunks: 7 chunks, one barrier per four k-steps instead of per
+    // two. The 3-slot ring (144-element rows: ds_read_b128 conflict-free) spans
+    // R0 and the head of R1; H1 goes to R1 only after the barrier of the last
+    // k-step, when every slot has been read.
+    constexpr int XLD = 144, NCH = (L1_KSTEPS_ROWS + 3) / 4;
+    static_assert(3 * BM * XLD <= 2 * REGB, "wide X ring must fit regions 0 and 1");
+    const int xc2 = (tid & 3) * 32;
+    const uint8_t* xg2 = a.x + (srow0 + xrow) * D_IN + xc2;
+    uint4 xw[NCH][2];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        xw[c][h] = (c * 128 + xc2 + 16 * h < D_IN) ? *reinterpret_cast<const uint4*>(xg2 + c * 128 + 16 * h)
+                                                   : make_uint4(0, 0, 0, 0);
+    auto xstore2 = [&](int c) {
+      uint16_t* d = smem + (c % 3) * BM * XLD + xrow * XLD + xc2;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        short8_t lo = zero8(), hi = zero8();
+        if (c * 128 + xc2 + 16 * h < D_IN) {
+          lo = u8x8_to_bf16(make_uint2(xw[c][h].x, xw[c][h].y), nxa, nxb);
+          hi = u8x8_to_bf16(make_uint2(xw[c][h].z, xw[c][h].w), nxa, nxb);
+        }
+        *reinterpret_cast<short8_t*>(d + 16 * h) = lo;
+        *reinterpret_cast<short8_t*>(d + 16 * h + 8) = hi;
+      }
+    };
+    xstore2(0);
+    __syncthreads();
+    kloop_ring_a<L1_KSTEPS_ROWS, NF, MF, RING>(
+        [&](short8_t (&r)[NF], int st) {
+#pragma unroll
+          for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
+        },
+        [&](short8_t (&af)[MF], int st) {
+          const uint16_t* ab = smem + ((st >> 2) % 3) * BM * XLD + lr * XLD + (st & 3) * 32 + 8 * lg;
+#pragma unroll
+          for (int m = 0; m < MF; ++m) af[m] = lds8(ab + (rw + m * 16) * XLD);
+        },
+        mfma_ab,
+        [&](int st) {
+          // chunk c+1 converted after the first k-step of chunk c, published by this
+          // barrier before step 4c+3 prefetches it; its slot held chunk c-2
+          if (!(st & 3)) {
+            if ((st >> 2) + 1 < NCH) xstore2((st >> 2) + 1);
+            __syncthreads();
+          }
+        });
+  } else {
     // X chunks c+1 .. c+XQ wait in registers (slot chunk % XQ): the u8 input
     // comes from HBM, so its prefetch distance is set apart from the weight ring
     uint4 xq[SL_MLP_XQ];

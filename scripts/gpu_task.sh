@@ -4,6 +4,7 @@
 # the script stops at the first crash / timeout (gpu_step.sh exits 99 on anything but 0/1).
 #
 #   scripts/gpu_task.sh tests [pytest selectors...]          GPU test suite (default: tests -m gpu)
+#   scripts/gpu_task.sh vtests <variant> <selectors...>       tests against a variant build (SL_KERNELS_SO)
 #   scripts/gpu_task.sh bench <name> [bench.py args...]       one bench run -> gpurun_out/<name>.log
 #   scripts/gpu_task.sh prof <name> [bench.py args...]        rocprofv3 kernel stats -> gpurun_out/<name>/
 #   scripts/gpu_task.sh pmc <name> <counters> [bench args]    one PMC pass (counters comma-separated)
@@ -28,6 +29,10 @@ run_task() {
       local sel=("$@"); [ ${#sel[@]} -eq 0 ] && sel=(tests -m gpu)
       step 900 pytest_gpu.log $PYT "${sel[@]}"
       grep -q " passed" gpurun_out/pytest_gpu.log && ! grep -q " failed" gpurun_out/pytest_gpu.log || exit 1 ;;
+    vtests)
+      local v=$1; shift
+      SL_KERNELS_SO=$(so_of "$v") step 600 "pytest_$v.log" $PYT "$@"
+      grep -q " passed" "gpurun_out/pytest_$v.log" && ! grep -q " failed" "gpurun_out/pytest_$v.log" || exit 1 ;;
     bench)
       local name=$1; shift
       step 300 "$name.log" python bench.py "$@" ;;
