@@ -74,6 +74,10 @@ def parse(argv=None):
     ap.add_argument("--oversubscribe", action="store_true",
                     help="allow --gpus N on fewer than N visible devices (ranks share GPUs: rehearsal only, "
                          "needs --dist-backend gloo)")
+    ap.add_argument("--runtime", action="store_true",
+                    help="train through the runtime roles instead of the bare engine: an in-process file "
+                         "server, master and worker (gRPC control + data plane, the worker's hipGraph "
+                         "chunks, its logging and feedback); 1 GPU")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     mlp = a.model == "mlp"
@@ -140,8 +144,108 @@ def launch_ranks(args, argv) -> int:
     return p.returncode
 
 
+def record(args, *, world, elapsed, model_name, n_params, use_graph, collective, first_loss, st, t_ingest,
+           ingest_stats, replicas_identical, n_dev) -> dict:
+    """The one JSON line (driver contract: whole-job value, max-over-ranks time)."""
+    import torch.distributed as dist
+
+    mlp = args.model == "mlp"
+    B = args.batch
+    global_batch = B * world
+    value = global_batch * args.steps / elapsed
+    out = {
+        "metric": METRIC if mlp else METRIC_CNN,
+        "value": round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (REF_CEILING_PER_WORKER * world), 2),
+        "dtype": "bf16",
+        "data": f"synthetic (seeded {'MNIST' if mlp else 'CIFAR'}-shaped u8 shards, random-init weights)",
+        "config": {
+            "model": model_name,
+            "params": n_params,
+            "global_batch": global_batch,
+            "per_gpu_batch": B,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+            "optimizer": f"sgd(lr={args.lr}, momentum={args.momentum}) fp32 master",
+            "hipgraph": use_graph,
+            "steps_per_graph": (args.unroll if mlp else 1) if use_graph else 0,
+            "ingest": args.ingest,
+            "collective_backend": collective,
+        },
+        "baseline_note": "reference publishes no number; vs_baseline is vs its derived data-delivery "
+                         "ceiling of 25,478 samples/s/worker (BASELINE.md)",
+        "train_loss_first": None if first_loss is None else round(first_loss, 4),
+        "train_loss_last": round(st.loss, 4),
+        "train_acc_last": round(st.accuracy, 4),
+        "ingest_s": round(t_ingest, 3),
+        "ingest": ingest_stats or None,
+        "ingest_gbps": ingest_stats.get("gbps"),
+        "replicas_identical": replicas_identical,
+        "dist": {
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
+            "collective_backend": collective,
+            "devices_visible": n_dev,
+            "ranks_share_gpus": world > n_dev,
+            "launcher": "bench.py" if os.environ.get("SL_BENCH_LAUNCHED") else ("torchrun" if world > 1 else None),
+        },
+    }
+    return out
+
+
+def runtime_bench(args, dev) -> tuple[float, dict, object]:
+    """``--runtime``: the reference's three roles end-to-end on this GPU (file_server.cc,
+    master.cc, worker.cc).  The file server streams the shard to the worker over gRPC, the
+    master tracks it, and the worker trains from hipGraph chunks on its own thread with its
+    periodic logs / group metrics / feedback.  ``Worker.hold_at`` pauses it exactly at a step
+    once its device work has drained: hold at W, release to W + K, and the K steps between
+    are timed.  Returns (seconds, runtime info, the worker's trainer)."""
+    from serverless_learn_amd.proto import messages as pb
+    from serverless_learn_amd.runtime.local_cluster import LocalCluster, fast_config
+
+    cfg = fast_config(device=str(dev), model=args.model, batch=args.batch,
+                      shard_records=args.batch * args.shard_batches, log_every=64, graph_steps=16,
+                      lr=args.lr, momentum=args.momentum, rpc_timeout_s=30.0, checkup_interval_ms=500,
+                      dataset="synthetic-mnist" if args.model == "mlp" else "synthetic-cifar")
+    c = LocalCluster(cfg)
+    w = None
+    try:
+        w = c.add_worker(sync="none")
+        t_ingest = time.perf_counter()
+        w.hold_at = args.warmup
+        if not c.wait_for(lambda: w.held_step == args.warmup, 600, interval=0.001):
+            raise RuntimeError(f"runtime worker never reached warmup step {args.warmup} (state {w.state})")
+        t_ingest = time.perf_counter() - t_ingest
+        t0 = time.perf_counter()
+        w.hold_at = args.warmup + args.steps
+        if not c.wait_for(lambda: w.held_step == args.warmup + args.steps, 600, interval=0.0002):
+            raise RuntimeError(f"runtime worker stalled at step {w.step} (state {w.state})")
+        elapsed = time.perf_counter() - t0
+        fb = pb.FlowFeedback.FromString(w._check_up(pb.PeerList().SerializeToString(), None))
+        info = {"roles": ["file_server", "master", "worker"], "worker_graph_chunks": w.graph_chunks,
+                "worker_feedback_samples_per_sec": round(fb.samples_per_sec, 1),
+                "master_job": c.master.job_metrics(), "bytes_ingested": w.bytes_ingested,
+                "warmup_incl_shard_s": round(t_ingest, 3), "log_every": cfg.log_every,
+                "graph_steps": cfg.graph_steps}
+        return elapsed, info, w.trainer
+    finally:
+        if w is not None:
+            w.hold_at = None
+        c.stop()
+
+
 def main(argv=None) -> int:
     args = parse(argv)
+    if args.runtime and args.gpus != 1:
+        print("bench.py: --runtime runs the roles in one process on one GPU (--gpus 1)", file=sys.stderr)
+        return 2
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args, argv)
 
@@ -175,6 +279,21 @@ def main(argv=None) -> int:
             dist.init_process_group("gloo")
 
     mlp = args.model == "mlp"
+    if args.runtime:
+        elapsed, rt_info, tr = runtime_bench(args, dev)
+        out = record(args, world=1, elapsed=elapsed,
+                     model_name="mlp-784-256-256-10" if mlp else "resnet18-cifar (11.17M params)",
+                     n_params=tr.n_params if mlp else tr.spec.n_logical, use_graph=True, collective=None, first_loss=None, st=tr.stats(),
+                     t_ingest=rt_info["warmup_incl_shard_s"], ingest_stats={}, replicas_identical=None, n_dev=n_dev)
+        out["config"]["ingest"] = "grpc (file server role)"
+        out["config"]["mode"] = "runtime"
+        out["config"]["steps_per_graph"] = rt_info["graph_steps"]
+        out["runtime"] = rt_info
+        print(json.dumps(out), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(json.dumps(out) + "\n")
+        return 0
     dataset = "synthetic-mnist" if mlp else "synthetic-cifar"
     B = args.batch
     n_records = B * args.shard_batches
@@ -353,53 +472,9 @@ def main(argv=None) -> int:
             run(3)
             elapsed = timed()
             replicas_identical = replicas_agree()
-    st = tr.stats()
-    global_batch = B * world
-    value = global_batch * args.steps / elapsed
-    out = {
-        "metric": METRIC if mlp else METRIC_CNN,
-        "value": round(value, 1),
-        "unit": "samples/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": round(value / (REF_CEILING_PER_WORKER * world), 2),
-        "dtype": "bf16",
-        "data": f"synthetic (seeded {'MNIST' if mlp else 'CIFAR'}-shaped u8 shards, random-init weights)",
-        "config": {
-            "model": model_name,
-            "params": n_params,
-            "global_batch": global_batch,
-            "per_gpu_batch": B,
-            "seq_len": None,
-            "parallelism": f"dp{world}",
-            "optimizer": f"sgd(lr={args.lr}, momentum={args.momentum}) fp32 master",
-            "hipgraph": use_graph,
-            "steps_per_graph": (args.unroll if mlp else 1) if use_graph else 0,
-            "ingest": args.ingest,
-            "collective_backend": collective,
-        },
-        "baseline_note": "reference publishes no number; vs_baseline is vs its derived data-delivery "
-                         "ceiling of 25,478 samples/s/worker (BASELINE.md)",
-        "train_loss_first": round(first_loss, 4),
-        "train_loss_last": round(st.loss, 4),
-        "train_acc_last": round(st.accuracy, 4),
-        "ingest_s": round(t_ingest, 3),
-        "ingest": ingest_stats or None,
-        "ingest_gbps": ingest_stats.get("gbps"),
-        "replicas_identical": replicas_identical,
-        "dist": {
-            "world_size": dist.get_world_size() if world > 1 else 1,
-            "backend": dist.get_backend() if world > 1 else None,
-            "collective_backend": collective,
-            "devices_visible": n_dev,
-            "ranks_share_gpus": world > n_dev,
-            "launcher": "bench.py" if os.environ.get("SL_BENCH_LAUNCHED") else ("torchrun" if world > 1 else None),
-        },
-    }
+    out = record(args, world=world, elapsed=elapsed, model_name=model_name, n_params=n_params,
+                 use_graph=use_graph, collective=collective, first_loss=first_loss, st=tr.stats(),
+                 t_ingest=t_ingest, ingest_stats=ingest_stats, replicas_identical=replicas_identical, n_dev=n_dev)
     if xgmi_fallback:
         out["xgmi_fallback"] = xgmi_fallback
     if autotune:

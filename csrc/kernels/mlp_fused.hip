@@ -79,7 +79,7 @@ using namespace sl;
 #define SL_ROWS_KO 0  // timing knockouts of mlp_rows_kernel (1: every wave streams wave 0's weight columns, 2: no X loads)
 #endif
 #ifndef SL_MLP_XW
-#define SL_MLP_XW 64  // rows kernel layer 1: X chunk width (128 = one barrier per 4 k-steps, ring over R0+R1)
+#define SL_MLP_XW 128  // rows kernel layer 1: X chunk width (128: one barrier per 4 k-steps, ring over R0+R1; 64: per 2)
 #endif
 #ifndef SL_MLP_XQ
 #define SL_MLP_XQ 13  // X prefetch distance in 64-column chunks: 13 = every chunk's load issued up front

@@ -3,7 +3,7 @@
 # transient box problem (nothing ran on the GPU), never after a GPU-side failure.
 # usage: scripts/gpu.sh <timeout_s> <command...>
 t=$1; shift
-rm -f gpurun_out/*.log
+mkdir -p gpurun_out/prev; mv -f gpurun_out/*.log gpurun_out/prev/ 2>/dev/null
 for attempt in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun --timeout "$t" -- "$@"
   rc=$?

@@ -6,6 +6,7 @@
 #   scripts/gpu_task.sh tests [pytest selectors...]          GPU test suite (default: tests -m gpu)
 #   scripts/gpu_task.sh vtests <variant> <selectors...>       tests against a variant build (SL_KERNELS_SO)
 #   scripts/gpu_task.sh bench <name> [bench.py args...]       one bench run -> gpurun_out/<name>.log
+#   scripts/gpu_task.sh py <name> <script.py> [args...]       any probe script -> gpurun_out/<name>.log
 #   scripts/gpu_task.sh prof <name> [bench.py args...]        rocprofv3 kernel stats -> gpurun_out/<name>/
 #   scripts/gpu_task.sh pmc <name> <counters> [bench args]    one PMC pass (counters comma-separated)
 #   scripts/gpu_task.sh ab <reps> <v1,v2,..> [bench args]     interleaved A/B of variant builds
@@ -36,6 +37,9 @@ run_task() {
     bench)
       local name=$1; shift
       step 300 "$name.log" python bench.py "$@" ;;
+    py)
+      local name=$1; shift
+      step 300 "$name.log" python "$@" ;;
     prof)
       local name=$1; shift
       step 300 "$name.log" rocprofv3 --kernel-trace --stats -d "gpurun_out/$name" -o run -- python bench.py "$@"

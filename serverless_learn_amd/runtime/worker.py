@@ -92,6 +92,8 @@ class Worker:
         self.resumed_step = -1
         self._resume_pulled = 0   # PeerList.resume_file already pulled from the file server
         self.graph_chunks = 0     # graph replays run (tests / feedback)
+        self.hold_at = None       # pause training exactly at this step (bench.py --runtime, tests)
+        self.held_step = -1       # step the worker is paused at, once its device work has drained
         self._agreed_epoch = -1   # newest membership epoch the whole lock-step group has agreed to see
         self._broken_since = None  # when the live group was first seen broken (monotonic s)
         self._agree_stream = None  # side stream of the epoch agreement on RCCL groups
@@ -642,7 +644,18 @@ class Worker:
                 self.has_data.wait(0.2)
                 self.has_data.clear()
                 continue
+            hold = self.hold_at
+            if hold is not None and self.step >= hold:
+                if self.held_step != self.step:
+                    if self.device.type == "cuda":
+                        torch.cuda.synchronize(self.device)
+                    self.held_step = self.step  # every step up to here has finished on the device
+                    self.state = "held"
+                self._stop.wait(0.0002)
+                continue
             want = self.cfg.max_steps - self.step if self.cfg.max_steps else 1 << 30
+            if hold is not None:
+                want = min(want, hold - self.step)
             # chunks end on log / checkpoint boundaries, so every member of a lock-step group
             # runs its group collectives (metrics) at the same step
             for every in (self.cfg.log_every, self.cfg.checkpoint_every):

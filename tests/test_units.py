@@ -275,6 +275,20 @@ def test_mlp_dw1_fp16_coefficients_reproduce_normalised_gradient():
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-18)
 
 
+def test_runtime_bench_times_exactly_k_worker_steps():
+    """bench.py --runtime: the worker pauses exactly at W (hold_at), then at W + K once its
+    device work drained; the roles ran end-to-end (shard over gRPC, master registration)."""
+    import bench
+
+    args = bench.parse(["--runtime", "--batch", "64", "--steps", "24", "--warmup", "5"])
+    elapsed, info, tr = bench.runtime_bench(args, torch.device("cpu"))
+    assert elapsed > 0
+    assert info["roles"] == ["file_server", "master", "worker"]
+    assert info["bytes_ingested"] > 64 * 784
+    assert tr.cursor == 5 + 24  # CPU trainer: one batch per step, none skipped or repeated
+    assert bench.main(["--runtime", "--gpus", "2"]) == 2
+
+
 def test_bench_refuses_more_gpus_than_visible():
     """``bench.py --gpus 8`` on a machine with fewer devices exits non-zero and prints no
     JSON line: it never reports an N-GPU number measured on fewer GPUs (here: 0 visible)."""
