@@ -76,7 +76,8 @@ using namespace sl;
 #define SL_MLP_APF 1  // rows kernel: prefetch the next k-step's A fragments (3-slot X ring)
 #endif
 #ifndef SL_ROWS_KO
-#define SL_ROWS_KO 0  // timing knockouts of mlp_rows_kernel (1: every wave streams wave 0's weight columns, 2: no X loads)
+#define SL_ROWS_KO 0  // timing knockouts of mlp_rows_kernel (1: every wave streams wave 0's weight columns, 2: no X loads,
+                     // 3: 256-row tile, no W1 reloads in layer 1, 4: 256-row tile, no barriers in layer 1)
 #endif
 #ifndef SL_MLP_XW
 #define SL_MLP_XW 128  // rows kernel layer 1: X chunk width (128: one barrier per 4 k-steps, ring over R0+R1; 64: per 2)
@@ -84,6 +85,15 @@ using namespace sl;
 #ifndef SL_MLP_XQ
 #define SL_MLP_XQ 13  // X prefetch distance in 64-column chunks: 13 = every chunk's load issued up front
                       // (+1.5 % MLP over 4, profiles/r03_xq; 4 measured +1 % over 2 in round 1)
+#endif
+#ifndef SL_MLP_XQ256
+#define SL_MLP_XQ256 2  // the same for the 256-row tile (2 uint4 per thread and chunk: registers are short)
+#endif
+#ifndef SL_MLP_APF256
+#define SL_MLP_APF256 0  // A-fragment prefetch in the 256-row tile (64 more VGPRs)
+#endif
+#ifndef SL_MLP_RING256
+#define SL_MLP_RING256 2  // weight ring depth of the 256-row tile
 #endif
 namespace {
 constexpr int D_IN = 784;   // input features (28x28)
@@ -95,6 +105,7 @@ constexpr int BM = 64;       // batch rows granularity (the rows kernel runs 64 
 constexpr int HS_LD = 264;   // [64][256] bf16 LDS images: 528-B rows
 constexpr int XC_LD = 72;    // X chunk image rows: 64 k + 8 pad = 144 B (ds_read_b128 conflict-free)
 constexpr int DZ_LD = 40;
+constexpr int DZ_LD256 = 16;  // 256-row tile: the 10 (16) real dZ columns only; k 16..31 of the K=32 MFMA are zero registers
 constexpr int KS1 = D_INP / 32, KS2 = HID / 32;  // 32-deep k-steps of layer 1 / of 256-wide layers
 // k-steps layer 1 actually runs: 25 (784 = 24.5 x 32; the 26th step of the padded K is all zeros)
 constexpr int L1_KSTEPS_ROWS = (D_IN + 31) / 32;
@@ -272,10 +283,34 @@ __device__ __forceinline__ int row16_min(int v) {
 template <int BM, int NT, int NCOLS>
 __device__ __forceinline__ void copy_part(const uint16_t* src, int ld, uint16_t* dst, int gld, int tid, int it) {
   constexpr int CPR = NCOLS / 8;
-  static_assert(BM * CPR == 8 * NT, "copy_part splits the copy in 8 equal parts");
-  const int q = tid + it * NT;
-  const int r = q / CPR, c = (q - r * CPR) * 8;
-  *reinterpret_cast<short8_t*>(dst + (long)r * gld + c) = *reinterpret_cast<const short8_t*>(src + r * ld + c);
+  constexpr int PER = BM * CPR / (8 * NT);  // 16-B pieces per thread and call
+  static_assert(PER >= 1 && BM * CPR == 8 * NT * PER, "copy_part splits the copy in 8 equal parts");
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int q = tid + (it * PER + i) * NT;
+    const int r = q / CPR, c = (q - r * CPR) * 8;
+    *reinterpret_cast<short8_t*>(dst + (long)r * gld + c) = *reinterpret_cast<const short8_t*>(src + r * ld + c);
+  }
+}
+
+// copy_part through a buffer resource: one per-lane byte offset plus a constant SGPR
+// offset per piece (the flat form kept a 64-bit address per piece live across the
+// k-loop and spilled in the 256-row tile).  dst is the workgroup's first row.
+template <int BM, int NT, int NCOLS>
+__device__ __forceinline__ void copy_part_buf(const uint16_t* src, int ld, __amdgpu_buffer_rsrc_t dst, int gld, int tid,
+                                              int it) {
+  constexpr int CPR = NCOLS / 8, RPP = NT / CPR;  // rows per pass of all threads
+  constexpr int PER = BM * CPR / (8 * NT);
+  static_assert(PER >= 1 && BM * CPR == 8 * NT * PER && NT % CPR == 0, "copy_part_buf splits the copy in 8 equal parts");
+  const int r = tid / CPR, c = (tid % CPR) * 8;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int rr = r + (it * PER + i) * RPP;
+    const short8_t v = *reinterpret_cast<const short8_t*>(src + rr * ld + c);
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), dst, (r * gld + c) * 2,
+                                           (it * PER + i) * RPP * gld * 2, 0);
+  }
 }
 
 // BM batch rows per workgroup, BM/16 waves.  Wave w owns 16*NF output columns
@@ -291,22 +326,42 @@ __device__ __forceinline__ void copy_part(const uint16_t* src, int ld, uint16_t*
 // H2 overwrites H1 after layer 2 (the H1 ReLU mask survives as 4-bit bytes) and
 // dH1 overwrites dH2 -- so the LDS footprint drops from 72.7 KB to 42.8 KB and
 // three workgroups fit on a CU.
+//
+// BM = 256 (one 8-wave workgroup per CU, 2 x 4 waves of 128 rows x 64 features): every
+// weight fragment a wave streams from L2 feeds 8 MFMAs instead of 4, so the weight stream
+// per CU is half that of the 64- and 128-row tiles (32 KB per 1,024 MFMA cycles per SIMD
+// instead of per 512: those tiles ask the CU's vector-memory path for ~64 B/clk, its
+// limit).  At B = 65,536 the grid is exactly one workgroup per CU.  It runs the ONE
+// layout (one activation image + H1 nibble mask + a 16-column dZ image = 156 KB of LDS),
+// two X row passes per thread, a 2-deep weight ring and no A prefetch (register budget:
+// 128 accumulators of 256).
+template <int BM> constexpr int rows_nwv() { return BM == 256 ? 8 : BM / 16; }
 template <bool TRAIN, int BM, int WMG, bool L1 = true>
-__global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) void mlp_rows_kernel(MlpRowArgs a) {
-  constexpr int NWV = BM / 16;       // waves per workgroup
-  constexpr int MF = BM / 16 / WMG;  // m-fragments per wave
-  constexpr int NT = BM * 4;         // threads
-  constexpr int NF = 16 * WMG / NWV; // n-fragments per wave
-  constexpr bool ONE = SL_MLP_ONEIMG && BM == 64 && L1;
-  constexpr int RING = ONE ? SL_MLP_RING_ONE : (NF >= 4 ? SL_MLP_RING4 : SL_MLP_RING2);  // weight ring depth (k-steps)
+__global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) void mlp_rows_kernel(MlpRowArgs a) {
+  constexpr int NWV = rows_nwv<BM>();  // waves per workgroup
+  constexpr int MF = BM / 16 / WMG;    // m-fragments per wave
+  constexpr int NT = NWV * 64;         // threads
+  constexpr int NF = 16 * WMG / NWV;   // n-fragments per wave
+  constexpr bool BIG = BM == 256;
+  constexpr bool ONE = ((SL_MLP_ONEIMG && BM == 64) || BIG) && L1;
+  static_assert(!BIG || L1, "the 256-row tile has no train == 2 form");
+  constexpr int RING = BIG ? SL_MLP_RING256 : ONE ? SL_MLP_RING_ONE : (NF >= 4 ? SL_MLP_RING4 : SL_MLP_RING2);  // weight ring depth (k-steps)
+  constexpr bool APF = BIG ? SL_MLP_APF256 : SL_MLP_APF;  // prefetch the next k-step's A fragments
+  constexpr int XQ = BIG ? SL_MLP_XQ256 : SL_MLP_XQ;      // X chunks waiting in registers
+  constexpr int XP = BM * 4 / NT;                          // X row passes per thread (16 columns each)
+  constexpr int DZL = BIG ? DZ_LD256 : DZ_LD;
+  constexpr int SPW = BM / 16 / NWV;                       // 16-row softmax blocks per wave
   constexpr int REGB = BM * HS_LD;   // one LDS region (elements)
   static_assert(3 * BM * XC_LD <= REGB, "X ring must fit region 0");
-  constexpr int SMEM = ONE ? REGB + BM * DZ_LD + BM * 32 : 2 * REGB + BM * DZ_LD;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
+  constexpr int SMEM = ONE ? REGB + BM * DZL + BM * 32 : 2 * REGB + BM * DZL;
+  constexpr int BSZ = BIG ? (2 * HID + 16) * 2 : 0;  // BIG: b1 | b2 | b3 staged in LDS (fp32, as uint16 pairs)
+  static_assert((SMEM + BSZ) * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM + BSZ];
+  float* BS = reinterpret_cast<float*>(smem + SMEM);
   uint16_t* R0 = smem;                          // X ring -> H2 image -> dH2 image
   uint16_t* R1 = ONE ? smem : smem + REGB;      // H1 image -> dH1 image
   uint16_t* RZ = smem + (ONE ? REGB : 2 * REGB);  // dZ image
-  uint8_t* M1 = reinterpret_cast<uint8_t*>(smem + REGB + BM * DZ_LD);  // ONE: [BM][64] H1 mask nibbles
+  uint8_t* M1 = reinterpret_cast<uint8_t*>(smem + REGB + BM * DZL);  // ONE: [BM][64] H1 mask nibbles
   // ReLU masks are NOT kept in registers: H1/H2 stay in LDS until the masked
   // backward products overwrite them in place (hipcc held 64 compare masks per
   // layer in SGPR pairs and spilled ~200 SGPRs).
@@ -324,6 +379,27 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
     if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
+  // Workgroup barrier.  The 256-row tile (one workgroup per CU) waits only for LDS
+  // traffic: __syncthreads() also drains every outstanding global store (vmcnt(0)), and
+  // with all CUs storing the same activation at once that drain stalled the CU for
+  // up to ~12k cycles per barrier.  No global data is exchanged through a barrier here.
+  auto bar = [&]() {
+    if constexpr (BIG) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
+  };
+  if constexpr (BIG) {  // the epilogues read the biases from LDS (published by layer 1's barriers)
+    if (tid < 2 * HID / 4)
+      reinterpret_cast<float4*>(BS)[tid] = reinterpret_cast<const float4*>(tid < HID / 4 ? a.b1 : a.b2 - HID)[tid];
+    else if (tid < 2 * HID / 4 + NC)
+      BS[2 * HID + tid - 2 * HID / 4] = a.b3[tid - 2 * HID / 4];
+    static_assert(!BIG || NT * 8 == 16 * HID && BM * DZL >= 16 * HID, "W3 staging: one 16-B piece per thread into RZ");
+    reinterpret_cast<uint4*>(RZ)[tid] = reinterpret_cast<const uint4*>(a.w3h)[tid];
+  }
   if (a.stamps && tid == 0) {  // placement: HW_ID (CU / SH / SE) and XCC_ID
     a.stamps[(long)blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     a.stamps[(long)blockIdx.x * 16 + 11] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
@@ -335,12 +411,17 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
   // Normalisation coefficients as lane values (VGPRs): with both in SGPRs,
   // ROCm 7.2 emits a packed FMA that breaks the gfx950 constant-bus limit.
   const float nxa = a.xa + 0.f * (float)lane, nxb = a.xb + 0.f * (float)lane;
-  auto xload = [&](int c) -> uint4 {
+  // X row pass p covers rows xrow + p * NT / 4
+  auto xload = [&](int c, int p = 0) -> uint4 {
     if (SL_ROWS_KO == 2) return make_uint4(c, xrow, 7, 9);
-    return (c * 64 + xcol < D_IN) ? *reinterpret_cast<const uint4*>(xg + c * 64) : make_uint4(0, 0, 0, 0);
+    if (SL_ROWS_KO == 5)  // timing knockout: the same bytes as contiguous 16 KB blocks per chunk (wrong data)
+      return *reinterpret_cast<const uint4*>(a.x + (srow0 - row0 + row0) * D_IN +
+                                             ((long)c * BM * 64 + (long)p * NT * 16 + tid * 16) % ((long)BM * D_IN));
+    return (c * 64 + xcol < D_IN) ? *reinterpret_cast<const uint4*>(xg + (long)p * (NT / 4) * D_IN + c * 64)
+                                  : make_uint4(0, 0, 0, 0);
   };
-  auto xstore = [&](int c, uint4 v) {
-    uint16_t* d = R0 + (SL_MLP_APF ? c % 3 : c & 1) * BM * XC_LD + xrow * XC_LD + xcol;
+  auto xstore = [&](int c, uint4 v, int p = 0) {
+    uint16_t* d = R0 + (APF ? c % 3 : c & 1) * BM * XC_LD + (xrow + p * (NT / 4)) * XC_LD + xcol;
     short8_t lo = zero8(), hi = zero8();
     if (c * 64 + xcol < D_IN) {
       lo = u8x8_to_bf16(make_uint2(v.x, v.y), nxa, nxb);
@@ -375,6 +456,28 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
 #pragma unroll
       for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(b[n], af[m], acc[m][n]);
   };
+  // one 256-deep layer (K = 256, A = an activation image, B = a fragment-ordered weight)
+  auto k256 = [&](const FragSrc& fw, const uint16_t* ha, auto&& after) {
+    if constexpr (APF) {
+      kloop_ring_a<KS2, NF, MF, RING>(
+          [&](short8_t (&r)[NF], int st) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) r[n] = fw(n, st, KS2);
+          },
+          [&](short8_t (&af)[MF], int st) {
+#pragma unroll
+            for (int m = 0; m < MF; ++m) af[m] = lds8(ha + st * 32 + (rw + m * 16) * HS_LD);
+          },
+          mfma_ab, after);
+    } else {
+      kloop_ring<KS2, NF, RING>(
+          [&](short8_t (&r)[NF], int st) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) r[n] = fw(n, st, KS2);
+          },
+          [&](int st, short8_t (&b)[NF]) { mfma_step(ha + st * 32, HS_LD, b); }, after);
+    }
+  };
   // bias + ReLU epilogue into a [BM][HS_LD] image (+ the nibble mask of H > 0)
   auto relu_out = [&](const float* bias_v, uint16_t* img, bool with_mask) {
 #pragma unroll
@@ -394,14 +497,20 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
       }
     }
   };
-  // ONE: write acc * 1[H1 > 0] from the nibble mask
+  // ONE: write acc * 1[H1 > 0] from the nibble mask.  The byte base is made opaque so
+  // that hipcc recomputes it here instead of keeping relu_out's 32 mask addresses
+  // alive across the whole kernel (it spilled them, and each spill reload's vmcnt(0)
+  // drained the dH2 stores in flight).
   auto masked_bits_out = [&](uint16_t* img) {
+    int mbo = (rw + lr) * 64 + (cw >> 2) + lg;
+    asm volatile("" : "+v"(mbo));
+    const uint8_t* M1b = M1 + mbo;
 #pragma unroll
     for (int n = 0; n < NF; ++n) {
       const int col = cw + n * 16 + 4 * lg;
 #pragma unroll
       for (int m = 0; m < MF; ++m) {
-        const uint32_t b = M1[(rw + m * 16 + lr) * 64 + (col >> 2)];
+        const uint32_t b = M1b[(m * 16) * 64 + n * 4];
         uint2 v;
         v.x = pack2((b & 1u) ? acc[m][n][0] : 0.f, (b & 2u) ? acc[m][n][1] : 0.f);
         v.y = pack2((b & 4u) ? acc[m][n][2] : 0.f, (b & 8u) ? acc[m][n][3] : 0.f);
@@ -433,8 +542,11 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
   const FragSrc f_w3(a.w3h, 16 * HID * 2, 0, KS2, lane);
   const FragSrc f_w3t(a.w3th, HID * 32 * 2, NF * wng, 1, lane);
 
-  // labels of this lane's 4 softmax rows (wave * 16 + 4 lg + r), fetched long before use
-  const uint32_t lab4 = a.y ? *reinterpret_cast<const uint32_t*>(a.y + srow0 + wave * 16 + 4 * lg) : 0u;
+  // labels of this lane's 4 softmax rows ((sp * NWV + wave) * 16 + 4 lg + r), fetched long before use
+  uint32_t lab4[SPW];
+#pragma unroll
+  for (int sp = 0; sp < SPW; ++sp)
+    lab4[sp] = a.y ? *reinterpret_cast<const uint32_t*>(a.y + srow0 + (sp * NWV + wave) * 16 + 4 * lg) : 0u;
 
   if constexpr (!L1) {
 #pragma unroll
@@ -445,7 +557,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
     stamp(1);
   } else {
   zero_acc();
-  constexpr bool XWIDE = SL_MLP_XW == 128 && SL_MLP_APF && !ONE;
+  constexpr bool XWIDE = SL_MLP_XW == 128 && APF && !ONE;
   if constexpr (XWIDE) {
     // 128-column X chunks: 7 chunks, one barrier per four k-steps instead of per
     // two. The 3-slot ring (144-element rows: ds_read_b128 conflict-free) spans
@@ -476,7 +588,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
       }
     };
     xstore2(0);
-    __syncthreads();
+    bar();
     kloop_ring_a<L1_KSTEPS_ROWS, NF, MF, RING>(
         [&](short8_t (&r)[NF], int st) {
 #pragma unroll
@@ -493,97 +605,182 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
           // barrier before step 4c+3 prefetches it; its slot held chunk c-2
           if (!(st & 3)) {
             if ((st >> 2) + 1 < NCH) xstore2((st >> 2) + 1);
-            __syncthreads();
+            bar();
           }
         });
   } else {
     // X chunks c+1 .. c+XQ wait in registers (slot chunk % XQ): the u8 input
     // comes from HBM, so its prefetch distance is set apart from the weight ring
-    uint4 xq[SL_MLP_XQ];
+    uint4 xq[XQ][XP];
+    if constexpr (!BIG) {
 #pragma unroll
-    for (int i = 1; i <= SL_MLP_XQ; ++i) xq[i % SL_MLP_XQ] = i < NCHUNK ? xload(i) : make_uint4(0, 0, 0, 0);
-    xstore(0, xload(0));
-    __syncthreads();
-#if SL_MLP_APF
-    // 3-slot X ring: chunk c+1 is converted after the first k-step of chunk c and
-    // published by the barrier right after it, so step 2c+1 can prefetch step
-    // 2c+2's fragments; its slot last held chunk c-2, read before the barrier of
-    // step 2c-2
-    kloop_ring_a<L1_KSTEPS_ROWS, NF, MF, RING>(
-        [&](short8_t (&r)[NF], int st) {
+      for (int i = 1; i <= XQ; ++i)
 #pragma unroll
-          for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
-        },
-        [&](short8_t (&af)[MF], int st) {
-          const uint16_t* ab = R0 + ((st >> 1) % 3) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg;
+        for (int p = 0; p < XP; ++p) xq[i % XQ][p] = i < NCHUNK ? xload(i, p) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-          for (int m = 0; m < MF; ++m) af[m] = lds8(ab + (rw + m * 16) * XC_LD);
-        },
-        mfma_ab,
-        [&](int st) {
-          const int c = st >> 1;
-          if (!(st & 1)) {
-            if (c + 1 < NCHUNK) xstore(c + 1, xq[(c + 1) % SL_MLP_XQ]);
-            if (c + 1 + SL_MLP_XQ < NCHUNK) xq[(c + 1) % SL_MLP_XQ] = xload(c + 1 + SL_MLP_XQ);
-            __syncthreads();
-          }
-        });
-#else
-    kloop_ring<L1_KSTEPS_ROWS, NF, RING>(
-        [&](short8_t (&r)[NF], int st) {
+      for (int p = 0; p < XP; ++p) xstore(0, xload(0, p), p);
+      bar();
+    }
+    auto xnext = [&](int c) {  // convert chunk c+1 into its ring slot, refill its register slot
 #pragma unroll
-          for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
-        },
-        [&](int st, short8_t (&b)[NF]) {
-          mfma_step(R0 + ((st >> 1) & 1) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg, XC_LD, b);
-        },
-        [&](int st) {
-          // chunk c+1 is converted into the free ring slot after the FIRST k-step of
-          // chunk c (that slot's readers all passed the barrier that ended chunk c-1);
-          // the barrier after the second k-step publishes it
-          const int c = st >> 1;
-          if (!(st & 1)) {
-            if (c + 1 < NCHUNK) xstore(c + 1, xq[(c + 1) % SL_MLP_XQ]);
-            if (c + 1 + SL_MLP_XQ < NCHUNK) xq[(c + 1) % SL_MLP_XQ] = xload(c + 1 + SL_MLP_XQ);
-          } else {
-            __syncthreads();
-          }
-        });
-#endif
+      for (int p = 0; p < XP; ++p) {
+        if (c + 1 < NCHUNK) xstore(c + 1, xq[(c + 1) % XQ][p], p);
+        if (c + 1 + XQ < NCHUNK) xq[(c + 1) % XQ][p] = xload(c + 1 + XQ, p);
+      }
+    };
+    if constexpr (BIG) {
+      // 256-row tile: a 4-slot ring of unpadded 64-column bf16 chunks (4 x 32 KB; 16-B
+      // pieces XOR-swizzled by (row / 2) % 8, which keeps the A-fragment ds_read_b128
+      // conflict-free without the 144-B padded rows), so the waves meet at one barrier
+      // per two chunks (4 k-steps) instead of one per chunk: with all 8 waves in
+      // lock-step each barrier exposed the slowest wave's X-load and weight latency
+      // (barrier knockout: -14k of 48k layer-1 cycles).  Period k reads chunks 2k, 2k+1
+      // and converts chunks 2k+2, 2k+3 (one row pass per k-step, each conversion piece
+      // between two MFMA groups), whose slots were last read in period k-1.
+      static_assert(XP == 2 && !APF && XQ == 2, "one row pass per k-step, chunks 2k+2 / 2k+3 in registers");
+      static_assert(4 * BM * 64 <= REGB, "4-slot X ring must fit the image region");
+      constexpr int XS = BM * 64;  // slot (elements)
+      auto xput = [&](int c, int p, const uint32_t (&pk)[8]) {
+        const int row = xrow + p * (NT / 4);
+        const bool real = c * 64 + xcol < D_IN;
+        uint16_t* d = R0 + (c & 3) * XS + row * 64;
+        const int ch = xcol >> 3, sw = (row >> 1) & 7;
+        *reinterpret_cast<uint4*>(d + ((ch ^ sw) << 3)) = real ? make_uint4(pk[0], pk[1], pk[2], pk[3]) : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(d + (((ch + 1) ^ sw) << 3)) = real ? make_uint4(pk[4], pk[5], pk[6], pk[7]) : make_uint4(0, 0, 0, 0);
+      };
+      auto xcvt = [&](const uint4& v, uint32_t (&pk)[8]) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          pk[m] = pack2((float)((w[m >> 1] >> ((m & 1) * 16)) & 0xffu) * nxa + nxb,
+                        (float)((w[m >> 1] >> ((m & 1) * 16 + 8)) & 0xffu) * nxa + nxb);
+      };
+      // prologue: chunks 0, 1 converted, 2, 3 waiting in registers
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int p = 0; p < XP; ++p) {
+          uint32_t pk[8];
+          xcvt(xload(c, p), pk);
+          xput(c, p, pk);
+        }
+#pragma unroll
+      for (int c = 2; c < 4; ++c)
+#pragma unroll
+        for (int p = 0; p < XP; ++p) xq[c & 1][p] = xload(c, p);
+      short8_t r[RING][NF];
+#pragma unroll
+      for (int i = 0; i < RING; ++i)
+#pragma unroll
+        for (int n = 0; n < NF; ++n) r[i][n] = f_w1(n, i, KS1);
+      bar();
+      __builtin_amdgcn_sched_barrier(0);
+      const int swz = (lr >> 1) & 7;
+#pragma unroll
+      for (int st = 0; st < L1_KSTEPS_ROWS; ++st) {
+        const int c = st >> 1, q = st & 3;
+        const int cc = 2 * (st >> 2) + 2 + (q >> 1);  // chunk converted at this step (pass q & 1)
+        const bool conv = cc < NCHUNK;
+        const uint16_t* ab = R0 + (c & 3) * XS + lr * 64 + ((((st & 1) * 4 + lg) ^ swz) << 3);
+        const uint4 xv = xq[cc & 1][q & 1];
+        const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+        uint32_t pk[8];
+        short8_t af[MF];
+        af[0] = lds8(ab + rw * 64);
+        af[1] = lds8(ab + (rw + 16) * 64);
+#pragma unroll
+        for (int m = 0; m < MF; ++m) {
+          if (m + 2 < MF) af[m + 2] = lds8(ab + (rw + (m + 2) * 16) * 64);
+#pragma unroll
+          for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(r[st % RING][n], af[m], acc[m][n]);
+          if (conv)  // piece m of the pass: bytes 2m, 2m+1
+            pk[m] = pack2((float)((xw[m >> 1] >> ((m & 1) * 16)) & 0xffu) * nxa + nxb,
+                          (float)((xw[m >> 1] >> ((m & 1) * 16 + 8)) & 0xffu) * nxa + nxb);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (conv) xput(cc, q & 1, pk);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + RING < L1_KSTEPS_ROWS && SL_ROWS_KO != 3) {  // knockout 3: no W1 reloads (wrong numerics)
+#pragma unroll
+          for (int n = 0; n < NF; ++n) r[st % RING][n] = f_w1(n, st + RING, KS1);
+        }
+        if ((q & 1) && cc + 2 < NCHUNK) {  // both passes of chunk cc are out: its register slot takes cc + 2
+#pragma unroll
+          for (int p = 0; p < XP; ++p) xq[cc & 1][p] = xload(cc + 2, p);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (q == 3 && SL_ROWS_KO != 4) bar();  // publishes chunks 2k+2, 2k+3; period k's slots are free
+      }
+    } else if constexpr (APF) {
+      // 3-slot X ring: chunk c+1 is converted after the first k-step of chunk c and
+      // published by the barrier right after it, so step 2c+1 can prefetch step
+      // 2c+2's fragments; its slot last held chunk c-2, read before the barrier of
+      // step 2c-2
+      kloop_ring_a<L1_KSTEPS_ROWS, NF, MF, RING>(
+          [&](short8_t (&r)[NF], int st) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
+          },
+          [&](short8_t (&af)[MF], int st) {
+            const uint16_t* ab = R0 + ((st >> 1) % 3) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg;
+#pragma unroll
+            for (int m = 0; m < MF; ++m) af[m] = lds8(ab + (rw + m * 16) * XC_LD);
+          },
+          mfma_ab,
+          [&](int st) {
+            if (!(st & 1)) {
+              xnext(st >> 1);
+              bar();
+            }
+          });
+    } else {
+      kloop_ring<L1_KSTEPS_ROWS, NF, RING>(
+          [&](short8_t (&r)[NF], int st) {
+#pragma unroll
+            for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
+          },
+          [&](int st, short8_t (&b)[NF]) {
+            mfma_step(R0 + ((st >> 1) & 1) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg, XC_LD, b);
+          },
+          [&](int st) {
+            // chunk c+1 is converted into the free ring slot after the FIRST k-step of
+            // chunk c (that slot's readers all passed the barrier that ended chunk c-1);
+            // the barrier after the second k-step publishes it
+            if (!(st & 1)) xnext(st >> 1);
+            else bar();
+          });
+    }
   }
   stamp(1);
-  if constexpr (ONE) __syncthreads();  // the X ring shares the image H1 goes to
-  relu_out(a.b1, R1, true);
+  if constexpr (ONE) bar();  // the X ring shares the image H1 goes to
+  stamp(12);
+  relu_out(BIG ? BS : a.b1, R1, true);
+  stamp(13);
   }
-  __syncthreads();
+  bar();
   stamp(2);
 
   // ---- layer 2: H2 = relu(H1 W2^T + b2), K = 256; A = R1, out -> R0 ----
+  // BIG: the dH2 weights are loaded before the H1 stores go out.  vmcnt retires in issue
+  // order, so a load issued after them would make its first use wait for every H1 store.
+  short8_t w3tf[NF];
+  if constexpr (BIG) {
+#pragma unroll
+    for (int n = 0; n < NF; ++n) w3tf[n] = f_w3t(n, 0, 1);
+  }
   zero_acc();
   {
     const uint16_t* ha = R1 + lr * HS_LD + 8 * lg;
-#if SL_MLP_APF
-    kloop_ring_a<KS2, NF, MF, RING>(
-        [&](short8_t (&r)[NF], int st) {
-#pragma unroll
-          for (int n = 0; n < NF; ++n) r[n] = f_w2(n, st, KS2);
-        },
-        [&](short8_t (&af)[MF], int st) {
-#pragma unroll
-          for (int m = 0; m < MF; ++m) af[m] = lds8(ha + st * 32 + (rw + m * 16) * HS_LD);
-        },
-        mfma_ab,
-#else
-    kloop_ring<KS2, NF, RING>(
-        [&](short8_t (&r)[NF], int st) {
-#pragma unroll
-          for (int n = 0; n < NF; ++n) r[n] = f_w2(n, st, KS2);
-        },
-        [&](int st, short8_t (&b)[NF]) { mfma_step(ha + st * 32, HS_LD, b); },
-#endif
-        [&](int st) {
-          if (TRAIN && L1) copy_part<BM, NT, HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid, st);
-        });
+    if constexpr (BIG) {
+      const auto dst = __builtin_amdgcn_make_buffer_rsrc(a.h1 + (long)row0 * HID, 0, BM * HID * 2, 0x00020000);
+      k256(f_w2, ha, [&](int st) {
+        if (TRAIN) copy_part_buf<BM, NT, HID>(R1, HS_LD, dst, HID, tid, st);
+      });
+    } else {
+      k256(f_w2, ha, [&](int st) {
+        if (TRAIN && L1) copy_part<BM, NT, HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid, st);
+      });
+    }
   }
   stamp(3);
   short8_t w3f[KS2];  // layer-3 weights, prefetched under the ReLU-2 epilogue
@@ -591,33 +788,45 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
 #pragma unroll
     for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
   }
-  if constexpr (ONE) __syncthreads();  // every wave is done reading H1: H2 replaces it
-  relu_out(a.b2, R0, false);
-  if constexpr (ONE) {  // after the epilogue: the 32 registers would push past the 168 budget
+  if constexpr (ONE) bar();  // every wave is done reading H1: H2 replaces it
+  stamp(14);
+  relu_out(BIG ? BS + HID : a.b2, R0, false);
+  if constexpr (BIG) {  // from the copy of W3 staged in the dZ image at the start (no global load)
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) w3f[ks] = lds8(RZ + ks * 512 + lane * 8);
+  } else if constexpr (ONE) {  // after the epilogue: the 32 registers would push past the 168 budget
 #pragma unroll
     for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
   }
-  __syncthreads();
+  bar();
   stamp(4);
 
   // ---- layer 3 + softmax cross-entropy: wave w owns rows 16w..16w+15; dZ -> RZ ----
   // Row reductions over the 16 lanes holding one row's logits run on DPP
   // (quad perms + row half-mirror + row mirror), not ds_bpermute shuffles whose
   // LDS round trips made this phase ~10k cycles; W3 and labels were prefetched.
-  {
-    floatx4_t z = zero4();
-    const uint16_t* ha = R0 + (wave * 16 + lr) * HS_LD + 8 * lg;
+  floatx4_t z3[SPW];  // the passes' logits first: their MFMA chains interleave
 #pragma unroll
-    for (int ks = 0; ks < KS2; ++ks) z = mfma16(lds8(ha + ks * 32), w3f[ks], z);
+  for (int sp = 0; sp < SPW; ++sp) z3[sp] = zero4();
+#pragma unroll
+  for (int ks = 0; ks < KS2; ++ks)
+#pragma unroll
+    for (int sp = 0; sp < SPW; ++sp)
+      z3[sp] = mfma16(lds8(R0 + ((sp * NWV + wave) * 16 + lr) * HS_LD + 8 * lg + ks * 32), w3f[ks], z3[sp]);
+  if constexpr (BIG) bar();  // every wave holds W3 in registers: dZ may overwrite its staging copy
+#pragma unroll
+  for (int sp = 0; sp < SPW; ++sp) {
+    const int rb = (sp * NWV + wave) * 16;  // this pass's 16 rows
+    const floatx4_t z = z3[sp];
     const int c = lr;
-    const float bias3 = c < NC ? a.b3[c] : 0.f;
+    const float bias3 = c < NC ? (BIG ? BS[2 * HID + c] : a.b3[c]) : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = wave * 16 + 4 * lg + r;
+      const int row = rb + 4 * lg + r;
       const float zz = c < NC ? z[r] + bias3 : -INFINITY;
       const float mx = row16_max(zz);
       const float e = c < NC ? __expf(zz - mx) : 0.f;
-      int lab = (int)((lab4 >> (8 * r)) & 0xffu);
+      int lab = (int)((lab4[sp] >> (8 * r)) & 0xffu);
       lab = lab < NC ? lab : 0;
       const float s = row16_sum(e);
       const float zl = row16_sum(c == lab ? zz : 0.f);
@@ -630,13 +839,13 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
       if (a.logits && c < NC) a.logits[(long)(row0 + row) * NC + c] = zz;
       if (TRAIN) {
         const float dzv = c < NC ? (e / s - (c == lab ? 1.f : 0.f)) * a.grad_scale : 0.f;
-        RZ[row * DZ_LD + c] = f2bf(dzv);
-        RZ[row * DZ_LD + 16 + c] = 0;
+        RZ[row * DZL + c] = f2bf(dzv);
+        if constexpr (DZL > 16) RZ[row * DZL + 16 + c] = 0;
       }
     }
   }
   if (!TRAIN) return;
-  __syncthreads();
+  bar();
   stamp(5);
 
   // ---- [dW3 | db3] partial over this wave's 64 rows: dZ^T (RZ) . H2 (R0), both read
@@ -655,7 +864,7 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int k0 = rh + 32 * ks;
-      const short8_t af = lds_tr8(RZ + k0 * DZ_LD, DZ_LD, lane);  // A[c][row] = dZ[row][c]
+      const short8_t af = lds_tr8(RZ + k0 * DZL, DZL, lane);  // A[c][row] = dZ[row][c]
 #pragma unroll
       for (int n = 0; n < NF; ++n) d3[n] = mfma16(af, lds_tr8(R0 + k0 * HS_LD + cw + n * 16, HS_LD, lane), d3[n]);
       if (wng == 0) db3 = mfma16(af, ones, db3);
@@ -677,12 +886,24 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
   {
     short8_t bf[NF];
 #pragma unroll
-    for (int n = 0; n < NF; ++n) bf[n] = f_w3t(n, 0, 1);
-    mfma_step(RZ + lr * DZ_LD + 8 * lg, DZ_LD, bf);
+    for (int n = 0; n < NF; ++n) bf[n] = BIG ? w3tf[n] : f_w3t(n, 0, 1);
+    if constexpr (DZL > 16) {
+      mfma_step(RZ + lr * DZL + 8 * lg, DZL, bf);
+    } else {  // columns 16..31 of the K = 32 step are zero registers, not LDS
+      short8_t af[MF];
+      int lane_o = threadIdx.x & 63;  // recomputed, not a long-lived (spilled) register
+      asm volatile("" : "+v"(lane_o));
+#pragma unroll
+      for (int m = 0; m < MF; ++m) {
+        const short8_t v = lds8(RZ + (rw + m * 16 + lr) * DZL + 8 * ((lane_o >> 4) & 1));
+        af[m] = lane_o < 32 ? v : zero8();
+      }
+      mfma_ab(af, bf);
+    }
   }
   stamp(6);
   masked_out(R0);
-  __syncthreads();
+  bar();
   stamp(7);
   // column sums of the masked dH2 over this wave's 64 rows: the db2 partial (ones-row MFMA)
   auto col_sums = [&](const uint16_t* img, int off) {
@@ -713,35 +934,22 @@ __global__ __launch_bounds__(BM * 4, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) voi
   zero_acc();
   {
     const uint16_t* ha = R0 + lr * HS_LD + 8 * lg;
-#if SL_MLP_APF
-    kloop_ring_a<KS2, NF, MF, RING>(
-        [&](short8_t (&r)[NF], int st) {
-#pragma unroll
-          for (int n = 0; n < NF; ++n) r[n] = f_w2t(n, st, KS2);
-        },
-        [&](short8_t (&af)[MF], int st) {
-#pragma unroll
-          for (int m = 0; m < MF; ++m) af[m] = lds8(ha + st * 32 + (rw + m * 16) * HS_LD);
-        },
-        mfma_ab,
-#else
-    kloop_ring<KS2, NF, RING>(
-        [&](short8_t (&r)[NF], int st) {
-#pragma unroll
-          for (int n = 0; n < NF; ++n) r[n] = f_w2t(n, st, KS2);
-        },
-        [&](int st, short8_t (&b)[NF]) { mfma_step(ha + st * 32, HS_LD, b); },
-#endif
-        [&](int st) { copy_part<BM, NT, HID>(R0, HS_LD, a.dh2 + (long)row0 * HID, HID, tid, st); });
+    if constexpr (BIG) {
+      const auto dst = __builtin_amdgcn_make_buffer_rsrc(a.dh2 + (long)row0 * HID, 0, BM * HID * 2, 0x00020000);
+      k256(f_w2t, ha, [&](int st) { copy_part_buf<BM, NT, HID>(R0, HS_LD, dst, HID, tid, st); });
+    } else {
+      k256(f_w2t, ha, [&](int st) { copy_part<BM, NT, HID>(R0, HS_LD, a.dh2 + (long)row0 * HID, HID, tid, st); });
+    }
   }
   stamp(8);
   if constexpr (ONE) {
-    __syncthreads();  // every wave is done reading dH2: dH1 replaces it
+    bar();  // every wave is done reading dH2: dH1 replaces it
     masked_bits_out(R1);
   } else {
     masked_out(R1);
   }
-  __syncthreads();
+  bar();
+  stamp(15);
   copy_out_f16<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid, a.dh1_scale);
   col_sums(R1, W3P_DB1);
   stamp(9);
@@ -1832,10 +2040,19 @@ int sl_mlp_set_rows_bm(int bm) {
 
 // Rows per workgroup (64 by default; 128 = one 8-wave workgroup per CU on request).
 int sl_mlp_rows_bm(int batch) {
-  if (g_rows_bm == 64 || (g_rows_bm == 128 && batch % 128 == 0)) return g_rows_bm;
-  // 64 (two co-resident workgroups per CU overlap each other's epilogues) measured
-  // ahead of 128 at every batch size tried (profiles/r01_v7)
-  (void)batch;
+  if (g_rows_bm == 64 || (g_rows_bm == 128 && batch % 128 == 0) || (g_rows_bm == 256 && batch % 256 == 0))
+    return g_rows_bm;
+  // 256 (one 8-wave workgroup per CU, half the weight stream per FLOP) once the batch
+  // fills every CU with such tiles: +2-4 % MLP over 64 at B = 65,536 in same-box A/B
+  // runs (profiles/r03_big).  Below that, 64 (two co-resident workgroups per CU overlap
+  // each other's epilogues) measured ahead of 128 at every batch size tried (r01_v7).
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  if (batch % 256 == 0 && batch / 256 >= cus) return 256;
   return 64;
 }
 
@@ -1856,7 +2073,10 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
   // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_l1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);
-  if (bm == 128) {
+  if (bm == 256 && train != 2) {
+    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 256, 2>), dim3(batch / 256), dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 256, 2>), dim3(batch / 256), dim3(512), 0, stream, a);
+  } else if (bm == 128) {
     if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, SL_ROWS128_WMG, false>), dim3(batch / 128), dim3(512), 0, stream, a);
     else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, SL_ROWS128_WMG>), dim3(batch / 128), dim3(512), 0, stream, a);
     else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, SL_ROWS128_WMG>), dim3(batch / 128), dim3(512), 0, stream, a);

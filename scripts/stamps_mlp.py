@@ -30,6 +30,12 @@ names = ["layer1", "relu1", "layer2+h1", "relu2", "layer3+ce", "dW3 part+dH2", "
 print(f"B={B} BM={bm} workgroups={s.shape[0]}  total median cycles {float((s[:, 9] - s[:, 0]).median()):.0f}")
 for i, n in enumerate(names):
     print(f"  {n:14s} median {float(d[:, i].median()):8.0f}  mean {float(d[:, i].mean()):8.0f}")
+e = st.view(-1, 16).cpu().double()
+if bool((e[:, 12] != 0).all()):
+    for n, (i, j) in {"l1 end wait": (1, 12), "relu1 body": (12, 13), "relu1 barrier": (13, 2),
+                      "l2 end wait": (3, 14), "relu2+w3 tail": (14, 4), "dH1 mask+bar": (8, 15),
+                      "dh1 out+colsum": (15, 9)}.items():
+        print(f"  {n:14s} median {float((e[:, j] - e[:, i]).median()):8.0f}")
 t0 = s[:, 0] - s[:, 0].min()
 print(f"  start spread: median {float(t0.median()):.0f} max {float(t0.max()):.0f}")
 

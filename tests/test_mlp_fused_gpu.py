@@ -17,7 +17,7 @@ def _rel(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
 
-@pytest.mark.parametrize("bm", [64, 128])
+@pytest.mark.parametrize("bm", [64, 128, 256])
 def test_logits_match_reference(bm, rows_bm):
     rows_bm(bm)
     x, y = _data(256)
@@ -38,7 +38,8 @@ def rows_bm():
 
 
 @pytest.mark.parametrize("batch,bm,l1", [(64, 64, True), (512, 64, True), (2048, 64, True), (512, 128, True),
-                                         (2048, 128, True), (2048, 64, False), (512, 128, False)])
+                                         (2048, 128, True), (2048, 64, False), (512, 128, False),
+                                         (512, 256, False), (2048, 256, False)])
 def test_gradients_match_reference(batch, bm, l1, rows_bm):
     from serverless_learn_amd.ops import _native
 
