@@ -92,6 +92,12 @@ using namespace sl;
 #ifndef SL_MLP_APF256
 #define SL_MLP_APF256 0  // A-fragment prefetch in the 256-row tile (64 more VGPRs)
 #endif
+#ifndef SL_DH1_WIDE
+#define SL_DH1_WIDE 0  // 256-row tile: dH1 stored as 16-B pieces after a permlane16 swap.  Off: the
+                       // gradients of one step are right, but training diverges non-deterministically
+                       // (NaN within 30 steps, scripts/check_mlp_det.py) even with s_nop around the
+                       // swap; the 8-B stores are exact and deterministic (profiles/r03_big)
+#endif
 #ifndef SL_MLP_RING256
 #define SL_MLP_RING256 2  // weight ring depth of the 256-row tile
 #endif
@@ -942,16 +948,113 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
     }
   }
   stamp(8);
-  if constexpr (ONE) {
-    bar();  // every wave is done reading dH2: dH1 replaces it
-    masked_bits_out(R1);
+  if constexpr (BIG) {
+    // dH1 straight from the accumulators: mask (H1 nibbles), fp16 of dH1 * dh1_scale to
+    // HBM (8 B per fragment row), and the db1 partial as fp32 column sums (DPP over the
+    // 16 rows of a fragment).  The LDS image + barrier + re-read of the other tiles cost
+    // ~16k cycles here with every CU in this phase at once (profiles/r03_big).
+    int mbo = (rw + lr) * 64 + (cw >> 2) + lg;
+    asm volatile("" : "+v"(mbo));
+    const uint8_t* M1b = M1 + mbo;
+    const auto dst = __builtin_amdgcn_make_buffer_rsrc(a.dh1 + (long)row0 * HID, 0, BM * HID * 2, 0x00020000);
+    // after the permlane16 swap of fragments (n, n+1) a lane holds 8 consecutive columns:
+    // fragment n + (lg & 1), columns 8 (lg >> 1) .. +7 (cdna_hip_programming.md T21)
+    const int voff = ((rw + lr) * HID + cw + (lg & 1) * 16 + (lg >> 1) * 8) * 2;
+    const int voff8 = ((rw + lr) * HID + cw + 4 * lg) * 2;  // 8-B form: this lane's own 4 columns
+    const float sc = a.dh1_scale;
+    uint32_t hv[NF][2];
+    floatx4_t cs[MF / 4][NF];
+#pragma unroll
+    for (int hr = 0; hr < MF / 4; ++hr)
+#pragma unroll
+      for (int n = 0; n < NF; ++n) cs[hr][n] = zero4();
+#pragma unroll
+    for (int m = 0; m < MF; ++m) {
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        const int b = M1b[(m * 16) * 64 + n * 4];
+        floatx4_t v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)  // bit r sign-extended to an all-ones / zero mask
+          v[r] = __int_as_float(__float_as_int(acc[m][n][r]) & __builtin_amdgcn_sbfe(b, r, 1));
+        cs[m >> 2][n] += v;
+        const floatx4_t vs = v * sc;
+        hv[n][0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(vs[0], vs[1]));
+        hv[n][1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(vs[2], vs[3]));
+      }
+#if !SL_DH1_WIDE
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t h = {hv[n][0], hv[n][1]};
+        __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, 0);
+      }
+#else
+#pragma unroll
+      for (int n = 0; n < NF; n += 2) {
+        typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+        u32x4_t o;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          // inline asm with the 2 wait states the VALU write -> v_permlane read hazard
+          // needs: the builtin's codegen (ROCm 7.2) issued the swap right behind the
+          // v_cvt_pkrtz that wrote its operand and read stale lanes (non-deterministic
+          // dH1, training diverged in the bench while the small-batch tests passed)
+          uint32_t lo = hv[n][d], hi = hv[n + 1][d];
+          asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(lo), "+v"(hi));
+          o[d] = lo;
+          o[2 + d] = hi;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(o, dst, voff, (m * 16 * HID + n * 16) * 2, 0);
+      }
+#endif
+    }
+    // Transpose-reduce of the 32 column partials over the 16 rows of a DPP row: each
+    // stage pairs lane i with i^15, i^7, i^2, i^1 (row_mirror, row_half_mirror, quad
+    // perms), keeps the half of the values chosen by the lane bit the partners differ
+    // in and adds the partner's other half: 90 VALU instead of 32 row16_sums (256).
+    // Value index hr*16 + n*4 + r; lane lr ends with index j*16 + lr0*8 + lr1*4 +
+    // lr2*2 + lr3 (lrK = bit K of lr) for j = 0, 1.
+    static_assert(MF / 4 == 2 && NF == 4, "32 partials per lane");
+    float red[32];
+#pragma unroll
+    for (int hr = 0; hr < 2; ++hr)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[hr * 16 + n * 4 + r] = cs[hr][n][r];
+    auto stage = [&](auto ctrl_c, int bit, int cnt) {
+      constexpr int CTRL = decltype(ctrl_c)::value;
+#pragma unroll
+      for (int i = 0; i < cnt; ++i) {
+        const float keep = bit ? red[2 * i + 1] : red[2 * i];
+        const float send = bit ? red[2 * i] : red[2 * i + 1];
+        red[i] = keep + dpp_f<CTRL>(send);
+      }
+    };
+    stage(std::integral_constant<int, 0x140>{}, (lr >> 3) & 1, 16);
+    stage(std::integral_constant<int, 0x141>{}, (lr >> 2) & 1, 8);
+    stage(std::integral_constant<int, 0x4E>{}, (lr >> 1) & 1, 4);
+    stage(std::integral_constant<int, 0xB1>{}, lr & 1, 2);
+    {
+      const int n = 2 * (lr & 1) + ((lr >> 1) & 1), r = 2 * ((lr >> 2) & 1) + ((lr >> 3) & 1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        a.w3p[(long)((row0 + rw + 64 * j) >> 6) * W3P_LD + W3P_DB1 + cw + n * 16 + 4 * lg + r] = red[j];
+    }
+    stamp(15);
   } else {
-    masked_out(R1);
+    if constexpr (ONE) {
+      bar();  // every wave is done reading dH2: dH1 replaces it
+      masked_bits_out(R1);
+    } else {
+      masked_out(R1);
+    }
+    bar();
+    stamp(15);
+    copy_out_f16<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid, a.dh1_scale);
+    col_sums(R1, W3P_DB1);
   }
-  bar();
-  stamp(15);
-  copy_out_f16<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid, a.dh1_scale);
-  col_sums(R1, W3P_DB1);
   stamp(9);
 }
 

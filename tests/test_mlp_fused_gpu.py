@@ -168,3 +168,27 @@ def test_allreduce_hook_path_matches_single_rank():
         b.step()
     torch.cuda.synchronize()
     assert torch.allclose(a.get_flat(), b.get_flat(), rtol=1e-5, atol=1e-6)
+
+
+def test_training_is_deterministic_at_full_batch():
+    """Two 30-step runs from the same start give bit-identical, finite parameters at the
+    bench batch (B = 65,536: the 256-row rows tile on a 256-CU part).  A one-step gradient
+    check alone missed a store hazard that only broke multi-step training."""
+    from serverless_learn_amd.ops import _native
+
+    B = 65536
+    x, y = _data(B * 2, seed=5)
+    flat = M.init_params(4)
+    out = []
+    for _ in range(2):
+        t = M.FusedMLPTrainer(batch=B, flat=flat, momentum=0.9)
+        t.load_shard(x, y)
+        for _ in range(30):
+            t.step()
+        torch.cuda.synchronize()
+        out.append((t.params.clone(), t.stats()))
+    assert _native.lib().sl_mlp_rows_bm(B) in (64, 256)
+    (p1, s1), (p2, s2) = out
+    assert bool(torch.isfinite(p1).all())
+    assert torch.equal(p1, p2)
+    assert s1.loss < 1.5, s1.loss
