@@ -102,12 +102,12 @@ __device__ __forceinline__ void bnb_fold(const BnBwdEpi& b, const BnbAcc& A, flo
     const int col = col0 + chunk * 8 + j;
     if (col >= C) continue;
     if (q == 0) {
-      atomicAdd(rep + col, acc);
-      if (rep2) atomicAdd(rep2 + col, acc);  // sum g is shared by both BNs
+      rsum_add(rep, col, acc);
+      if (rep2) rsum_add(rep2, col, acc);  // sum g is shared by both BNs
     } else if (q == 1) {
-      atomicAdd(rep + C + col, acc);
+      rsum_add(rep, C + col, acc);
     } else {
-      atomicAdd(rep2 + C + col, acc);
+      rsum_add(rep2, C + col, acc);
     }
   }
 }

@@ -197,8 +197,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     const int col = (qsel == 2 ? 0 : qsel == 3 ? 16 : qsel * 8) + j;
     float acc = 0.f;
     for (int r = 0; r < rpp; ++r) acc += part[r * tpr + g][col];
-    if (qsel < 2) atomicAdd(rep + qsel * C + c, acc);
-    else atomicAdd(rep2 + (qsel - 2) * C + c, acc);
+    if (qsel < 2) rsum_add(rep, qsel * C + c, acc);
+    else rsum_add(rep2, (qsel - 2) * C + c, acc);
   }
 }
 
@@ -552,6 +552,10 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const uint16_t* __rest
 }
 
 // ---------------------------------------------------------------------------
+#if SL_DETERMINISTIC
+__device__ unsigned long long g_dbias_fix[16];  // fixed-point bias-gradient accumulator (zero between launches)
+__device__ unsigned g_dbias_ticket;
+#endif
 // Softmax cross-entropy over fp32 logits [N][ncls] (ncls <= 16); one row per
 // 16-lane group.  dlogits (bf16, [N][ldd], zero beyond ncls) are scaled by
 // grad_scale; the bias gradient (sum over rows of dlogits) is folded per
@@ -597,8 +601,30 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict
   if (dbias && tid < ncls) {
     float acc = 0.f;
     for (int g2 = 0; g2 < 16; ++g2) acc += bsum[g2][tid];
+#if SL_DETERMINISTIC
+    atomicAdd(&g_dbias_fix[tid], (unsigned long long)__double2ll_rn((double)acc * SL_FIX_SCALE));
+#else
     atomicAdd(dbias + tid, acc);
+#endif
   }
+#if SL_DETERMINISTIC
+  // the last workgroup to finish adds the fixed-point total into dbias and resets the
+  // accumulator (all in wave 0: the fence covers every lane that added)
+  if (dbias) {
+    __shared__ int last;
+    if (tid == 0) {
+      __threadfence();
+      last = atomicAdd(&g_dbias_ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && tid < ncls) {
+      __threadfence();
+      const unsigned long long v = atomicExch(&g_dbias_fix[tid], 0ull);
+      dbias[tid] += (float)((double)(long long)v / SL_FIX_SCALE);
+    }
+    if (last && tid == 0) atomicExch(&g_dbias_ticket, 0u);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -609,6 +635,7 @@ extern "C" {
 
 long sl_rsum_floats(int n) { return rsum_floats(n); }
 long sl_rsum_result_offset(int n) { return (long)SL_REP * n; }
+int sl_deterministic() { return SL_DETERMINISTIC; }
 
 int sl_input_norm(const uint8_t* x, const uint8_t* lab, const int* cursor, int n_batches, int batch,
                   long img_pixels, uint16_t* y, uint8_t* lab_out, float m0, float m1, float m2, float s0, float s1,

@@ -106,8 +106,31 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 constexpr int SL_REP = 32;
 __host__ __device__ constexpr long rsum_floats(int n) { return (long)(SL_REP + 1) * n + 4; }
 
-__device__ __forceinline__ float* rsum_replica(float* buf, int n) { return buf + (long)(blockIdx.x % SL_REP) * n; }
+// Deterministic build (SL_DETERMINISTIC=1, libslkernels_det.so, loaded when the
+// SL_DETERMINISTIC env var is set): the float atomics' order varies from run to run, so
+// every cross-workgroup sum is instead a 64-bit fixed-point integer atomic (2^-32
+// resolution, |sum| < 2^31) into replica 0, read as int64[n].  Integer addition is
+// associative: the folded result is bit-identical for any workgroup order.
+#ifndef SL_DETERMINISTIC
+#define SL_DETERMINISTIC 0
+#endif
+constexpr double SL_FIX_SCALE = 4294967296.0;
+// launcher return code: a deterministic build needs a bigger split-K workspace for this call
+// (the python wrapper grows it and calls again; the other builds fall back to atomics)
+constexpr int SL_NEED_WS = 7;
+
+__device__ __forceinline__ float* rsum_replica(float* buf, int n) {
+  return SL_DETERMINISTIC ? buf : buf + (long)(blockIdx.x % SL_REP) * n;
+}
 __device__ __forceinline__ float* rsum_result(float* buf, int n) { return buf + (long)SL_REP * n; }
+// add v to entry i of a replica returned by rsum_replica
+__device__ __forceinline__ void rsum_add(float* rep, long i, float v) {
+#if SL_DETERMINISTIC
+  atomicAdd(reinterpret_cast<unsigned long long*>(rep) + i, (unsigned long long)__double2ll_rn((double)v * SL_FIX_SCALE));
+#else
+  atomicAdd(rep + i, v);
+#endif
+}
 
 }  // namespace sl
 

@@ -389,8 +389,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
       q += __shfl_xor(q, 32);
       const int col = n0 + wn * (BN / 2) + j * 16 + lr;
       if (lg == 0 && col < e.ncols) {
-        atomicAdd(rep + col, s);
-        atomicAdd(rep + e.ncols + col, q);
+        rsum_add(rep, col, s);
+        rsum_add(rep, e.ncols + col, q);
       }
     }
   }
@@ -645,8 +645,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
       q += __shfl_xor(q, 32);
       const int col = n0 + wn * 64 + j * 16 + lr;
       if (lg == 0 && col < e.ncols) {
-        atomicAdd(rep + col, s);
-        atomicAdd(rep + e.ncols + col, q);
+        rsum_add(rep, col, s);
+        rsum_add(rep, e.ncols + col, q);
       }
     }
   }
@@ -1294,12 +1294,16 @@ __global__ __launch_bounds__(64) void rsum_fold_kernel(float* buf, int n, float*
     i -= nb * 64;
   }
   if (i >= n) return;
+#if SL_DETERMINISTIC
+  const float acc = (float)((double)reinterpret_cast<const long long*>(buf)[i] / SL_FIX_SCALE);
+#else
   float v[SL_REP];
 #pragma unroll
   for (int r = 0; r < SL_REP; ++r) v[r] = buf[(long)r * n + i];
   float acc = 0.f;
 #pragma unroll
   for (int r = 0; r < SL_REP; ++r) acc += v[r];
+#endif
   rsum_result(buf, n)[i] = acc;
 }
 
@@ -1523,6 +1527,7 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
     a.steps_per_slice = (total_steps + slices - 1) / slices;
     a.slices = (total_steps + a.steps_per_slice - 1) / a.steps_per_slice;
     const bool slab = wgrad_use_slab(a, ws, ws_floats);
+    if (SL_DETERMINISTIC && a.slices > 1 && !slab) return SL_NEED_WS;  // no order-dependent atomics
     hipLaunchKernelGGL(conv_wgrad_big_kernel, dim3(tiles * a.slices), dim3(512), 0, stream, a);
     SL_CHECK_LAUNCH();
     return wgrad_finish(a, ws, ws_floats, stream, slab);
@@ -1541,6 +1546,7 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   a.slices = (total_steps + a.steps_per_slice - 1) / a.steps_per_slice;
   dim3 grid(tiles * a.slices);
   const bool slab = wgrad_use_slab(a, ws, ws_floats);
+  if (SL_DETERMINISTIC && a.slices > 1 && !slab) return SL_NEED_WS;
   if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3, 1>), grid, dim3(256), 0, stream, a);
   else if (SL_WGRAD128_KS == 2)
     hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_KS2_SLOTS, 2>), grid, dim3(512), 0, stream, a);

@@ -274,8 +274,8 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       q += __shfl_xor(q, 32);
       if (lg == 0) {
         float* rep = rsum_replica(a.stats, 2 * HC);
-        atomicAdd(rep + j * 16 + lr, s);
-        atomicAdd(rep + HC + j * 16 + lr, q);
+        rsum_add(rep, j * 16 + lr, s);
+        rsum_add(rep, HC + j * 16 + lr, q);
       }
     }
   }
@@ -603,6 +603,7 @@ int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, 
   const long need = (long)grid * 64 * 9 * HC;
   sl_wgrad_note_need(need);
   a.ws = (ws && need <= ws_floats && !((uintptr_t)ws & 15) && !((uintptr_t)dw & 15)) ? ws : nullptr;
+  if (SL_DETERMINISTIC && !a.ws) return SL_NEED_WS;  // no order-dependent atomics
   hipLaunchKernelGGL(conv3x3_wgrad_c64_kernel, dim3(grid), dim3(WNT), 0, stream, a);
   SL_CHECK_LAUNCH();
   if (a.ws) {

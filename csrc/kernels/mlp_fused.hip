@@ -2145,17 +2145,12 @@ int sl_mlp_set_rows_bm(int bm) {
 int sl_mlp_rows_bm(int batch) {
   if (g_rows_bm == 64 || (g_rows_bm == 128 && batch % 128 == 0) || (g_rows_bm == 256 && batch % 256 == 0))
     return g_rows_bm;
-  // 256 (one 8-wave workgroup per CU, half the weight stream per FLOP) once the batch
-  // fills every CU with such tiles: +2-4 % MLP over 64 at B = 65,536 in same-box A/B
-  // runs (profiles/r03_big).  Below that, 64 (two co-resident workgroups per CU overlap
-  // each other's epilogues) measured ahead of 128 at every batch size tried (r01_v7).
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-  }
-  if (batch % 256 == 0 && batch / 256 >= cus) return 256;
+  // 64 (two co-resident workgroups per CU overlap each other's epilogues) measured ahead
+  // of 128 at every batch size tried (r01_v7), and 2 % ahead of the 256-row tile in the
+  // in-process interleaved A/B at B = 65,536 (scripts/ab_mlp_inproc.py, profiles/r03_big:
+  // the 256-row tile spends fewer cycles per CU but loses them back at the clock and
+  // its serialized epilogues), so 256 stays opt-in (SL_MLP_ROWS_BM=256).
+  (void)batch;
   return 64;
 }
 

@@ -34,6 +34,9 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("SL_OFFLOAD_ARCH", "gfx950")
 
 KERNELS_SO = os.path.join(NATIVE_DIR, "libslkernels.so")
+# the same kernels built with -DSL_DETERMINISTIC=1 (fixed-point cross-workgroup sums, no
+# split-K atomics): loaded instead when the SL_DETERMINISTIC environment variable is 1
+KERNELS_DET_SO = os.path.join(NATIVE_DIR, "libslkernels_det.so")
 
 
 def _core_so_name() -> str:
@@ -65,18 +68,20 @@ def _hipcc() -> str:
     return p
 
 
-def build_kernels(force: bool = False, jobs: int = 8) -> str:
-    """Compile csrc/kernels/*.hip for gfx950 into one shared object."""
+def build_kernels(force: bool = False, jobs: int = 8, deterministic: bool = False) -> str:
+    """Compile csrc/kernels/*.hip for gfx950 into one shared object (``deterministic``:
+    the SL_DETERMINISTIC=1 build, :data:`KERNELS_DET_SO`)."""
     os.makedirs(NATIVE_DIR, exist_ok=True)
+    so_path = KERNELS_DET_SO if deterministic else KERNELS_SO
     srcs = sorted(glob.glob(os.path.join(KERNEL_DIR, "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(KERNEL_DIR, "*.h")))
-    if not force and not _stale(KERNELS_SO, srcs + hdrs):
-        return KERNELS_SO
-    objdir = os.path.join(ROOT, "build", "kernels")
+    if not force and not _stale(so_path, srcs + hdrs):
+        return so_path
+    objdir = os.path.join(ROOT, "build", "kernels_det" if deterministic else "kernels")
     os.makedirs(objdir, exist_ok=True)
     hipcc = _hipcc()
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I" + KERNEL_DIR,
-             "-munsafe-fp-atomics", "-Wno-unused-result"]
+             "-munsafe-fp-atomics", "-Wno-unused-result"] + (["-DSL_DETERMINISTIC=1"] if deterministic else [])
     objs = []
     procs = []
     for src in srcs:
@@ -92,10 +97,10 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
         if p.returncode != 0:
             sys.stderr.write(out)
             raise RuntimeError("hipcc failed on " + src)
-    tmp = KERNELS_SO + ".tmp"
+    tmp = so_path + ".tmp"
     _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", tmp])
-    os.replace(tmp, KERNELS_SO)
-    return KERNELS_SO
+    os.replace(tmp, so_path)
+    return so_path
 
 
 def build_core(force: bool = False) -> str:
@@ -126,6 +131,7 @@ def build_core(force: bool = False) -> str:
 
 def build_all(force: bool = False) -> None:
     build_kernels(force=force)
+    build_kernels(force=force, deterministic=True)
     build_core(force=force)
 
 
@@ -136,6 +142,7 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
     if args.only in (None, "kernels"):
         print(build_kernels(force=args.force))
+        print(build_kernels(force=args.force, deterministic=True))
     if args.only in (None, "core"):
         print(build_core(force=args.force))
     return 0

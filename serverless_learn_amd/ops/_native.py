@@ -17,7 +17,7 @@ import threading
 
 import torch
 
-from ..build import KERNELS_SO
+from ..build import KERNELS_DET_SO, KERNELS_SO
 
 _lock = threading.Lock()
 _lib = None
@@ -73,14 +73,15 @@ def lib():
         return _lib
     with _lock:
         if _lib is None:
-            path = os.environ.get("SL_KERNELS_SO") or KERNELS_SO  # override: A/B builds of the kernels
+            det = os.environ.get("SL_DETERMINISTIC", "0") == "1"  # bit-reproducible kernel build
+            path = os.environ.get("SL_KERNELS_SO") or (KERNELS_DET_SO if det else KERNELS_SO)  # override: A/B builds
             if not os.path.exists(path):
                 from ..build import build_kernels
 
-                build_kernels()
+                build_kernels(deterministic=det)
             handle = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
             for name in _SIGS:
-                if path != KERNELS_SO and not hasattr(handle, name):
+                if path not in (KERNELS_SO, KERNELS_DET_SO) and not hasattr(handle, name):
                     continue  # an A/B build of older kernels: only what it exports
                 _bind(handle, name)
             _lib = handle

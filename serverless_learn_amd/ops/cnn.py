@@ -139,6 +139,16 @@ def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None, bn
 _WGRAD_WGS = int(os.environ.get("SL_WGRAD_WGS", "768"))  # swept 512..2048, profiles/r01_v16
 
 
+NEED_WS = 7  # csrc/kernels/common.h SL_NEED_WS
+
+
+def deterministic() -> bool:
+    """True when the loaded kernel library is the deterministic build (fixed-point
+    cross-workgroup sums, no split-K atomics: bit-identical runs)."""
+    fn = getattr(N.lib(), "sl_deterministic", None)
+    return bool(fn and fn())
+
+
 class WgradWorkspace:
     """Slab for the weight gradient's split-K partials (plain stores + one ordered reduce
     launch instead of fp32 atomics into dw).  Sized by the launcher's own request: a call
@@ -162,9 +172,19 @@ def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: 
     n, h, wd, c = x.shape
     _, oh, ow, ldy = dy.shape
     assert dw.dtype == torch.float32 and dw.numel() >= cout * k * k * c
-    buf = ws.buf if ws is not None else None
-    N.call("sl_conv_wgrad", _bf16(x), n, h, wd, c, _bf16(dy), ldy, cout, k, k, stride, pad, oh, ow, p(dw),
-           int(target_wgs or _WGRAD_WGS), p(buf), int(buf.numel()) if buf is not None else 0, N.stream_ptr())
+    for attempt in range(2):
+        buf = ws.buf if ws is not None else None
+        rc = N.lib().sl_conv_wgrad(_bf16(x), n, h, wd, c, _bf16(dy), ldy, cout, k, k, stride, pad, oh, ow, p(dw),
+                                   int(target_wgs or _WGRAD_WGS), p(buf), int(buf.numel()) if buf is not None else 0,
+                                   N.stream_ptr())
+        # deterministic kernel build: no atomic split-K fallback, the workspace must fit (grown
+        # here, eagerly: a first step runs before any graph capture)
+        if rc == NEED_WS and ws is not None and attempt == 0 and not torch.cuda.is_current_stream_capturing():
+            ws.grow()
+            continue
+        if rc != 0:
+            raise RuntimeError(f"sl_conv_wgrad failed with code {rc}")
+        return
 
 
 class WtDesc(ctypes.Structure):

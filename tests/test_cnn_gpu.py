@@ -720,3 +720,23 @@ def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h, cin):
     if cin == 64:
         assert rel(dx - add.float(), dx_ref) < 2e-2
         assert rel(dx, outs[0][2]) < 5e-3
+
+
+def test_deterministic_build_is_bit_reproducible():
+    """SL_DETERMINISTIC=1 loads the deterministic kernel build (64-bit fixed-point
+    cross-workgroup sums, no split-K atomics): two fresh ResNet-18 engines give
+    bit-identical gradients and parameters after 3 training steps.  Runs in a child
+    process, since a process loads one kernel library."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SL_DETERMINISTIC="1")
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "resnet_det_check.py"), "64", "3"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["deterministic_build"] and r["finite"], r
+    assert r["grad_identical"] and r["params_identical"], r
