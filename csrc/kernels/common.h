@@ -10,10 +10,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short short8_t __attribute__((ext_vector_type(8)));
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
+typedef float floatx16_t __attribute__((ext_vector_type(16)));
 typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
 
 #define SL_LDS __attribute__((address_space(3)))
@@ -27,6 +30,24 @@ __device__ __forceinline__ floatx4_t mfma16(const short8_t& a, const short8_t& b
 __device__ __forceinline__ floatx4_t mfma16h(const short8_t& a, const short8_t& b, const floatx4_t& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b), c,
                                                 0, 0, 0);
+}
+
+// 32x32x16 forms: lane l holds A[row l&31][k 8(l>>5)+j], B[k 8(l>>5)+j][col l&31];
+// C/D: lane l, register r holds C[row (r&3) + 8(r>>2) + 4(l>>5)][col l&31]
+__device__ __forceinline__ floatx16_t mfma32(const short8_t& a, const short8_t& b, const floatx16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16((bf16x8_t)a, (bf16x8_t)b, c, 0, 0, 0);
+}
+__device__ __forceinline__ floatx16_t mfma32h(const short8_t& a, const short8_t& b, const floatx16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b), c,
+                                                0, 0, 0);
+}
+// compile-time loop: fn(std::integral_constant<int, I>) for I in [I0, I1)
+template <int I0, int I1, class Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  if constexpr (I0 < I1) {
+    fn(std::integral_constant<int, I0>{});
+    static_for<I0 + 1, I1>(fn);
+  }
 }
 
 // fp32 -> bf16 bits, round-to-nearest-even.  A plain cast lowers to the

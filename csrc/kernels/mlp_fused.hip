@@ -60,6 +60,9 @@ using namespace sl;
 #ifndef SL_WG_CVT
 #define SL_WG_CVT 1  // wgrad u8 B-fragment conversions scheduled under the MFMAs of the previous k-step
 #endif
+#ifndef SL_WG_MFMA32
+#define SL_WG_MFMA32 0  // weight gradient on v_mfma_f32_32x32x16 (4 x 1 tiles of 32 x 32 per wave) instead of 16x16x32
+#endif
 #ifndef SL_WG_PIPE
 #define SL_WG_PIPE 1  // software-pipelined wgrad main loop (0: the plain loop)
 #endif
@@ -1314,10 +1317,19 @@ template <bool U8> constexpr int wg_slot() { return U8 ? WG_SLOT8 : WG_SLOT; }
 // transposed fragment read (rows k..k+3 and k+8..k+11 per 32-lane half)
 // conflict-free; LDS-DMA writes the image linearly, so the same involution is
 // applied to the per-lane SOURCE address (cdna_hip_programming.md rule 21).
+// The 32x32x16 form's reads (SL_WG_MFMA32) cover 4 rows x 4 chunks per 32-lane half
+// (rows 8 (l >> 5) + q, columns of two 16-lane groups), on which that XOR leaves 2-way
+// bank conflicts: there chunk ^ ((r & 3) << 2) spreads the 16 (row, chunk) pairs of a half
+// over 16 distinct chunks, and the u8 image uses chunk ^ (((r >> 1) & 3) << 1).
+#if SL_WG_MFMA32
+__device__ __forceinline__ int wg_swz(int c, int r) { return c ^ ((r & 3) << 2); }
+__device__ __forceinline__ int wg_swz8(int c, int r) { return c ^ (((r >> 1) & 3) << 1); }
+#else
 __device__ __forceinline__ int wg_swz(int c, int r) { return c ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
 // u8 image: 128-B rows of 8 chunks; chunk ^ ((r >> 1) & 7) puts the 16 rows a
 // 32-lane half of ds_read_b64_tr_b8 touches on 16 distinct 4-bank groups.
 __device__ __forceinline__ int wg_swz8(int c, int r) { return c ^ ((r >> 1) & 7); }
+#endif
 
 // Transposed B-style fragment (8 consecutive k rows of one column) from a
 // swizzled image.  Issued as inline asm on purpose: hipcc treats a visible
@@ -1341,6 +1353,21 @@ __device__ __forceinline__ uint32_t wg_tr8_addr(int n0, int lane) {
   const int g = lane >> 4, q = (lane & 15) >> 1, p = lane & 1;
   const int r = 8 * g + q;
   return (uint32_t)(r * 128 + wg_swz8(n0 >> 4, r) * 16 + 8 * p);
+}
+// The same transposed reads for the 32x32x16 operand maps: lane l takes column
+// c0 + (l & 31) (16-lane group (l >> 4) & 1 holds columns 16..31) and rows 8 (l >> 5) ..
+// +7; the swizzles are unchanged, so k-substep s (16 rows) is a constant offset
+// (s * 4096 B in a bf16 image, s * 2048 B in a u8 image: f(r) and the u8 XOR ignore bit 4).
+__device__ __forceinline__ uint32_t wg_tr_addr32(int n0, int lane) {
+  const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int c = ((n0 + (G & 1) * 16) >> 3) + (p >> 1), w = (p & 1) * 4;
+  const int ra = 8 * (G >> 1) + q;
+  return (uint32_t)((ra * 128 + wg_swz(c, ra) * 8 + w) * 2);
+}
+__device__ __forceinline__ uint32_t wg_tr8_addr32(int n0, int lane) {
+  const int G = lane >> 4, q = (lane & 15) >> 1, p = lane & 1;
+  const int r = 8 * (G >> 1) + q;
+  return (uint32_t)(r * 128 + wg_swz8((n0 + (G & 1) * 16) >> 4, r) * 16 + 8 * p);
 }
 template <int OFF>
 __device__ __forceinline__ short4_t ds_tr16_off(uint32_t a) {
@@ -1379,6 +1406,12 @@ template <bool U8>
 __device__ __forceinline__ floatx4_t wg_mma(const short8_t& b, const short8_t& a, const floatx4_t& c) {
   if constexpr (U8) return mfma16h(b, a, c);
   else return mfma16(b, a, c);
+}
+
+template <bool U8>
+__device__ __forceinline__ floatx16_t wg_mma32(const short8_t& b, const short8_t& a, const floatx16_t& c) {
+  if constexpr (U8) return mfma32h(b, a, c);
+  else return mfma32(b, a, c);
 }
 
 // vmcnt needs an immediate: wait until this wave has at most N younger stages
@@ -1729,7 +1762,100 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   using I4 = std::integral_constant<int, WG_NJ>;  // all n-blocks live
   using I1 = std::integral_constant<int, 1>;
   using I0 = std::integral_constant<int, 0>;
-#if SL_WG_KO == 1  // timing knockout: no fragment reads / MFMAs
+#if SL_WG_MFMA32
+  // ---- 32x32x16 form: each wave's 128 (m) x 32 (n) output is 4 tiles of 32 x 32; a
+  // 64-row stage is 4 k-substeps of 16 x 4 MFMAs (16 per stage instead of 32) reading the
+  // same 16 A + 4 B fragments.  The next stage's 20 fragment reads are spread over the
+  // stage's 16 MFMAs (32-cycle gaps, profiles/r03_mfma). ----
+  floatx16_t acc32[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc32[i][r] = 0.f;
+  uint32_t a32[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wm * 128 + i * 32;
+    a32[i] = (r >> 7) * WG_IMG * 2 + wg_tr_addr32(r & 127, lane);
+  }
+  const uint32_t b32 = 2 * WG_IMG * 2 + (u8b ? wg_tr8_addr32(wn * 32, lane) : wg_tr_addr32(wn * 32, lane));
+  const int live32 = __builtin_amdgcn_readfirstlane(P.n_real - n0 - wn * 32 > 0 ? 1 : 0);
+  auto mainloop32 = [&](auto u8_c, auto nb_c) {
+    constexpr bool U8 = decltype(u8_c)::value;
+    constexpr int NB = decltype(nb_c)::value;
+    constexpr int PPS = U8 ? 5 : 6;
+    constexpr int NS = wg_ns<U8>(), SLOT = wg_slot<U8>();
+    short8_t fa[2][4][4];  // [set][k-substep][m-tile]
+    short8_t fb[2][4];     // bf16 B fragments [set][k-substep]
+    uint2v_t fr[2][4];     // raw u8 B fragments
+    // fragment f of a stage: 0..15 A (substep f / 4, m-tile f % 4), 16..19 B (substep f - 16)
+    auto read_frag = [&](uint32_t sb, auto f_c, auto set_c) {
+      constexpr int f = decltype(f_c)::value, S = decltype(set_c)::value;
+      if constexpr (f < 16) {
+        fa[S][f >> 2][f & 3] = wg_tr8<(f >> 2) * 4096>(sb + a32[f & 3]);
+      } else if constexpr (NB > 0) {
+        if constexpr (U8) fr[S][f - 16] = ds_tr8_off<(f - 16) * 2048>(sb + b32);
+        else fb[S][f - 16] = wg_tr8<(f - 16) * 4096>(sb + b32);
+      }
+    };
+    auto read_stage = [&](int st, auto set_c) {
+      const uint32_t sb = lds_base + (uint32_t)((st % NS) * SLOT * 2);
+      static_for<0, 20>([&](auto f_c) { read_frag(sb, f_c, set_c); });
+    };
+    auto step = [&](int st, auto cur_c, auto nxt_c) {
+      constexpr int C = decltype(cur_c)::value;
+      if (st + 1 < nst) {
+        wg_vmcnt<PPS>(min(NS - 2, nst - 2 - st));  // stage st+1 has landed (st+2 .. may be in flight)
+        __builtin_amdgcn_s_barrier();          // ... for everyone; every wave is done reading stage st
+        if (st + NS < nst) issue(st + NS, u8_c);
+      }
+      const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % NS) * SLOT * 2);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NB > 0) {
+        // u8 B fragments: substep s+1's conversion (4 v_perm) is issued behind substep s's
+        // first MFMA, so no MFMA waits on its own operand's conversion
+        short8_t bq[4];
+        if constexpr (U8) bq[0] = u8x8_f16_biased(fr[C][0]);
+        else bq[0] = fb[C][0];
+        static_for<0, 4>([&](auto s_c) {
+          constexpr int sub = decltype(s_c)::value;
+          static_for<0, 4>([&](auto i_c) {
+            constexpr int i = decltype(i_c)::value, q = 4 * sub + i;
+            acc32[i] = wg_mma32<U8>(bq[sub], fa[C][sub][i], acc32[i]);
+            if constexpr (i == 0 && sub + 1 < 4) {
+              if constexpr (U8) bq[sub + 1] = u8x8_f16_biased(fr[C][sub + 1]);
+              else bq[sub + 1] = fb[C][sub + 1];
+            }
+            constexpr int f0 = q * 20 / 16, f1 = (q + 1) * 20 / 16;
+            static_for<f0, f1>([&](auto f_c) { read_frag(sbn, f_c, nxt_c); });
+            if constexpr (f1 > f0) __builtin_amdgcn_sched_barrier(0);
+          });
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    wg_vmcnt<PPS>(min(NS - 2, nst - 1));
+    __builtin_amdgcn_s_barrier();
+    if (NS - 1 < nst) issue(NS - 1, u8_c);
+    read_stage(0, S0{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    for (int st = 0; st < nst; st += 2) {
+      step(st, S0{}, S1{});
+      if (st + 1 < nst) step(st + 1, S1{}, S0{});
+    }
+  };
+  if (u8b) {
+    if (live32) mainloop32(T_{}, I1{});
+    else mainloop32(T_{}, I0{});
+  } else {
+    mainloop32(F_{}, I1{});
+  }
+#elif SL_WG_KO == 1  // timing knockout: no fragment reads / MFMAs
   if (u8b) mainloop(T_{}, I0{});
   else mainloop(F_{}, I0{});
 #elif SL_WG_KO == 3  // timing knockout: no main loop (prologue sums + epilogue only)
@@ -1780,6 +1906,20 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   float* out = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096 + lane * 4;
 #else
   float* out = A.slab + (long)s * A.slab_stride + P.w_off;
+#endif
+#if SL_WG_MFMA32
+  // register r = 4 g + t of tile i: n = 8 g + 4 (lane >> 5) + t, m = 32 i + (lane & 31);
+  // store (i, g) is 1 KB of contiguous slab (sgd_tiled decodes the same order)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n = n0 + wn * 32 + 8 * g + 4 * (lane >> 5);
+      if (n < P.n_real)
+        *reinterpret_cast<floatx4_t*>(out + (i * 4 + g) * 256) =
+            floatx4_t{acc32[i][4 * g], acc32[i][4 * g + 1], acc32[i][4 * g + 2], acc32[i][4 * g + 3]};
+    }
+  if (false)
 #endif
 #pragma unroll
   for (int i = 0; i < WG_MI; ++i)
@@ -1943,8 +2083,13 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
     const int tile = (int)(off / TL_TILE), within = (int)(off % TL_TILE);
     const int wave = within >> 12, rem = within & 4095;
     const int ins = rem >> 8, lane = (rem & 255) >> 2;
+#if SL_WG_MFMA32  // store (tile i = ins / 4, register group g = ins % 4) of mlp_wgrad_kernel's 32x32x16 form
+    const int m = (wave & 1) * 128 + (ins >> 2) * 32 + (lane & 31);
+    const int nn = (wave >> 1) * 32 + (ins & 3) * 8 + (lane >> 5) * 4;
+#else
     const int m = (wave & 1) * 128 + (ins >> 1) * 16 + (lane & 15);
     const int nn = (wave >> 1) * 32 + (ins & 1) * 16 + (lane >> 4) * 4;
+#endif
     if (tile < 7) {
       const int n = tile * 128 + nn;
       if (n >= D_IN) return;  // dW1's last tile: 16 real columns (whole group exits together)
