@@ -95,12 +95,6 @@ using namespace sl;
 #ifndef SL_MLP_APF256
 #define SL_MLP_APF256 0  // A-fragment prefetch in the 256-row tile (64 more VGPRs)
 #endif
-#ifndef SL_DH1_WIDE
-#define SL_DH1_WIDE 0  // 256-row tile: dH1 stored as 16-B pieces after a permlane16 swap.  Off: the
-                       // gradients of one step are right, but training diverges non-deterministically
-                       // (NaN within 30 steps, scripts/check_mlp_det.py) even with s_nop around the
-                       // swap; the 8-B stores are exact and deterministic (profiles/r03_big)
-#endif
 #ifndef SL_MLP_RING256
 #define SL_MLP_RING256 2  // weight ring depth of the 256-row tile
 #endif
@@ -960,10 +954,11 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
     asm volatile("" : "+v"(mbo));
     const uint8_t* M1b = M1 + mbo;
     const auto dst = __builtin_amdgcn_make_buffer_rsrc(a.dh1 + (long)row0 * HID, 0, BM * HID * 2, 0x00020000);
-    // after the permlane16 swap of fragments (n, n+1) a lane holds 8 consecutive columns:
-    // fragment n + (lg & 1), columns 8 (lg >> 1) .. +7 (cdna_hip_programming.md T21)
-    const int voff = ((rw + lr) * HID + cw + (lg & 1) * 16 + (lg >> 1) * 8) * 2;
-    const int voff8 = ((rw + lr) * HID + cw + 4 * lg) * 2;  // 8-B form: this lane's own 4 columns
+    // 8-B stores of this lane's 4 columns per fragment.  A 16-B form (permlane16 swap of
+    // fragment pairs, cdna_hip_programming.md T21) gave exact one-step gradients but made
+    // multi-step training diverge non-deterministically, even with s_nop around the swap
+    // (profiles/r03_big); it was removed.
+    const int voff8 = ((rw + lr) * HID + cw + 4 * lg) * 2;
     const float sc = a.dh1_scale;
     uint32_t hv[NF][2];
     floatx4_t cs[MF / 4][NF];
@@ -985,32 +980,12 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
         hv[n][0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(vs[0], vs[1]));
         hv[n][1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(vs[2], vs[3]));
       }
-#if !SL_DH1_WIDE
 #pragma unroll
       for (int n = 0; n < NF; ++n) {
         typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
         const u32x2_t h = {hv[n][0], hv[n][1]};
         __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, 0);
       }
-#else
-#pragma unroll
-      for (int n = 0; n < NF; n += 2) {
-        typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-        u32x4_t o;
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          // inline asm with the 2 wait states the VALU write -> v_permlane read hazard
-          // needs: the builtin's codegen (ROCm 7.2) issued the swap right behind the
-          // v_cvt_pkrtz that wrote its operand and read stale lanes (non-deterministic
-          // dH1, training diverged in the bench while the small-batch tests passed)
-          uint32_t lo = hv[n][d], hi = hv[n + 1][d];
-          asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(lo), "+v"(hi));
-          o[d] = lo;
-          o[2 + d] = hi;
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(o, dst, voff, (m * 16 * HID + n * 16) * 2, 0);
-      }
-#endif
     }
     // Transpose-reduce of the 32 column partials over the 16 rows of a DPP row: each
     // stage pairs lane i with i^15, i^7, i^2, i^1 (row_mirror, row_half_mirror, quad
