@@ -14,19 +14,9 @@
 //   bn_bwd_apply    dx = a*dz + b*x + c
 //   maxpool / avgpool fwd+bwd, softmax cross-entropy (loss, correct, dlogits, dbias)
 #include "common.h"
+#include "bn_fwd.h"
 
 using namespace sl;
-
-__device__ __forceinline__ void unpack8(const short8_t& v, float (&f)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = bf2f((uint16_t)v[j]);
-}
-__device__ __forceinline__ short8_t pack8(const float (&f)[8]) {
-  short8_t v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(f[j]);
-  return v;
-}
 
 // Grid cap of the streaming BN apply kernels; SL_BN_APPLY_BLOCKS overrides it for A/B runs.
 static int bn_apply_cap() {
@@ -250,42 +240,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
 // coefficients once from the raw sums), and workgroup 0 publishes the
 // coefficients / running statistics / dgamma, dbeta.  Two fewer launches per
 // BatchNorm per direction (a 1-WG kernel costs ~4.5 us of serialised time).
-struct BnStats {
-  const float* stats;  // [2][C] sum, sum of squares (conv epilogue)
-  const float* gamma;
-  const float* beta;
-  float* coef;         // [4][C] out: scale, shift, mean, rstd (for backward)
-  float* run_mean;
-  float* run_var;
-};
-
-__device__ __forceinline__ void bn_coef8(const BnStats& b, int C, int c0, float count, float eps, float (&sc)[8],
-                                         float (&sh)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float mean = b.stats[c0 + j] / count;
-    const float var = fmaxf(b.stats[C + c0 + j] / count - mean * mean, 0.f);
-    sc[j] = b.gamma[c0 + j] * rsqrtf(var + eps);
-    sh[j] = b.beta[c0 + j] - mean * sc[j];
-  }
-}
-
-__device__ __forceinline__ void bn_publish(const BnStats& b, int C, float count, float eps, float momentum) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float mean = b.stats[c] / count;
-    const float var = fmaxf(b.stats[C + c] / count - mean * mean, 0.f);
-    const float rstd = rsqrtf(var + eps);
-    const float sc = b.gamma[c] * rstd;
-    b.coef[c] = sc;
-    b.coef[C + c] = b.beta[c] - mean * sc;
-    b.coef[2 * C + c] = mean;
-    b.coef[3 * C + c] = rstd;
-    if (b.run_mean) {
-      b.run_mean[c] = (1.f - momentum) * b.run_mean[c] + momentum * mean;
-      b.run_var[c] = (1.f - momentum) * b.run_var[c] + momentum * var * (count / fmaxf(count - 1.f, 1.f));
-    }
-  }
-}
+// BnStats, bn_coef8, bn_publish: bn_fwd.h
 
 // y = relu?(bn(x) + r), r = 0 | res | bn_r(res); grid stride is a multiple of C/8.
 __global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __restrict__ x, BnStats b,

@@ -27,6 +27,7 @@
 // all tiles of the workgroup and folded once through the replica buffers.
 #include "common.h"
 #include "bn_bwd_epi.h"
+#include "bn_fwd.h"
 
 #include <stdlib.h>
 
@@ -80,6 +81,11 @@ struct HaloArgs {
   float* stats;         // rsum buffer for 2*64 values (nullable)
   int tiles;
   BnBwdEpi bn;          // dgrad: ReLU mask + BN-backward sums of the output (bn.x null: off)
+  // forward, CIN = 64: src is a BN input x and the operand is relu(bn(x)), applied while the
+  // halo moves from registers to LDS (bin.stats null: off); workgroup 0 publishes the BN's
+  // coefficients and running statistics, as bn_apply_stats would have
+  BnStats bin;
+  float bin_count, bin_eps, bin_momentum;
 };
 
 template <int CIN>
@@ -104,8 +110,17 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
     *reinterpret_cast<uint4*>(Ws + (n * L::W_CH + c) * 16) = v;
   }
 
+  // BN-on-load: a thread's halo chunks are all channel chunk (tid & 7) (NTF % 8 == 0)
+  const bool bni = CIN == 64 && a.bin.stats != nullptr;
+  float isc[8], ish[8];
+  if (bni) {
+    bn_coef8(a.bin, HC, (tid & 7) * 8, a.bin_count, a.bin_eps, isc, ish);
+    if (blockIdx.x == 0) bn_publish(a.bin, HC, a.bin_count, a.bin_eps, a.bin_momentum);
+  }
+
   // ---- halo tile: global -> registers (prefetch) -> LDS ----
   uint4 hv[HL];
+  unsigned hok = 0;  // bit i: chunk i is inside the image (zero padding stays zero under BN-on-load)
   auto halo_load = [&](int tile) {
     const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
 #pragma unroll
@@ -117,6 +132,8 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       const bool ok = q < L::HALO_CHUNKS && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW;
       hv[i] = ok ? *reinterpret_cast<const uint4*>(a.src + (((long)img * a.H + ih) * IW + iw) * CIN + c * 8)
                  : make_uint4(0, 0, 0, 0);
+      if (i == 0) hok = 0;
+      hok |= (unsigned)ok << i;
     }
   };
   auto halo_store = [&]() {
@@ -124,7 +141,9 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
     for (int i = 0; i < HL; ++i) {
       const int q = tid + i * NTF;
       const int pix = q / L::DCH, c = q - pix * L::DCH;
-      if (q < L::HALO_CHUNKS) *reinterpret_cast<uint4*>(Hs + (pix * L::PIX_CH + c) * 16) = hv[i];
+      uint4 v = hv[i];
+      if (bni && ((hok >> i) & 1u)) v = bn_relu_chunk(v, isc, ish);
+      if (q < L::HALO_CHUNKS) *reinterpret_cast<uint4*>(Hs + (pix * L::PIX_CH + c) * 16) = v;
     }
   };
 
@@ -311,8 +330,9 @@ int sl_conv3x3_c64_applicable(int H, int W, int C, int cout, int KH, int KW, int
 // cin: 64 (forward or, with flip, data gradient) or 8 (forward only).
 // bn (nullable; dgrad only, ldy == 64): the output is stored ReLU-masked and its BatchNorm's
 // backward sums are accumulated (bn_bwd_epi.h).
-int sl_conv3x3_c64_bn(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
-                      const uint16_t* add, float* stats, const BnBwdEpi* bn, hipStream_t stream) {
+static int conv3x3_launch(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y,
+                          int ldy, const uint16_t* add, float* stats, const BnBwdEpi* bn, const BnStats* bin,
+                          float bin_count, float bin_eps, float bin_momentum, hipStream_t stream) {
   if (N <= 0 || H <= 0 || H % TR || ldy < HC || (ldy & 7) || !y || (cin != 64 && cin != 8) || (cin == 8 && flip))
     return -1;
   if (bn && (ldy != HC || stats || bn->x2)) return -2;  // no second BN here (register budget)
@@ -328,6 +348,12 @@ int sl_conv3x3_c64_bn(const uint16_t* src, const uint16_t* w, int cin, int flip,
   a.tiles = N * (H / TR);
   a.bn = BnBwdEpi{};
   if (bn) a.bn = *bn;
+  a.bin = BnStats{};
+  a.bin_count = bin_count; a.bin_eps = bin_eps; a.bin_momentum = bin_momentum;
+  if (bin) {
+    if (cin != 64 || flip || !bin->stats || !bin->gamma || !bin->beta || !bin->coef || bin_count <= 0.f) return -4;
+    a.bin = *bin;
+  }
   const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;  // persistent: one workgroup per CU (130 KB LDS)
   if (cin == 64) hipLaunchKernelGGL(conv3x3_kernel<64>, dim3(grid), dim3(NTF), 0, stream, a);
   else hipLaunchKernelGGL(conv3x3_kernel<8>, dim3(grid), dim3(NTF), 0, stream, a);
@@ -335,9 +361,30 @@ int sl_conv3x3_c64_bn(const uint16_t* src, const uint16_t* w, int cin, int flip,
   return 0;
 }
 
+int sl_conv3x3_c64_bn(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
+                      const uint16_t* add, float* stats, const BnBwdEpi* bn, hipStream_t stream) {
+  return conv3x3_launch(src, w, cin, flip, N, H, y, ldy, add, stats, bn, nullptr, 0.f, 0.f, 0.f, stream);
+}
+
 int sl_conv3x3_c64(const uint16_t* src, const uint16_t* w, int cin, int flip, int N, int H, uint16_t* y, int ldy,
                    const uint16_t* add, float* stats, hipStream_t stream) {
   return sl_conv3x3_c64_bn(src, w, cin, flip, N, H, y, ldy, add, stats, nullptr, stream);
+}
+
+int sl_rsum_fold(float* buf, int n, hipStream_t stream);
+
+// Forward 64 -> 64 conv of relu(bn(x)) straight from the BN input x: the BN's folded sums
+// (bstats), gamma / beta give the per-channel scale / shift, applied to each halo chunk
+// between its load and the LDS store; workgroup 0 writes the BN's coef / running stats.
+// Replaces bn_apply_stats + sl_conv3x3_c64 for a conv whose input feeds nothing else
+// in the forward (a basic block's conv2).  ``stats``: the output BN's rsum buffer.
+int sl_conv3x3_bnin_fwd(const uint16_t* x, const uint16_t* w, int N, int H, uint16_t* y, int ldy, float* stats,
+                        const float* bstats, const float* gamma, const float* beta, float* coef, float* run_mean,
+                        float* run_var, float count, float eps, float momentum, hipStream_t stream) {
+  const BnStats bin{bstats, gamma, beta, coef, run_mean, run_var};
+  const int rc = conv3x3_launch(x, w, 64, 0, N, H, y, ldy, nullptr, stats, nullptr, &bin, count, eps, momentum, stream);
+  if (rc || !stats) return rc;
+  return sl_rsum_fold(stats, 2 * HC, stream);  // as sl_conv_fwd does after its epilogue sums
 }
 
 }  // extern "C"
@@ -373,6 +420,8 @@ struct WgradHaloArgs {
   int N, H, tiles;
   float* dw;           // [64][9][64] fp32, accumulated
   float* ws;           // non-null: [gridDim.x][64][9][64] partials, summed by sl_wgrad_slab_reduce
+  BnStats bin;         // bin.stats non-null: the X operand is relu(bn(x)), applied on load
+  float bin_count, bin_eps;
 };
 
 template <int OFF>
@@ -487,10 +536,16 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
   const int cb = wave & 3, th = wave >> 2;
   const int lg = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   const int tiles_per_img = a.H / TR;
+  // BN-on-load of X: a thread's X chunks are all channel chunk (tid & 7) (WNT % 8 == 0)
+  const bool bni = a.bin.stats != nullptr;
+  float isc[8], ish[8];
+  if (bni) bn_coef8(a.bin, HC, (tid & 7) * 8, a.bin_count, a.bin_eps, isc, ish);
 
   uint4 pv[WLOADS];
-  auto tile_load = [&](int tile) {
+  unsigned xok = 0;  // bit i: chunk i is an X chunk inside the image
+  auto tile_load = [&](int tile) __attribute__((always_inline)) {
     const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
+    xok = 0;
 #pragma unroll
     for (int i = 0; i < WLOADS; ++i) {
       const int c = tid + i * WNT;
@@ -499,8 +554,10 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
         const int pix = c >> 3, ch = c & 7;
         const int hr = pix / HCOL, hc = pix - hr * HCOL;
         const int ih = r0 - 1 + hr, iw = hc - 1;
-        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW)
+        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW) {
           v = *reinterpret_cast<const uint4*>(a.x + (((long)img * a.H + ih) * IW + iw) * HC + ch * 8);
+          xok |= 1u << i;
+        }
       } else if (c < WX_CHUNKS + WY_CHUNKS) {
         const int cc = c - WX_CHUNKS, pix = cc >> 3, ch = cc & 7;
         v = *reinterpret_cast<const uint4*>(a.dy + ((long)tile * TPIX + pix) * a.ldy + ch * 8);
@@ -508,12 +565,14 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
       pv[i] = v;
     }
   };
-  auto tile_store = [&]() {
+  auto tile_store = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < WLOADS; ++i) {
       const int c = tid + i * WNT;
       if (c < WX_CHUNKS) {
-        *reinterpret_cast<uint4*>(Xs + (c >> 3) * WPS + (c & 7) * 16) = pv[i];
+        uint4 v = pv[i];
+        if (bni && ((xok >> i) & 1u)) v = bn_relu_chunk(v, isc, ish);
+        *reinterpret_cast<uint4*>(Xs + (c >> 3) * WPS + (c & 7) * 16) = v;
       } else if (c < WX_CHUNKS + WY_CHUNKS) {
         const int cc = c - WX_CHUNKS;
         *reinterpret_cast<uint4*>(Ys + (cc >> 3) * WPS + (cc & 7) * 16) = pv[i];
@@ -532,7 +591,7 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
     for (int t = 0; t < 5; ++t) acc[i][t] = zero4();
 
   // The tile loop is instantiated per tap half and selected by a scalar branch outside it.
-  auto run = [&](auto t0_c) {
+  auto run = [&](auto t0_c) __attribute__((always_inline)) {
     constexpr int T0 = decltype(t0_c)::value, NTAP = T0 == 0 ? 5 : 4;
     int tile = blockIdx.x;
     if (tile < a.tiles) tile_load(tile);
@@ -584,9 +643,11 @@ int sl_conv3x3_wgrad_c64_applicable(int H, int W, int C, int cout, int KH, int K
 int sl_wgrad_slab_reduce(const float* ws, int slices, long n, float* dw, hipStream_t stream);
 void sl_wgrad_note_need(long floats);
 
-int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, float* ws,
-                         long ws_floats, hipStream_t stream) {
+static int conv3x3_wgrad_launch(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, float* ws,
+                                long ws_floats, const BnStats* bin, float bin_count, float bin_eps,
+                                hipStream_t stream) {
   if (N <= 0 || H <= 0 || H % TR || ldy != HC || !dw) return -1;
+  if (bin && (!bin->stats || !bin->gamma || !bin->beta || bin_count <= 0.f)) return -4;
   if ((((uintptr_t)x) | ((uintptr_t)dy)) & 15) return -3;
   if (g_num_cus <= 0) {
     int dev = 0;
@@ -597,6 +658,8 @@ int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, 
   WgradHaloArgs a;
   a.x = x; a.dy = dy; a.ldy = ldy; a.N = N; a.H = H; a.dw = dw;
   a.tiles = N * (H / TR);
+  a.bin = bin ? *bin : BnStats{};
+  a.bin_count = bin_count; a.bin_eps = bin_eps;
   const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;
   // each persistent workgroup's partial dW: a slab + one ordered reduce (plain stores) rather
   // than 36,864 fp32 atomics per workgroup at the chip-wide atomic rate
@@ -613,6 +676,20 @@ int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, 
     SL_CHECK_LAUNCH();
   }
   return 0;
+}
+
+int sl_conv3x3_wgrad_c64(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, float* ws,
+                         long ws_floats, hipStream_t stream) {
+  return conv3x3_wgrad_launch(x, dy, ldy, N, H, dw, ws, ws_floats, nullptr, 0.f, 0.f, stream);
+}
+
+// Weight gradient of the conv fed by sl_conv3x3_bnin_fwd: X = relu(bn(x)) rebuilt on load
+// from the BN input x and the BN's folded sums (the same bf16 values the forward used).
+int sl_conv3x3_bnin_wgrad(const uint16_t* x, const uint16_t* dy, int N, int H, float* dw, float* ws, long ws_floats,
+                          const float* bstats, const float* gamma, const float* beta, float count, float eps,
+                          hipStream_t stream) {
+  const BnStats bin{bstats, gamma, beta, nullptr, nullptr, nullptr};
+  return conv3x3_wgrad_launch(x, dy, HC, N, H, dw, ws, ws_floats, &bin, count, eps, stream);
 }
 
 }  // extern "C"

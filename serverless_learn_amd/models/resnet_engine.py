@@ -9,8 +9,9 @@ cursor, like the MLP engine).
 
 Per step:
   forward   input_norm -> [conv (+BN stats in the epilogue) -> bn_apply with
-            the finalize folded in (+residual, ReLU)] x 20 -> avgpool -> fc -> 
-            softmax-CE (loss, dlogits, dbias)
+            the finalize folded in (+residual, ReLU)] x 20 -> avgpool -> fc ->
+            softmax-CE (loss, dlogits, dbias); a 64-channel block's conv2 applies
+            relu(bn1(.)) while loading c1 instead (BN-on-load, no a1 pass)
   backward  per block, in reverse: bn_bwd_apply (ReLU mask fused), conv wgrad
             (split-K partials in a slab + one ordered reduce into the flat
             gradient) and dgrad, whose epilogue adds the residual gradient,
@@ -89,6 +90,10 @@ class FusedResNetTrainer:
         self.grad_scale = 1.0 / (batch * world_size)
         self.bn_momentum = bn_momentum
         self.shortcut_even_on = os.environ.get("SL_SHORTCUT_EVEN", "1") != "0"
+        # BN-on-load: where the direct 3x3 kernel serves a block's conv2 (64 channels, 32 wide), it
+        # reads relu(bn1(c1)) straight from c1 -- forward and weight gradient -- and a1 is never
+        # written (SL_BN_ONLOAD=0: bn_apply_stats + a1, as before)
+        self.bn_onload = os.environ.get("SL_BN_ONLOAD", "1") != "0"
         n = spec.n_flat
         self.params = torch.zeros(n, dtype=torch.float32, device=dev)
         self.params.copy_((flat if flat is not None else init_params(spec, seed)).to(dev))
@@ -145,6 +150,8 @@ class FusedResNetTrainer:
                 if not self._shortcut_even(blk):  # else the shortcut gradient goes straight into dx
                     st["dxs"] = torch.empty_like(cur)
             st["dx"] = torch.empty_like(cur)
+            c2s = blk.conv2
+            st["bnin"] = self.bn_onload and K.conv3x3_bnin_applicable(shp, c2s.cout, c2s.k, c2s.stride, c2s.pad)
             self.blocks.append(st)
             cur = st["y"]
         self.feat_in = cur
@@ -233,8 +240,12 @@ class FusedResNetTrainer:
             b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
             self._conv_bn(st["x"], self.conv[blk.conv1.name], b1, st["c1"])
             cnt = st["c1"].numel() // blk.conv1.cout
-            K.bn_apply_stats(st["c1"], b1, st["a1"], cnt, momentum=self.bn_momentum)
-            self._conv_bn(st["a1"], self.conv[blk.conv2.name], b2, st["c2"])
+            if st["bnin"]:
+                K.conv3x3_bnin_fwd(st["c1"], self.conv[blk.conv2.name].w, b1, cnt, st["c2"], stats=b2.stats_buf,
+                                   momentum=self.bn_momentum)
+            else:
+                K.bn_apply_stats(st["c1"], b1, st["a1"], cnt, momentum=self.bn_momentum)
+                self._conv_bn(st["a1"], self.conv[blk.conv2.name], b2, st["c2"])
             if blk.down is not None:
                 bd = self.bn[blk.dbn.name]
                 self._conv_bn(st["x"], self.conv[blk.down.name], bd, st["cs"])
@@ -320,7 +331,10 @@ class FusedResNetTrainer:
                     add = st["dxs"]
             else:
                 K.bn_bwd_apply_sums(st["dz"], None, st["c2"], b2.sums, b2.coef, b2.ggamma, b2.gbeta, st["dc2"])
-            K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g, ws=self.wgws)
+            if st["bnin"]:
+                K.conv3x3_bnin_wgrad(st["c1"], st["dc2"], b1, st["c1"].numel() // blk.conv1.cout, c2.g, ws=self.wgws)
+            else:
+                K.conv_wgrad(st["a1"], st["dc2"], blk.conv2.cout, 3, 1, 1, c2.g, ws=self.wgws)
             # a1 = relu(bn1(c1)): the mask is re-derived from c1 and bn1's coefficients
             bn1 = dict(x=st["c1"], sums=b1.sums_buf, mask_coef=b1.coef)
             if fuse:

@@ -42,6 +42,9 @@ N.register("sl_maxpool_bwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_avgpool_fwd", [P, P, I, I, I, P])
 N.register("sl_avgpool_bwd", [P, P, I, I, I, P])
 N.register("sl_softmax_ce", [P, P, P, P, P, I, P, I, I, F, P])
+N.register("sl_conv3x3_c64_applicable", [I, I, I, I, I, I, I, I, I])
+N.register("sl_conv3x3_bnin_fwd", [P, P, I, I, P, I, P, P, P, P, P, P, P, F, F, F, P])
+N.register("sl_conv3x3_bnin_wgrad", [P, P, I, I, P, P, L, P, P, P, F, F, P])
 
 p = N.ptr
 
@@ -184,6 +187,44 @@ def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: 
             continue
         if rc != 0:
             raise RuntimeError(f"sl_conv_wgrad failed with code {rc}")
+        return
+
+
+def conv3x3_bnin_applicable(x_shape, cout: int, k: int, stride: int, pad: int) -> bool:
+    """Whether :func:`conv3x3_bnin_fwd` / :func:`conv3x3_bnin_wgrad` serve this convolution of a
+    BN output: the direct 3x3 kernel's 64 -> 64 / stride-1 / 32-wide case (csrc/kernels/conv3x3_halo.hip)."""
+    n, h, w, c = x_shape
+    return (c == 64 and cout == 64 and k == 3 and stride == 1 and pad == 1
+            and bool(N.lib().sl_conv3x3_c64_applicable(h, w, c, cout, 3, 3, 1, 1, c)))
+
+
+def conv3x3_bnin_fwd(x, w, bn, count: int, y, stats=None, eps: float = 1e-5, momentum: float = 0.1):
+    """y = conv3x3(relu(bn(x))) with the BatchNorm applied to each input chunk between its load and
+    the LDS store: bn_apply_stats's output is never written or read back.  ``bn`` exposes stats
+    (folded sums), gamma, beta, coef, run_mean, run_var; the kernel publishes coef and the running
+    statistics as :func:`bn_apply_stats` would.  ``stats``: the output BN's rsum buffer (folded here)."""
+    n, h, wd, c = x.shape
+    assert y.shape[:3] == (n, h, wd) and y.is_contiguous()
+    N.call("sl_conv3x3_bnin_fwd", _bf16(x), _bf16(w), n, h, _bf16(y), int(y.shape[3]), _f32(stats), _f32(bn.stats),
+           _f32(bn.gamma), _f32(bn.beta), _f32(bn.coef), _f32(bn.run_mean), _f32(bn.run_var), float(count),
+           float(eps), float(momentum), N.stream_ptr())
+
+
+def conv3x3_bnin_wgrad(x, dy, bn, count: int, dw, ws=None, eps: float = 1e-5):
+    """dw += weight gradient of the convolution fed by :func:`conv3x3_bnin_fwd`: the operand
+    relu(bn(x)) is rebuilt on load from the BN input ``x`` (same bf16 values as the forward)."""
+    n, h, wd, c = x.shape
+    assert dy.shape == (n, h, wd, 64) and dw.dtype == torch.float32 and dw.numel() >= 64 * 9 * 64
+    for attempt in range(2):
+        buf = ws.buf if ws is not None else None
+        rc = N.lib().sl_conv3x3_bnin_wgrad(_bf16(x), _bf16(dy), n, h, p(dw), p(buf),
+                                           int(buf.numel()) if buf is not None else 0, _f32(bn.stats),
+                                           _f32(bn.gamma), _f32(bn.beta), float(count), float(eps), N.stream_ptr())
+        if rc == NEED_WS and ws is not None and attempt == 0 and not torch.cuda.is_current_stream_capturing():
+            ws.grow()
+            continue
+        if rc != 0:
+            raise RuntimeError(f"sl_conv3x3_bnin_wgrad failed with code {rc}")
         return
 
 

@@ -740,3 +740,93 @@ def test_deterministic_build_is_bit_reproducible():
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["deterministic_build"] and r["finite"], r
     assert r["grad_identical"] and r["params_identical"], r
+
+
+class _BnObj:
+    """The attribute bundle the BN launchers read (stats, gamma, beta, coef, run_mean, run_var)."""
+
+    def __init__(self, x, seed):
+        c = x.shape[-1]
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        xf = x.float().reshape(-1, c)
+        self.stats = torch.stack([xf.sum(0), (xf * xf).sum(0)]).reshape(-1).contiguous()
+        self.gamma = (torch.rand(c, generator=g) + 0.5).to(DEV)
+        self.beta = torch.randn(c, generator=g).to(DEV)
+        self.coef = torch.zeros(4 * c, device=DEV)
+        self.run_mean, self.run_var = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+
+
+@pytest.mark.parametrize("n,h", [(3, 32), (16, 8)])
+def test_conv3x3_bn_on_load_matches_materialised_operand(n, h):
+    """BN-on-load (csrc/kernels/conv3x3_halo.hip bin): conv3x3(relu(bn(x))) computed from the BN
+    input x is bit-identical to bn_apply_stats + conv on the stored operand -- forward output,
+    published coef / running statistics, and the weight gradient -- and matches an fp32
+    PyTorch reference of the whole op."""
+    from serverless_learn_amd.ops import cnn as K
+
+    torch.manual_seed(11)
+    c = 64
+    x = bf(torch.randn(n, h, 32, c, device=DEV) * 1.5 + 0.3)
+    w = bf(torch.randn(c, 3, 3, c, device=DEV) / 24)
+    assert K.conv3x3_bnin_applicable(x.shape, c, 3, 1, 1)
+    cnt = n * h * 32
+    # reference path: a = relu(bn(x)) stored, then the conv
+    b0 = _BnObj(x, 5)
+    a = torch.empty_like(x)
+    K.bn_apply_stats(x, b0, a, cnt)
+    y0 = torch.empty_like(x)
+    s0 = torch.zeros(K.rsum_floats(2 * c), device=DEV)
+    K.conv_fwd(a, w, c, 3, 1, 1, y=y0, stats=s0)
+    # on-load path
+    b1 = _BnObj(x, 5)
+    y1 = torch.empty_like(x)
+    s1 = torch.zeros(K.rsum_floats(2 * c), device=DEV)
+    K.conv3x3_bnin_fwd(x, w, b1, cnt, y1, stats=s1)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert torch.equal(b0.coef, b1.coef) and torch.equal(b0.run_mean, b1.run_mean)
+    # the running variance may differ in the last ulp: the two translation units contract its
+    # multiply-adds differently
+    assert torch.allclose(b0.run_var, b1.run_var, rtol=1e-6, atol=0)
+    assert torch.allclose(K.rsum_result(s0, 2 * c), K.rsum_result(s1, 2 * c), rtol=1e-4, atol=1e-2)
+    # fp32 reference of the whole op
+    xr = x.float().permute(0, 3, 1, 2)
+    ar = F.relu(F.batch_norm(xr, None, None, b0.gamma, b0.beta, training=True, eps=1e-5))
+    ref = F.conv2d(ar, w.float().permute(0, 3, 1, 2), padding=1)
+    assert rel(y1.float().permute(0, 3, 1, 2), ref) < 1e-2
+    # weight gradient from x vs from the stored operand
+    dy = bf(torch.randn_like(y1.float()))
+    ws = K.WgradWorkspace(DEV)
+    dw0 = torch.zeros(c * 9 * c, device=DEV)
+    K.conv_wgrad(a, dy, c, 3, 1, 1, dw0, ws=ws)
+    ws.grow()
+    dw0.zero_()
+    K.conv_wgrad(a, dy, c, 3, 1, 1, dw0, ws=ws)
+    dw1 = torch.zeros(c * 9 * c, device=DEV)
+    K.conv3x3_bnin_wgrad(x, dy, b1, cnt, dw1, ws=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(dw0, dw1)
+    dref = torch.nn.grad.conv2d_weight(ar, (c, c, 3, 3), dy.float().permute(0, 3, 1, 2), padding=1)
+    assert rel(dw1.view(c, 3, 3, c).permute(0, 3, 1, 2), dref) < 1e-2
+
+
+def test_resnet_engine_bn_on_load_is_bit_identical_in_deterministic_build():
+    """Whole engine, deterministic kernel build: 3 training steps with BN-on-load (default) and
+    with SL_BN_ONLOAD=0 (bn_apply_stats + stored a1) give bit-identical parameters."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = os.path.join(root, "scripts", "resnet_onload_check.py")
+    res = {}
+    for v in ("1", "0"):
+        env = dict(os.environ, SL_DETERMINISTIC="1", SL_BN_ONLOAD=v)
+        out = subprocess.run([sys.executable, script, "64", "3"], env=env, capture_output=True, text=True,
+                             timeout=240)
+        assert out.returncode == 0, out.stderr[-2000:]
+        res[v] = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["1"]["bnin_blocks"] == 2 and res["0"]["bnin_blocks"] == 0, res
+    assert res["1"]["deterministic_build"] and res["1"]["finite"], res
+    assert res["1"]["param_hash"] == res["0"]["param_hash"], res
