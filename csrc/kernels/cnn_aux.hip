@@ -242,7 +242,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
 // BatchNorm per direction (a 1-WG kernel costs ~4.5 us of serialised time).
 // BnStats, bn_coef8, bn_publish: bn_fwd.h
 
-// y = relu?(bn(x) + r), r = 0 | res | bn_r(res); grid stride is a multiple of C/8.
+// y = relu?(bn(x) + r), r = 0 | res | bn_r(res) | relu(bn_r(res)) (modes 0-3); grid stride is a
+// multiple of C/8.
 __global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __restrict__ x, BnStats b,
                                                              const uint16_t* __restrict__ res, BnStats rb,
                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ mask_out,
@@ -254,13 +255,20 @@ __global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __r
   const int c0 = (int)(t0 % cpr) * 8;
   float sc[8], sh[8], rsc[8], rsh[8];
   bn_coef8(b, C, c0, count, eps, sc, sh);
-  if (mode == 2) bn_coef8(rb, C, c0, count, eps, rsc, rsh);
+  if (mode >= 2) bn_coef8(rb, C, c0, count, eps, rsc, rsh);
   for (long q = t0; q < total; q += (long)gridDim.x * blockDim.x) {
     float f[8];
     unpack8(ld8(x + q * 8), f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
-    if (mode) {
+    if (mode == 3) {
+      // residual = relu(bn_r(res)) rounded to bf16: the stored tensor it replaces (BN-on-load)
+      float r[8];
+      const uint4 rv = bn_relu_chunk(*reinterpret_cast<const uint4*>(res + q * 8), rsc, rsh);
+      unpack8(__builtin_bit_cast(short8_t, rv), r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += r[j];
+    } else if (mode) {
       float r[8];
       unpack8(ld8(res + q * 8), r);
 #pragma unroll
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __r
   }
   if (blockIdx.x == 0) {
     bn_publish(b, C, count, eps, momentum);
-    if (mode == 2) bn_publish(rb, C, count, eps, momentum);
+    if (mode == 2) bn_publish(rb, C, count, eps, momentum);  // mode 3: published by the BN-on-load conv
   }
 }
 
@@ -679,7 +687,8 @@ int sl_bn_apply_stats(const uint16_t* x, const float* stats, const float* gamma,
                       hipStream_t stream) {
   if ((C & 7) || 256 % (C / 8) != 0) return -1;
   if (mode && !res) return -2;
-  if (mode == 2 && !rstats) return -2;
+  if (mode >= 2 && !rstats) return -2;
+  if (mode > 3) return -1;
   BnStats b{stats, gamma, beta, coef, run_mean, run_var};
   BnStats rb{rstats, rgamma, rbeta, rcoef, rrun_mean, rrun_var};
   hipLaunchKernelGGL(bn_apply_stats_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0, stream, x, b, res, rb, y,

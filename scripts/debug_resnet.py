@@ -36,6 +36,8 @@ xi = normalize_input(torch.from_numpy(x).to(DEV))
 c0 = conv(xi, spec.stem_conv)
 print("stem conv out", rel(tr.c0, nhwc(c0)))
 a = F.relu(bn(c0, spec.stem_bn))
+if tr.stem_onload:  # a0 is rebuilt on load from c0 by the engine, never stored: materialise it
+    tr.K.bn_apply(tr.c0, tr.bn[spec.stem_bn.name].coef, tr.a0, relu=True)
 print("stem act", rel(tr.a0, nhwc(a)))
 outs = []
 for i, (st, blk) in enumerate(zip(tr.blocks, spec.blocks)):

@@ -26,6 +26,6 @@ for _ in range(steps):
 torch.cuda.synchronize()
 p = tr.get_flat().cpu()
 print(json.dumps({"deterministic_build": K.deterministic(), "bn_onload": tr.bn_onload,
-                  "bnin_blocks": sum(bool(st["bnin"]) for st in tr.blocks), "batch": batch, "steps": steps,
+                  "bnin_blocks": sum(bool(st["bnin"]) for st in tr.blocks), "stem_onload": tr.stem_onload, "batch": batch, "steps": steps,
                   "param_hash": hashlib.sha256(p.numpy().tobytes()).hexdigest()[:16], "loss": tr.stats().loss,
                   "finite": bool(torch.isfinite(p).all())}))

@@ -155,6 +155,12 @@ class FusedResNetTrainer:
             self.blocks.append(st)
             cur = st["y"]
         self.feat_in = cur
+        # stem BN-on-load: with an identity first block, a0 = relu(bn0(c0)) feeds only block 0's
+        # conv1 (forward, weight gradient) and its residual; both rebuild it from c0
+        b0 = self.blocks[0]
+        c1s = b0["spec"].conv1
+        self.stem_onload = (self.bn_onload and spec.stem != "imagenet" and b0["spec"].down is None
+                            and K.conv3x3_bnin_applicable(self.c0.shape, c1s.cout, c1s.k, c1s.stride, c1s.pad))
         self.feat = torch.empty(B, 1, 1, 512, **bf)
         self.dfeat = torch.empty_like(self.feat)
         self.dfeat_in = torch.empty_like(cur)
@@ -232,13 +238,20 @@ class FusedResNetTrainer:
         K.input_norm(self.x, self.y, self.cursor, self.batch, self.x0, self.labels, CIFAR_MEAN, CIFAR_STD)
         sbn = self.bn[spec.stem_bn.name]
         self._conv_bn(self.x0, self.conv["stem"], sbn, self.c0)
-        K.bn_apply_stats(self.c0, sbn, self.a0, self.c0.numel() // 64, momentum=self.bn_momentum)
+        cnt0 = self.c0.numel() // 64
+        if not self.stem_onload:
+            K.bn_apply_stats(self.c0, sbn, self.a0, cnt0, momentum=self.bn_momentum)
         if spec.stem == "imagenet":
             K.maxpool_fwd(self.a0, self.p0, self.p0_arg)
-        for st in self.blocks:
+        for i, st in enumerate(self.blocks):
             blk: BlockSpec = st["spec"]
             b1, b2 = self.bn[blk.bn1.name], self.bn[blk.bn2.name]
-            self._conv_bn(st["x"], self.conv[blk.conv1.name], b1, st["c1"])
+            stem_in = i == 0 and self.stem_onload
+            if stem_in:
+                K.conv3x3_bnin_fwd(self.c0, self.conv[blk.conv1.name].w, sbn, cnt0, st["c1"], stats=b1.stats_buf,
+                                   momentum=self.bn_momentum)
+            else:
+                self._conv_bn(st["x"], self.conv[blk.conv1.name], b1, st["c1"])
             cnt = st["c1"].numel() // blk.conv1.cout
             if st["bnin"]:
                 K.conv3x3_bnin_fwd(st["c1"], self.conv[blk.conv2.name].w, b1, cnt, st["c2"], stats=b2.stats_buf,
@@ -251,6 +264,9 @@ class FusedResNetTrainer:
                 self._conv_bn(st["x"], self.conv[blk.down.name], bd, st["cs"])
                 K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=st["cs"], rbn=bd, momentum=self.bn_momentum,
                                  mask_out=st["ym"])
+            elif stem_in:
+                K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=self.c0, rbn=sbn, res_relu=True,
+                                 momentum=self.bn_momentum, mask_out=st["ym"])
             else:
                 K.bn_apply_stats(st["c2"], b2, st["y"], cnt, res=st["x"], momentum=self.bn_momentum,
                                  mask_out=st["ym"])
@@ -344,7 +360,10 @@ class FusedResNetTrainer:
                 K.bn_bwd_reduce(st["da1"], None, st["c1"], b1.sums_buf, mask_coef=b1.coef)
             K.bn_bwd_apply_sums(st["da1"], None, st["c1"], b1.sums, b1.coef, b1.ggamma, b1.gbeta, st["dc1"],
                                 mask_coef=b1.coef)
-            K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g, ws=self.wgws)
+            if st is self.blocks[0] and self.stem_onload:
+                K.conv3x3_bnin_wgrad(self.c0, st["dc1"], sbn, self.c0.numel() // 64, c1.g, ws=self.wgws)
+            else:
+                K.conv_wgrad(st["x"], st["dc1"], blk.conv1.cout, 3, blk.conv1.stride, 1, c1.g, ws=self.wgws)
             K.conv_dgrad(st["dc1"], c1.wt, blk.conv1.cin, 3, blk.conv1.stride, 1, dx, add=add, bn=nxt,
                          add_even=add_even)
             dy = dx

@@ -317,14 +317,18 @@ def bn_bwd_apply(dy, y, x, dcoef, dx):
            rows, c, N.stream_ptr())
 
 
-def bn_apply_stats(x, bn, y, count, relu=True, res=None, rbn=None, eps=1e-5, momentum=0.1, mask_out=None):
+def bn_apply_stats(x, bn, y, count, relu=True, res=None, rbn=None, eps=1e-5, momentum=0.1, mask_out=None,
+                   res_relu=False):
     """Fused finalize + apply; ``bn``/``rbn`` expose stats, gamma, beta, coef, run_mean, run_var.
-    ``mask_out`` (u8, numel/8) receives bit j of byte q = ``y[8q+j] > 0``."""
+    ``mask_out`` (u8, numel/8) receives bit j of byte q = ``y[8q+j] > 0``.  ``res_relu``: the
+    residual is ``relu(rbn(res))`` (a BN-on-load block input, whose BN was published by the
+    conv that consumed it; ``rbn``'s coef / running stats are not written here)."""
     if mask_out is not None:
         assert mask_out.dtype == torch.uint8 and mask_out.numel() * 8 == x.numel() and mask_out.is_contiguous()
     c = x.shape[-1]
     rows = x.numel() // c
-    mode = 0 if res is None else (2 if rbn is not None else 1)
+    mode = 0 if res is None else ((3 if res_relu else 2) if rbn is not None else 1)
+    assert not res_relu or rbn is not None
     r = rbn
     N.call("sl_bn_apply_stats", _bf16(x), _f32(bn.stats), _f32(bn.gamma), _f32(bn.beta), _f32(bn.coef),
            _f32(bn.run_mean), _f32(bn.run_var), _bf16(res) if res is not None else None,

@@ -570,6 +570,9 @@ def test_resnet_block_backward_local():
         return F.batch_norm(xx, None, None, tr.params[b.g_off:b.g_off + b.c], tr.params[b.b_off:b.b_off + b.c],
                             training=True)
 
+    if tr.stem_onload:  # block 0's input a0 is rebuilt on load from c0, never stored: materialise it
+        tr.K.bn_apply(tr.c0, tr.bn[spec.stem_bn.name].coef, tr.a0, relu=True)
+        torch.cuda.synchronize()
     nb = len(tr.blocks)
     if tr.fuse_bn_bwd:
         # the data gradient of block i+1 lands in block i's dz, already ReLU-masked by block
@@ -811,8 +814,9 @@ def test_conv3x3_bn_on_load_matches_materialised_operand(n, h):
 
 
 def test_resnet_engine_bn_on_load_is_bit_identical_in_deterministic_build():
-    """Whole engine, deterministic kernel build: 3 training steps with BN-on-load (default) and
-    with SL_BN_ONLOAD=0 (bn_apply_stats + stored a1) give bit-identical parameters."""
+    """Whole engine, deterministic kernel build: 3 training steps with BN-on-load (default: the
+    64-channel blocks' a1 and the stem's a0 rebuilt on load) and with SL_BN_ONLOAD=0
+    (bn_apply_stats + stored operands) give bit-identical parameters."""
     import json
     import os
     import subprocess
@@ -828,5 +832,6 @@ def test_resnet_engine_bn_on_load_is_bit_identical_in_deterministic_build():
         assert out.returncode == 0, out.stderr[-2000:]
         res[v] = json.loads(out.stdout.strip().splitlines()[-1])
     assert res["1"]["bnin_blocks"] == 2 and res["0"]["bnin_blocks"] == 0, res
+    assert res["1"]["stem_onload"] and not res["0"]["stem_onload"], res
     assert res["1"]["deterministic_build"] and res["1"]["finite"], res
     assert res["1"]["param_hash"] == res["0"]["param_hash"], res
