@@ -1473,6 +1473,71 @@ void sl_wgrad_note_need(long floats) {
   if (floats > g_wgrad_ws_need) g_wgrad_ws_need = floats;
 }
 
+// Slab reduces on a side stream (sl_wgrad_side_begin ... sl_wgrad_side_join): a convolution's
+// reduce then runs beside the next data gradient instead of between two big kernels.  A slab
+// must not be rewritten while its reduce still reads it: each slab pointer keeps the event
+// recorded after its last reduce, and a weight-gradient kernel that writes the slab waits on it
+// first (the engine alternates two slabs, so that wait is normally long satisfied).
+static hipStream_t g_side = nullptr;
+static hipEvent_t g_fork = nullptr;
+struct SlabEvent {
+  const float* ws;
+  hipEvent_t ev;
+  bool live;
+};
+static SlabEvent g_slab_ev[4];
+static int g_slab_next = 0;
+
+int sl_wgrad_side_begin(hipStream_t side) {
+  if (!g_fork) {
+    if (hipEventCreateWithFlags(&g_fork, hipEventDisableTiming) != hipSuccess) return -1;
+    for (auto& e : g_slab_ev)
+      if (hipEventCreateWithFlags(&e.ev, hipEventDisableTiming) != hipSuccess) return -1;
+  }
+  for (auto& e : g_slab_ev) e.live = false;  // events of an earlier step are never waited on (capture isolation)
+  g_side = side;
+  return 0;
+}
+
+// `main` waits for everything issued on the side stream so far; end != 0 also stops routing
+// reduces to the side stream (the last join of a step, before the optimizer reads the gradient)
+int sl_wgrad_side_join(hipStream_t main, int end) {
+  if (!g_side) return 0;
+  if (hipEventRecord(g_fork, g_side) != hipSuccess || hipStreamWaitEvent(main, g_fork, 0) != hipSuccess) return -1;
+  if (end) {
+    g_side = nullptr;
+    for (auto& e : g_slab_ev) e.live = false;
+  }
+  return 0;
+}
+
+void sl_wgrad_slab_acquire(const float* ws, hipStream_t main) {
+  if (!g_side || !ws) return;
+  for (auto& e : g_slab_ev)
+    if (e.live && e.ws == ws) (void)hipStreamWaitEvent(main, e.ev, 0);
+}
+
+hipStream_t sl_wgrad_reduce_stream(hipStream_t main) {
+  if (!g_side) return main;
+  if (hipEventRecord(g_fork, main) != hipSuccess || hipStreamWaitEvent(g_side, g_fork, 0) != hipSuccess) return main;
+  return g_side;
+}
+
+void sl_wgrad_reduce_done(const float* ws, hipStream_t rs) {
+  if (!g_side || rs != g_side) return;
+  SlabEvent* slot = nullptr;
+  for (auto& e : g_slab_ev)
+    if (e.live && e.ws == ws) slot = &e;
+  if (!slot) {
+    slot = &g_slab_ev[g_slab_next];
+    g_slab_next = (g_slab_next + 1) % 4;
+  }
+  if (hipEventRecord(slot->ev, rs) == hipSuccess) {
+    slot->ws = ws;
+    slot->live = true;
+  }
+}
+
 // dw[0..n) += sum over `slices` partial vectors of n floats (n % 4 == 0, 16-B aligned)
 int sl_wgrad_slab_reduce(const float* ws, int slices, long n, float* dw, hipStream_t stream) {
   const long n4 = n / 4;
@@ -1486,7 +1551,10 @@ int sl_wgrad_slab_reduce(const float* ws, int slices, long n, float* dw, hipStre
 static int wgrad_finish(WgradArgs& a, float* ws, long ws_floats, hipStream_t stream, bool launch_reduce) {
   (void)ws_floats;
   if (!launch_reduce) return 0;
-  return sl_wgrad_slab_reduce(ws, a.slices, (long)a.cout * a.g.K, a.dw, stream);
+  hipStream_t rs = sl_wgrad_reduce_stream(stream);
+  const int rc = sl_wgrad_slab_reduce(ws, a.slices, (long)a.cout * a.g.K, a.dw, rs);
+  sl_wgrad_reduce_done(ws, rs);
+  return rc;
 }
 
 // slab mode when a workspace big enough for this call's partials is given; else atomics
@@ -1528,6 +1596,7 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
     a.slices = (total_steps + a.steps_per_slice - 1) / a.steps_per_slice;
     const bool slab = wgrad_use_slab(a, ws, ws_floats);
     if (SL_DETERMINISTIC && a.slices > 1 && !slab) return SL_NEED_WS;  // no order-dependent atomics
+    if (slab) sl_wgrad_slab_acquire(ws, stream);
     hipLaunchKernelGGL(conv_wgrad_big_kernel, dim3(tiles * a.slices), dim3(512), 0, stream, a);
     SL_CHECK_LAUNCH();
     return wgrad_finish(a, ws, ws_floats, stream, slab);
@@ -1547,6 +1616,7 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   dim3 grid(tiles * a.slices);
   const bool slab = wgrad_use_slab(a, ws, ws_floats);
   if (SL_DETERMINISTIC && a.slices > 1 && !slab) return SL_NEED_WS;
+  if (slab) sl_wgrad_slab_acquire(ws, stream);
   if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3, 1>), grid, dim3(256), 0, stream, a);
   else if (SL_WGRAD128_KS == 2)
     hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_KS2_SLOTS, 2>), grid, dim3(512), 0, stream, a);

@@ -641,6 +641,9 @@ int sl_conv3x3_wgrad_c64_applicable(int H, int W, int C, int cout, int KH, int K
 }
 
 int sl_wgrad_slab_reduce(const float* ws, int slices, long n, float* dw, hipStream_t stream);
+void sl_wgrad_slab_acquire(const float* ws, hipStream_t main);   // conv.hip: side-stream reduces
+hipStream_t sl_wgrad_reduce_stream(hipStream_t main);
+void sl_wgrad_reduce_done(const float* ws, hipStream_t rs);
 void sl_wgrad_note_need(long floats);
 
 static int conv3x3_wgrad_launch(const uint16_t* x, const uint16_t* dy, int ldy, int N, int H, float* dw, float* ws,
@@ -667,13 +670,16 @@ static int conv3x3_wgrad_launch(const uint16_t* x, const uint16_t* dy, int ldy, 
   sl_wgrad_note_need(need);
   a.ws = (ws && need <= ws_floats && !((uintptr_t)ws & 15) && !((uintptr_t)dw & 15)) ? ws : nullptr;
   if (SL_DETERMINISTIC && !a.ws) return SL_NEED_WS;  // no order-dependent atomics
+  if (a.ws) sl_wgrad_slab_acquire(a.ws, stream);
   hipLaunchKernelGGL(conv3x3_wgrad_c64_kernel, dim3(grid), dim3(WNT), 0, stream, a);
   SL_CHECK_LAUNCH();
   if (a.ws) {
     constexpr long units = 64L * 9 * HC / 4;
-    hipLaunchKernelGGL(halo_wgrad_reduce_kernel, dim3((int)((units * HSLAB_G + 255) / 256)), dim3(256), 0, stream,
+    hipStream_t rs = sl_wgrad_reduce_stream(stream);
+    hipLaunchKernelGGL(halo_wgrad_reduce_kernel, dim3((int)((units * HSLAB_G + 255) / 256)), dim3(256), 0, rs,
                        reinterpret_cast<const float4*>(a.ws), grid, dw);
     SL_CHECK_LAUNCH();
+    sl_wgrad_reduce_done(a.ws, rs);
   }
   return 0;
 }

@@ -19,6 +19,8 @@ Per step:
             sums (csrc/kernels/bn_bwd_epi.h), so only the first BN after the
             average pool still needs a bn_bwd_reduce pass (SL_BNB_FUSE=0: one
             per BN, as before)
+            (SL_WGRAD_SIDE=1: the split-K slab reduces run on a side stream, forked
+            per reduce and joined before the optimizer and each gradient bucket)
   comms     optional: the flat gradient is laid out in forward order, so
             when a block's backward is done its whole parameter range is final
             -> a bucket hook can launch RCCL all-reduce of that range while
@@ -175,7 +177,11 @@ class FusedResNetTrainer:
         self.bucket_wait = None   # callable(handles) -> None, before the optimizer
         self.allreduce = None     # callable(grad) -> None (simple, non-overlapped)
         self.bucket_bytes = 16 << 20
-        self.wgws = K.WgradWorkspace(dev)  # split-K slab of the weight gradients (grown on the first step)
+        self.wgws = K.WgradWorkspace(dev)  # split-K slabs of the weight gradients (grown on the first step)
+        # SL_WGRAD_SIDE=1: the slab reduces run on a side stream beside the next data gradient.  Off by
+        # default: starved by the one-workgroup-per-CU conv kernels, the reduces stretched from 13 to
+        # 36 us and the step got 3.6 % slower (profiles/r03_side)
+        self.wgrad_side = torch.cuda.Stream(dev) if os.environ.get("SL_WGRAD_SIDE", "0") == "1" else None
         # BN-backward sums in the data-gradient epilogues instead of bn_bwd_reduce passes
         self.fuse_bn_bwd = os.environ.get("SL_BNB_FUSE", "1") != "0"
 
@@ -281,11 +287,17 @@ class FusedResNetTrainer:
         pending_from = spec.n_flat  # grad[pending_from:] is final and not yet reduced
         bucket_elems = self.bucket_bytes // 4
 
+        side = self.wgrad_side
+        if side is not None:
+            K.wgrad_side_begin(side)
+
         def maybe_bucket(lo, force=False):
             nonlocal pending_from
             if self.bucket_hook is None:
                 return
             if force or (pending_from - lo) >= bucket_elems:
+                if side is not None:
+                    K.wgrad_side_join(end=False)  # the bucket's reduces are in the gradient
                 handles.append(self.bucket_hook(self.grad[lo:pending_from]))
                 pending_from = lo
 
@@ -379,6 +391,8 @@ class FusedResNetTrainer:
         sc = spec.stem_conv
         K.conv_wgrad(self.x0, self.dc0, 64, sc.k, sc.stride, sc.pad, self.conv["stem"].g, ws=self.wgws)
         maybe_bucket(0, force=True)
+        if side is not None:
+            K.wgrad_side_join(end=True)
         return handles
 
     def _step_eager(self) -> None:

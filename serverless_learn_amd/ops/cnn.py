@@ -42,6 +42,8 @@ N.register("sl_maxpool_bwd", [P, P, P, I, I, I, I, I, I, I, I, I, P])
 N.register("sl_avgpool_fwd", [P, P, I, I, I, P])
 N.register("sl_avgpool_bwd", [P, P, I, I, I, P])
 N.register("sl_softmax_ce", [P, P, P, P, P, I, P, I, I, F, P])
+N.register("sl_wgrad_side_begin", [P])
+N.register("sl_wgrad_side_join", [P, I])
 N.register("sl_conv3x3_c64_applicable", [I, I, I, I, I, I, I, I, I])
 N.register("sl_conv3x3_bnin_fwd", [P, P, I, I, P, I, P, P, P, P, P, P, P, F, F, F, P])
 N.register("sl_conv3x3_bnin_wgrad", [P, P, I, I, P, P, L, P, P, P, F, F, P])
@@ -153,21 +155,45 @@ def deterministic() -> bool:
 
 
 class WgradWorkspace:
-    """Slab for the weight gradient's split-K partials (plain stores + one ordered reduce
+    """Slabs for the weight gradient's split-K partials (plain stores + one ordered reduce
     launch instead of fp32 atomics into dw).  Sized by the launcher's own request: a call
-    that finds it too small falls back to atomics and records the size it wanted, and
-    :meth:`grow` (outside graph capture) makes the next call fit."""
+    that finds them too small falls back to atomics and records the size it wanted, and
+    :meth:`grow` (outside graph capture) makes the next call fit.  Two slabs, handed out
+    alternately (:meth:`take`), so a reduce running on a side stream (:func:`wgrad_side_begin`)
+    overlaps the next weight gradient instead of blocking its slab."""
 
     def __init__(self, device, floats: int = 0):
         self.device = device
-        self.buf = torch.empty(max(4, floats), dtype=torch.float32, device=device)
+        self.bufs = [torch.empty(max(4, floats), dtype=torch.float32, device=device) for _ in range(2)]
+        self.i = 0
+
+    @property
+    def buf(self):
+        return self.bufs[self.i]
+
+    def take(self):
+        b = self.bufs[self.i]
+        self.i ^= 1
+        return b
 
     def grow(self) -> bool:
         need = int(N.lib().sl_conv_wgrad_ws_need())
-        if need > self.buf.numel():
-            self.buf = torch.empty(need, dtype=torch.float32, device=self.device)
+        if need > self.bufs[0].numel():
+            self.bufs = [torch.empty(need, dtype=torch.float32, device=self.device) for _ in range(2)]
             return True
         return False
+
+
+def wgrad_side_begin(side_stream) -> None:
+    """Route the slab reduces of the following weight gradients to ``side_stream`` (forked from
+    the current stream per reduce, so it works inside a hipGraph capture); end with
+    :func:`wgrad_side_join`."""
+    N.call("sl_wgrad_side_begin", ctypes.c_void_p(side_stream.cuda_stream))
+
+
+def wgrad_side_join(end: bool = True) -> None:
+    """The current stream waits for every reduce issued so far; ``end`` stops the routing."""
+    N.call("sl_wgrad_side_join", N.stream_ptr(), 1 if end else 0)
 
 
 def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: int = 0, ws=None):
@@ -176,7 +202,7 @@ def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: 
     _, oh, ow, ldy = dy.shape
     assert dw.dtype == torch.float32 and dw.numel() >= cout * k * k * c
     for attempt in range(2):
-        buf = ws.buf if ws is not None else None
+        buf = ws.take() if ws is not None else None
         rc = N.lib().sl_conv_wgrad(_bf16(x), n, h, wd, c, _bf16(dy), ldy, cout, k, k, stride, pad, oh, ow, p(dw),
                                    int(target_wgs or _WGRAD_WGS), p(buf), int(buf.numel()) if buf is not None else 0,
                                    N.stream_ptr())
@@ -216,7 +242,7 @@ def conv3x3_bnin_wgrad(x, dy, bn, count: int, dw, ws=None, eps: float = 1e-5):
     n, h, wd, c = x.shape
     assert dy.shape == (n, h, wd, 64) and dw.dtype == torch.float32 and dw.numel() >= 64 * 9 * 64
     for attempt in range(2):
-        buf = ws.buf if ws is not None else None
+        buf = ws.take() if ws is not None else None
         rc = N.lib().sl_conv3x3_bnin_wgrad(_bf16(x), _bf16(dy), n, h, p(dw), p(buf),
                                            int(buf.numel()) if buf is not None else 0, _f32(bn.stats),
                                            _f32(bn.gamma), _f32(bn.beta), float(count), float(eps), N.stream_ptr())

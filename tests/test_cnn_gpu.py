@@ -816,7 +816,8 @@ def test_conv3x3_bn_on_load_matches_materialised_operand(n, h):
 def test_resnet_engine_bn_on_load_is_bit_identical_in_deterministic_build():
     """Whole engine, deterministic kernel build: 3 training steps with BN-on-load (default: the
     64-channel blocks' a1 and the stem's a0 rebuilt on load) and with SL_BN_ONLOAD=0
-    (bn_apply_stats + stored operands) give bit-identical parameters."""
+    (bn_apply_stats + stored operands) give bit-identical parameters, and so does the run with
+    the weight-gradient slab reduces on a side stream (SL_WGRAD_SIDE=1)."""
     import json
     import os
     import subprocess
@@ -825,8 +826,10 @@ def test_resnet_engine_bn_on_load_is_bit_identical_in_deterministic_build():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     script = os.path.join(root, "scripts", "resnet_onload_check.py")
     res = {}
-    for v in ("1", "0"):
-        env = dict(os.environ, SL_DETERMINISTIC="1", SL_BN_ONLOAD=v)
+    for v in ("1", "0", "side1"):
+        # "side1": BN-on-load with the slab reduces on the side stream (opt-in SL_WGRAD_SIDE=1)
+        env = dict(os.environ, SL_DETERMINISTIC="1", SL_BN_ONLOAD="1" if v == "side1" else v,
+                   SL_WGRAD_SIDE="1" if v == "side1" else "0")
         out = subprocess.run([sys.executable, script, "64", "3"], env=env, capture_output=True, text=True,
                              timeout=240)
         assert out.returncode == 0, out.stderr[-2000:]
@@ -834,4 +837,4 @@ def test_resnet_engine_bn_on_load_is_bit_identical_in_deterministic_build():
     assert res["1"]["bnin_blocks"] == 2 and res["0"]["bnin_blocks"] == 0, res
     assert res["1"]["stem_onload"] and not res["0"]["stem_onload"], res
     assert res["1"]["deterministic_build"] and res["1"]["finite"], res
-    assert res["1"]["param_hash"] == res["0"]["param_hash"], res
+    assert res["1"]["param_hash"] == res["0"]["param_hash"] == res["side1"]["param_hash"], res
