@@ -123,6 +123,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   unsigned hok = 0;  // bit i: chunk i is inside the image (zero padding stays zero under BN-on-load)
   auto halo_load = [&](int tile) {
     const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
+    hok = 0;
 #pragma unroll
     for (int i = 0; i < HL; ++i) {
       const int q = tid + i * NTF;
@@ -132,7 +133,6 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       const bool ok = q < L::HALO_CHUNKS && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW;
       hv[i] = ok ? *reinterpret_cast<const uint4*>(a.src + (((long)img * a.H + ih) * IW + iw) * CIN + c * 8)
                  : make_uint4(0, 0, 0, 0);
-      if (i == 0) hok = 0;
       hok |= (unsigned)ok << i;
     }
   };

@@ -177,11 +177,12 @@ class FusedResNetTrainer:
         self.bucket_wait = None   # callable(handles) -> None, before the optimizer
         self.allreduce = None     # callable(grad) -> None (simple, non-overlapped)
         self.bucket_bytes = 16 << 20
-        self.wgws = K.WgradWorkspace(dev)  # split-K slabs of the weight gradients (grown on the first step)
         # SL_WGRAD_SIDE=1: the slab reduces run on a side stream beside the next data gradient.  Off by
         # default: starved by the one-workgroup-per-CU conv kernels, the reduces stretched from 13 to
         # 36 us and the step got 3.6 % slower (profiles/r03_side)
         self.wgrad_side = torch.cuda.Stream(dev) if os.environ.get("SL_WGRAD_SIDE", "0") == "1" else None
+        # split-K slab(s) of the weight gradients, grown on the first step
+        self.wgws = K.WgradWorkspace(dev, alternate=self.wgrad_side is not None)
         # BN-backward sums in the data-gradient epilogues instead of bn_bwd_reduce passes
         self.fuse_bn_bwd = os.environ.get("SL_BNB_FUSE", "1") != "0"
 

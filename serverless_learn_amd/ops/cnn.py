@@ -155,16 +155,17 @@ def deterministic() -> bool:
 
 
 class WgradWorkspace:
-    """Slabs for the weight gradient's split-K partials (plain stores + one ordered reduce
+    """Slab for the weight gradient's split-K partials (plain stores + one ordered reduce
     launch instead of fp32 atomics into dw).  Sized by the launcher's own request: a call
-    that finds them too small falls back to atomics and records the size it wanted, and
-    :meth:`grow` (outside graph capture) makes the next call fit.  Two slabs, handed out
-    alternately (:meth:`take`), so a reduce running on a side stream (:func:`wgrad_side_begin`)
-    overlaps the next weight gradient instead of blocking its slab."""
+    that finds it too small falls back to atomics and records the size it wanted, and
+    :meth:`grow` (outside graph capture) makes the next call fit.  ``alternate``: two slabs
+    handed out in turn (:meth:`take`), so a reduce running on a side stream
+    (:func:`wgrad_side_begin`) does not block the next weight gradient's slab."""
 
-    def __init__(self, device, floats: int = 0):
+    def __init__(self, device, floats: int = 0, alternate: bool = False):
         self.device = device
-        self.bufs = [torch.empty(max(4, floats), dtype=torch.float32, device=device) for _ in range(2)]
+        self.bufs = [torch.empty(max(4, floats), dtype=torch.float32, device=device)
+                     for _ in range(2 if alternate else 1)]
         self.i = 0
 
     @property
@@ -173,13 +174,13 @@ class WgradWorkspace:
 
     def take(self):
         b = self.bufs[self.i]
-        self.i ^= 1
+        self.i = (self.i + 1) % len(self.bufs)
         return b
 
     def grow(self) -> bool:
         need = int(N.lib().sl_conv_wgrad_ws_need())
         if need > self.bufs[0].numel():
-            self.bufs = [torch.empty(need, dtype=torch.float32, device=self.device) for _ in range(2)]
+            self.bufs = [torch.empty(need, dtype=torch.float32, device=self.device) for _ in self.bufs]
             return True
         return False
 
