@@ -44,6 +44,11 @@ constexpr int NTH = 256;
 #define SL_HALO_WAVES 8  // 8 measured +1% over 4 (two waves per SIMD)
 #endif
 constexpr int NWF = SL_HALO_WAVES;     // waves of the forward / dgrad kernel
+#ifndef SL_HALO_KO
+// timing knockouts of conv3x3_kernel (results wrong; profiles/r03_haloko): 1 no epilogue global
+// traffic, 2 no halo loads after the first tile, 3 no MFMAs / fragment reads, 4 no epilogue
+#define SL_HALO_KO 0
+#endif
 constexpr int NTF = 64 * NWF;
 constexpr int MF = TPIX / NWF / 16;    // m-fragments (16 output pixels) per wave
 constexpr int OUT_LD = 72;             // staging row stride (elements)
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   __syncthreads();
   for (; t < a.tiles; t += gridDim.x) {
     const int next = t + gridDim.x;
-    if (next < a.tiles) halo_load(next);  // lands under this tile's MFMAs
+    if (next < a.tiles && SL_HALO_KO != 2) halo_load(next);  // lands under this tile's MFMAs
 
     floatx4_t acc[MF][4];
 #pragma unroll
@@ -220,14 +225,21 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
     for (int s = 0; s < L::NKS; s += 2) {
       if (s + 1 < L::NKS) frag_reads(s + 1, a1, b1);
       __builtin_amdgcn_sched_barrier(0);
-      mfmas(a0, b0);
+      if (SL_HALO_KO != 3) mfmas(a0, b0);
       __builtin_amdgcn_sched_barrier(0);
       if (s + 2 < L::NKS) frag_reads(s + 2, a0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < L::NKS) mfmas(a1, b1);
+      if (s + 1 < L::NKS && SL_HALO_KO != 3) mfmas(a1, b1);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // every wave is done with this halo
+    if (SL_HALO_KO == 4) {
+      if (next < a.tiles) {
+        halo_store();
+        __syncthreads();
+      }
+      continue;
+    }
 
     // ---- epilogue: statistics in registers, bf16 tile staged through LDS ----
     if (a.stats) {
@@ -259,6 +271,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
 #pragma unroll
     for (int k = 0; k < EIT; ++k) {
       const long off = (pix0 + ((tid + k * NTF) >> 3)) * a.ldy + c;
+      if (SL_HALO_KO == 1) continue;
       if (a.add) ea[k] = ld8(a.add + off);
       if (bnb) bnb_load<false>(a.bn, off, ebn[k]);
     }
@@ -271,6 +284,10 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       if (a.add) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (short)f2bf(bf2f((uint16_t)v[e]) + bf2f((uint16_t)ea[k][e]));
+      }
+      if (SL_HALO_KO == 1) {
+        if (v[0] == 12345) a.y[m * a.ldy + c] = 0;  // keeps the staging read alive
+        continue;
       }
       if (bnb) bnb_chunk<false>(a.bn, ebn[k], v, msc, msh, bacc);
       *reinterpret_cast<short8_t*>(a.y + m * a.ldy + c) = v;
