@@ -266,7 +266,7 @@ class FusedMLPTrainer:
             raise ValueError(f"batch must be a multiple of {BLOCK_ROWS}")
         self._n = _native
         _native.lib()  # fail loudly if the HIP library cannot be loaded
-        if os.environ.get("SL_MLP_ROWS_BM"):  # force the rows kernel's tile height (64 / 128)
+        if os.environ.get("SL_MLP_ROWS_BM"):  # force the rows kernel's tile height (64 / 128 / 256)
             _native.call("sl_mlp_set_rows_bm", int(os.environ["SL_MLP_ROWS_BM"]))
         dev = torch.device(device)
         self.device = dev
