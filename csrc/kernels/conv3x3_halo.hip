@@ -44,6 +44,9 @@ constexpr int NTH = 256;
 #define SL_HALO_WAVES 8  // 8 measured +1% over 4 (two waves per SIMD)
 #endif
 constexpr int NWF = SL_HALO_WAVES;     // waves of the forward / dgrad kernel
+#ifndef SL_HALO_DEFER
+#define SL_HALO_DEFER 1  // plain forward: output stores deferred into the next tile's k-loop
+#endif
 #ifndef SL_HALO_KO
 // timing knockouts of conv3x3_kernel (results wrong; profiles/r03_haloko): 1 no epilogue global
 // traffic, 2 no halo loads after the first tile, 3 no MFMAs / fragment reads, 4 no epilogue
@@ -93,13 +96,22 @@ struct HaloArgs {
   float bin_count, bin_eps, bin_momentum;
 };
 
-template <int CIN>
+// DEFER (plain forward: no residual, no fused BN backward): the bf16 output tile is staged in
+// its own unpadded, XOR-swizzled 32 KB LDS image and written to HBM during the NEXT tile's
+// k-loop, one 16-B store per thread every other k-step pair, instead of in a serial epilogue
+// with the matrix cores idle (profiles/r03_haloko).  LDS: 54.4 + 75.8 + 32 KB = 159.1 KB.
+constexpr int DEFER_BYTES = TPIX * HC * 2;
+__device__ __forceinline__ int cs_swz(int p, int chunk) { return p * (HC * 2) + ((chunk ^ ((p >> 1) & 7)) << 4); }
+
+template <int CIN, bool DEFER>
 __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   using L = Lay<CIN>;
   constexpr int HL = (L::HALO_CHUNKS + NTF - 1) / NTF;  // halo chunks per thread
-  __shared__ __attribute__((aligned(16))) uint8_t smem[L::REGION + L::W_BYTES];
+  static_assert(!DEFER || L::REGION + L::W_BYTES + DEFER_BYTES <= 160 * 1024, "deferred image must fit LDS");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[L::REGION + L::W_BYTES + (DEFER ? DEFER_BYTES : 0)];
   uint8_t* Hs = smem;
   uint8_t* Ws = smem + L::REGION;
+  uint8_t* Ds = smem + L::REGION + L::W_BYTES;  // DEFER: the previous tile's output
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lg = lane >> 4;
@@ -183,6 +195,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   if (bnb) bnb_init(a.bn, HC, (tid & 7) * 8, bacc, msc, msh);
 
   int t = blockIdx.x;
+  int prev_t = -1;  // DEFER: tile whose output waits in Ds
   if (t < a.tiles) halo_load(t);
   halo_store();
   __syncthreads();
@@ -220,9 +233,18 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
     };
+    // DEFER: this thread's 4 chunks of the previous tile's output, one per k-step pair 1, 3, 5, 7
+    auto defer_store = [&](int k) __attribute__((always_inline)) {
+      const int p = (tid + k * NTF) >> 3, ch = tid & 7;
+      const short8_t v = *reinterpret_cast<const short8_t*>(Ds + cs_swz(p, ch));
+      *reinterpret_cast<short8_t*>(a.y + ((long)prev_t * TPIX + p) * a.ldy + ch * 8) = v;
+    };
     frag_reads(0, a0, b0);
 #pragma unroll
     for (int s = 0; s < L::NKS; s += 2) {
+      if constexpr (DEFER) {
+        if ((s >> 1) % 2 == 1 && (s >> 2) < 4 && prev_t >= 0) defer_store(s >> 2);
+      }
       if (s + 1 < L::NKS) frag_reads(s + 1, a1, b1);
       __builtin_amdgcn_sched_barrier(0);
       if (SL_HALO_KO != 3) mfmas(a0, b0);
@@ -253,6 +275,24 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
             ssum[j] += v;
             ssq[j] += v * v;
           }
+    }
+    if constexpr (DEFER) {
+      // the k-loop above has read all of Ds (every wave passed the barrier): overwrite it
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int p = wave * (TPIX / NWF) + i * 16 + 4 * lg + r, col = j * 16 + lr;
+            *reinterpret_cast<uint16_t*>(Ds + cs_swz(p, col >> 3) + (col & 7) * 2) = f2bf(acc[i][j][r]);
+          }
+      prev_t = t;
+      if (next < a.tiles) {
+        halo_store();
+        __syncthreads();  // halo and Ds visible to the next k-loop
+      }
+      continue;
     }
     uint16_t* Cs = reinterpret_cast<uint16_t*>(Hs);
 #pragma unroll
@@ -299,6 +339,17 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
     }
   }
 
+  if constexpr (DEFER) {
+    if (prev_t >= 0) {
+      __syncthreads();  // the last tile's Ds writes are visible
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = (tid + k * NTF) >> 3, ch = tid & 7;
+        const short8_t v = *reinterpret_cast<const short8_t*>(Ds + cs_swz(p, ch));
+        *reinterpret_cast<short8_t*>(a.y + ((long)prev_t * TPIX + p) * a.ldy + ch * 8) = v;
+      }
+    }
+  }
   if (a.stats) {
     // lanes lg = 0..3 hold partials of channel 16 j + lr over different rows
 #pragma unroll
@@ -372,8 +423,10 @@ static int conv3x3_launch(const uint16_t* src, const uint16_t* w, int cin, int f
     a.bin = *bin;
   }
   const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;  // persistent: one workgroup per CU (130 KB LDS)
-  if (cin == 64) hipLaunchKernelGGL(conv3x3_kernel<64>, dim3(grid), dim3(NTF), 0, stream, a);
-  else hipLaunchKernelGGL(conv3x3_kernel<8>, dim3(grid), dim3(NTF), 0, stream, a);
+  const bool defer = SL_HALO_DEFER && cin == 64 && !flip && !add && !bn;
+  if (defer) hipLaunchKernelGGL((conv3x3_kernel<64, true>), dim3(grid), dim3(NTF), 0, stream, a);
+  else if (cin == 64) hipLaunchKernelGGL((conv3x3_kernel<64, false>), dim3(grid), dim3(NTF), 0, stream, a);
+  else hipLaunchKernelGGL((conv3x3_kernel<8, false>), dim3(grid), dim3(NTF), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
