@@ -516,7 +516,7 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const uint16_t* __rest
 
 // ---------------------------------------------------------------------------
 #if SL_DETERMINISTIC
-__device__ unsigned long long g_dbias_fix[16];  // fixed-point bias-gradient accumulator (zero between launches)
+__device__ unsigned long long g_dbias_fix[32];  // fixed-point (hi, lo) bias-gradient pairs (zero between launches)
 __device__ unsigned g_dbias_ticket;
 #endif
 // Softmax cross-entropy over fp32 logits [N][ncls] (ncls <= 16); one row per
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict
     float acc = 0.f;
     for (int g2 = 0; g2 < 16; ++g2) acc += bsum[g2][tid];
 #if SL_DETERMINISTIC
-    atomicAdd(&g_dbias_fix[tid], (unsigned long long)__double2ll_rn((double)acc * SL_FIX_SCALE));
+    fix_add(&g_dbias_fix[2 * tid], acc);
 #else
     atomicAdd(dbias + tid, acc);
 #endif
@@ -582,8 +582,10 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict
     __syncthreads();
     if (last && tid < ncls) {
       __threadfence();
-      const unsigned long long v = atomicExch(&g_dbias_fix[tid], 0ull);
-      dbias[tid] += (float)((double)(long long)v / SL_FIX_SCALE);
+      unsigned long long v[2];
+      v[0] = atomicExch(&g_dbias_fix[2 * tid], 0ull);
+      v[1] = atomicExch(&g_dbias_fix[2 * tid + 1], 0ull);
+      dbias[tid] += (float)fix_value(v);
     }
     if (last && tid == 0) atomicExch(&g_dbias_ticket, 0u);
   }

@@ -129,16 +129,34 @@ __host__ __device__ constexpr long rsum_floats(int n) { return (long)(SL_REP + 1
 
 // Deterministic build (SL_DETERMINISTIC=1, libslkernels_det.so, loaded when the
 // SL_DETERMINISTIC env var is set): the float atomics' order varies from run to run, so
-// every cross-workgroup sum is instead a 64-bit fixed-point integer atomic (2^-32
-// resolution, |sum| < 2^31) into replica 0, read as int64[n].  Integer addition is
+// every cross-workgroup sum is instead kept in 64-bit fixed point.  Integer addition is
 // associative: the folded result is bit-identical for any workgroup order.
+//
+// One fixed-point scale cannot cover both a BatchNorm sum of squares over millions of
+// pixels (|sum| up to ~1e10) and a tiny gradient sum, so each value v is added as a pair
+// of int64 atomics (fix_add): hi = rn(v * 2^8), lo = rn((v - hi / 2^8) * 2^40).  Each value
+// is kept to 2^-41; hi wraps only past |sum| = 2^55 and lo (|lo| <= 2^31 per value) only
+// past 2^32 values per entry.  The pairs sit interleaved at the start of the replica area
+// ([n][2] int64 = 16 n bytes of the [SL_REP][n] floats).
 #ifndef SL_DETERMINISTIC
 #define SL_DETERMINISTIC 0
 #endif
-constexpr double SL_FIX_SCALE = 4294967296.0;
+constexpr double SL_FIX_HI = 256.0;
+constexpr double SL_FIX_LO = 1099511627776.0;  // 2^40
 // launcher return code: a deterministic build needs a bigger split-K workspace for this call
 // (the python wrapper grows it and calls again; the other builds fall back to atomics)
 constexpr int SL_NEED_WS = 7;
+
+// p[0] += hi(v), p[1] += lo(v)
+__device__ __forceinline__ void fix_add(unsigned long long* p, float v) {
+  const double d = (double)v;
+  const double h = rint(d * SL_FIX_HI);
+  atomicAdd(p, (unsigned long long)(long long)h);
+  atomicAdd(p + 1, (unsigned long long)__double2ll_rn((d - h * (1.0 / SL_FIX_HI)) * SL_FIX_LO));
+}
+__host__ __device__ __forceinline__ double fix_value(const unsigned long long* p) {
+  return (double)(long long)p[0] * (1.0 / SL_FIX_HI) + (double)(long long)p[1] * (1.0 / SL_FIX_LO);
+}
 
 __device__ __forceinline__ float* rsum_replica(float* buf, int n) {
   return SL_DETERMINISTIC ? buf : buf + (long)(blockIdx.x % SL_REP) * n;
@@ -147,7 +165,7 @@ __device__ __forceinline__ float* rsum_result(float* buf, int n) { return buf + 
 // add v to entry i of a replica returned by rsum_replica
 __device__ __forceinline__ void rsum_add(float* rep, long i, float v) {
 #if SL_DETERMINISTIC
-  atomicAdd(reinterpret_cast<unsigned long long*>(rep) + i, (unsigned long long)__double2ll_rn((double)v * SL_FIX_SCALE));
+  fix_add(reinterpret_cast<unsigned long long*>(rep) + 2 * i, v);
 #else
   atomicAdd(rep + i, v);
 #endif

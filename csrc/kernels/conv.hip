@@ -1295,7 +1295,7 @@ __global__ __launch_bounds__(64) void rsum_fold_kernel(float* buf, int n, float*
   }
   if (i >= n) return;
 #if SL_DETERMINISTIC
-  const float acc = (float)((double)reinterpret_cast<const long long*>(buf)[i] / SL_FIX_SCALE);
+  const float acc = (float)fix_value(reinterpret_cast<const unsigned long long*>(buf) + 2 * i);
 #else
   float v[SL_REP];
 #pragma unroll

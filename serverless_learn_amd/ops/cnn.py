@@ -177,9 +177,19 @@ class WgradWorkspace:
         self.i = (self.i + 1) % len(self.bufs)
         return b
 
+    def untake(self) -> None:
+        """Hand the slab of the last :meth:`take` out again (a call retried after :meth:`grow`
+        keeps the alternation parity it would have had)."""
+        self.i = (self.i - 1) % len(self.bufs)
+
     def grow(self) -> bool:
         need = int(N.lib().sl_conv_wgrad_ws_need())
         if need > self.bufs[0].numel():
+            # a side-stream reduce (wgrad_side_begin) may still read the old slabs: let every
+            # queued use finish before the caching allocator may hand their memory out again
+            # (grow runs eagerly, outside graph capture, and rarely)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
             self.bufs = [torch.empty(need, dtype=torch.float32, device=self.device) for _ in self.bufs]
             return True
         return False
@@ -211,6 +221,7 @@ def conv_wgrad(x, dy, cout: int, k: int, stride: int, pad: int, dw, target_wgs: 
         # here, eagerly: a first step runs before any graph capture)
         if rc == NEED_WS and ws is not None and attempt == 0 and not torch.cuda.is_current_stream_capturing():
             ws.grow()
+            ws.untake()
             continue
         if rc != 0:
             raise RuntimeError(f"sl_conv_wgrad failed with code {rc}")
@@ -249,6 +260,7 @@ def conv3x3_bnin_wgrad(x, dy, bn, count: int, dw, ws=None, eps: float = 1e-5):
                                            _f32(bn.gamma), _f32(bn.beta), float(count), float(eps), N.stream_ptr())
         if rc == NEED_WS and ws is not None and attempt == 0 and not torch.cuda.is_current_stream_capturing():
             ws.grow()
+            ws.untake()
             continue
         if rc != 0:
             raise RuntimeError(f"sl_conv3x3_bnin_wgrad failed with code {rc}")

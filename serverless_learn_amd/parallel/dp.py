@@ -157,11 +157,11 @@ class ElasticGroup:
     def allreduce_async(self, t: torch.Tensor, op=None):
         if self.pg is None:
             return None
-        if op is None:
-            return self.pg.allreduce([t])
-        o = dist.AllreduceOptions()
-        o.reduceOp = op
         try:
+            if op is None:
+                return self.pg.allreduce([t])
+            o = dist.AllreduceOptions()
+            o.reduceOp = op
             return self.pg.allreduce([t], o)
         except Exception as e:
             self.broken = True

@@ -98,6 +98,7 @@ class Worker:
         self._broken_since = None  # when the live group was first seen broken (monotonic s)
         self._agree_stream = None  # side stream of the epoch agreement on RCCL groups
         self.bytes_ingested = 0
+        self._log_param_sum = os.environ.get("SL_LOG_PARAM_SUM", "0") == "1"
         self.files_received: list[int] = []
         self.state = "idle"
         self.registered = threading.Event()
@@ -545,29 +546,37 @@ class Worker:
                 and t.allreduce is None and getattr(t, "bucket_hook", None) is None)
 
     def _run_chunk(self, n: int) -> int:
-        """Run up to ``n`` steps; returns how many ran.  Graph mode replays a captured
-        k-step graph (re-captured whenever load_shard / set_world / enable_xgmi / a
-        checkpoint load dropped it); eager mode runs one step."""
+        """Run exactly ``min(n, graph_steps)`` steps and return that count.
+
+        The chunk length is a function of the step counter and the shared config only
+        (``n`` comes from the log / checkpoint / hold boundaries), never of this rank's own
+        graph state: every chunk posts one group collective (``_agree``), so members of a
+        lock-step group must cut their chunks at the same steps even when a shard landing
+        on one of them mid-run dropped only its graph.  Graph mode replays a
+        captured k-step graph; a chunk that finds no graph runs one eager step (sizes the
+        lazily-grown workspaces), captures, and replays the rest of the chunk."""
         t = self.trainer
-        if not self._use_graph():
-            t.step()
-            return 1
         k = max(1, self.cfg.graph_steps)
+        n = max(1, min(n, k))
+        if not self._use_graph():
+            for _ in range(n):
+                t.step()
+            return n
+        done = 0
         if t.graph is None:
-            # one eager step first (sizes lazily-grown workspaces), then capture
             t.step()
+            done = 1
             if hasattr(t, "steps"):
                 t.capture(warmup=0, unroll=k)
             else:
                 t.capture(warmup=0)
             self.log.info("graph_captured", steps=k, step=self.step + 1)
-            return 1
-        n = min(n, k)
-        if hasattr(t, "steps"):
-            t.steps(n)
-        else:
-            for _ in range(n):
-                t.step()
+        if n > done:
+            if hasattr(t, "steps"):
+                t.steps(n - done)
+            else:
+                for _ in range(n - done):
+                    t.step()
         self.graph_chunks += 1
         return n
 
@@ -716,11 +725,15 @@ class Worker:
                 t_last, s_last = time.perf_counter(), self.samples
                 self.loss = st.loss
                 gm = self.group_metrics
+                extra = {}
+                if self._log_param_sum:
+                    # replica checksum for the elastic rehearsal (scripts/elastic_demo.py): a float64
+                    # copy of every parameter and a device sync, so opt-in only
+                    extra["param_sum"] = float(self.trainer.params.double().sum())
                 self.log.info("train", step=self.step, loss=round(st.loss, 4), acc=round(st.accuracy, 4),
                               samples_per_sec=round(self.rate, 1), epoch=self.group.epoch,
                               group_samples_per_sec=round(gm["samples_per_sec"], 1), group_world=gm["world"],
-                              group_loss=round(gm["loss"], 4), graph=self._use_graph(),
-                              param_sum=float(self.trainer.params.double().sum()))
+                              group_loss=round(gm["loss"], 4), graph=self._use_graph(), **extra)
             if (self.cfg.checkpoint_every and self.step // self.cfg.checkpoint_every != prev // self.cfg.checkpoint_every
                     and (self.group.rank <= 0)):
                 try:

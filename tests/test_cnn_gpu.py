@@ -838,3 +838,29 @@ def test_resnet_engine_bn_on_load_is_bit_identical_in_deterministic_build():
     assert res["1"]["stem_onload"] and not res["0"]["stem_onload"], res
     assert res["1"]["deterministic_build"] and res["1"]["finite"], res
     assert res["1"]["param_hash"] == res["0"]["param_hash"] == res["side1"]["param_hash"], res
+
+
+def test_deterministic_sums_cover_large_and_tiny_magnitudes():
+    """The deterministic build's cross-workgroup sums (common.h fix_add: a (2^-8, 2^-40) pair of
+    int64 accumulators per entry) neither wrap on a BatchNorm sum of squares far past 2^31
+    (a single 2^-32 fixed-point int64 did) nor round tiny values away: conv-epilogue statistics
+    of large- and tiny-magnitude outputs match fp64 sums of the stored outputs, in the
+    deterministic build and in the default one."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for det in ("1", "0"):
+        env = dict(os.environ, SL_DETERMINISTIC=det)
+        if det == "0":
+            env.pop("SL_DETERMINISTIC")
+        out = subprocess.run([sys.executable, os.path.join(root, "scripts", "det_sums_check.py")],
+                             env=env, capture_output=True, text=True, timeout=240)
+        assert out.returncode == 0, out.stderr[-2000:]
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        assert r["deterministic_build"] == (det == "1"), r
+        assert r["large"]["sumsq_max"] > 2.0 ** 33, r
+        for k in ("large", "tiny"):
+            assert r[k]["finite"] and r[k]["rel_sum"] < 1e-2 and r[k]["rel_sumsq"] < 1e-2, r

@@ -420,3 +420,74 @@ def test_cpu_trainer_resume_is_exact(model):
             assert torch.allclose(rm, b.running[name][0], atol=1e-6) and torch.allclose(rv, b.running[name][1], atol=1e-6)
         st = b.evaluate(x[:batch], y[:batch])
         assert st.samples == batch and st.loss > 0
+
+
+class _FakeGraphTrainer:
+    """Counts steps; ``graph`` is dropped by ``load_shard`` like the fused engines'."""
+
+    allreduce = None
+
+    def __init__(self):
+        self.graph = None
+        self.ran = 0
+
+    def step(self):
+        self.ran += 1
+
+    def steps(self, n):
+        self.ran += n
+
+    def capture(self, warmup=0, unroll=1):
+        self.graph = object()
+
+    def load_shard(self):
+        self.graph = None
+
+
+def test_worker_chunk_length_does_not_depend_on_graph_state(monkeypatch):
+    """every chunk posts one group collective, so two lock-step members
+    must cut chunks at the same steps.  A rank whose graph was just dropped (a shard landed
+    on it mid-run) used to run a 1-step capture chunk while its peers ran 16."""
+    from serverless_learn_amd.runtime.local_cluster import fast_config
+    from serverless_learn_amd.runtime.worker import Worker
+
+    cfg = fast_config(graph_steps=16)
+    ws = [Worker("127.0.0.1:0", cfg) for _ in range(2)]
+    for w in ws:
+        w.trainer = _FakeGraphTrainer()
+        monkeypatch.setattr(w, "_use_graph", lambda: True)
+    cuts = [[], []]
+    for i, w in enumerate(ws):
+        step = 0
+        while step < 100:
+            if i == 1 and step in (16, 48):
+                w.trainer.load_shard()  # only this rank re-captures
+            want = min(100 - step, 10 - step % 10)  # a log boundary every 10 steps
+            ran = w._run_chunk(want)
+            assert w.trainer.ran == step + ran
+            step += ran
+            cuts[i].append(step)
+    assert cuts[0] == cuts[1]
+    # eager mode cuts the same chunks
+    w = Worker("127.0.0.1:0", cfg)
+    w.trainer = _FakeGraphTrainer()
+    monkeypatch.setattr(w, "_use_graph", lambda: False)
+    assert w._run_chunk(40) == 16 and w._run_chunk(3) == 3
+
+
+def test_allreduce_async_enqueue_failure_is_group_broken():
+    """an enqueue that fails on an aborted communicator must surface as
+    GroupBroken (which the training loop handles by re-forming) on both the sum path and
+    the op path."""
+    from serverless_learn_amd.parallel.dp import ElasticGroup, GroupBroken
+
+    class DeadPG:
+        def allreduce(self, *a):
+            raise RuntimeError("communicator aborted")
+
+    for op in (None, torch.distributed.ReduceOp.MAX):
+        g = ElasticGroup(backend="gloo")
+        g.pg = DeadPG()
+        with pytest.raises(GroupBroken):
+            g.allreduce_async(torch.zeros(2), op)
+        assert g.broken
