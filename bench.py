@@ -369,8 +369,13 @@ def main(argv=None) -> int:
             tr.bucket_wait = lambda handles: [h.wait() for h in handles]
     tr.load_shard(x, y)
 
-    # the xGMI exchange needs no host sync, so the N>1 MLP step is graph-captured like N=1
-    use_graph = args.graph == "on" or (args.graph == "auto" and (world == 1 or xg is not None))
+    # the xGMI exchange needs no host sync, so the N>1 MLP step is graph-captured like N=1; RCCL
+    # collectives (the MLP all-reduce hook, the ResNet bucket all-reduces and their waits) are
+    # stream-ordered device work and are captured into the step graph as well
+    # (tests/test_rccl_gpu.py: captured RCCL steps bit-identical to the hook-free step).  gloo
+    # collectives run on the host and keep the eager step.
+    graph_pg = args.dist_backend == "nccl"
+    use_graph = args.graph == "on" or (args.graph == "auto" and (world == 1 or xg is not None or graph_pg))
     warm_eager = min(args.warmup, 3)
     for _ in range(warm_eager):
         tr.step()
@@ -387,6 +392,10 @@ def main(argv=None) -> int:
     def pg_mode():
         tr.enable_xgmi(None)
         tr.allreduce = lambda g: dist.all_reduce(g)
+        tr.step()  # eager first: anything lazily set up by the collective happens outside capture
+        if use_graph and graph_pg:
+            tr.capture(warmup=0, unroll=args.unroll)
+            return getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
         return lambda n: [tr.step() for _ in range(n)]
 
     autotune = None
@@ -420,12 +429,14 @@ def main(argv=None) -> int:
         run_x2 = xgmi_mode(True)
         t_x2 = clock(run_x2, n_at)
         run_pg = pg_mode()
+        pg_graph = use_graph and graph_pg
         run_pg(2)
-        t_p = clock(run_pg, args.autotune)
+        n_pg = n_at if pg_graph else args.autotune
+        t_p = clock(run_pg, n_pg)
         autotune = {"xgmi_ms": round(t_x * 1e3, 4), "xgmi_two_shot_ms": round(t_x2 * 1e3, 4),
-                    "pg_ms": round(t_p * 1e3, 4), "steps": n_at, "pg_steps": args.autotune}
+                    "pg_ms": round(t_p * 1e3, 4), "pg_hipgraph": pg_graph, "steps": n_at, "pg_steps": n_pg}
         if t_p < min(t_x, t_x2):
-            run, use_graph = run_pg, False
+            run, use_graph = run_pg, pg_graph
             collective = "rccl" if args.dist_backend == "nccl" else "gloo"
             xg_keep = xg
             xg = None
@@ -491,11 +502,11 @@ def main(argv=None) -> int:
             # group's all-reduce and time the K steps again
             xgmi_fallback = "barrier timeout" if xg.error() else "replicas diverged"
             print(f"xgmi exchange failed ({xgmi_fallback}); re-timing with the process group", file=sys.stderr)
-            run = pg_mode()
             flat = tr.get_flat()
             dist.broadcast(flat, 0)
             tr.set_flat(flat)
-            use_graph, collective = False, ("rccl" if args.dist_backend == "nccl" else "gloo")
+            run = pg_mode()
+            use_graph, collective = use_graph and graph_pg, ("rccl" if args.dist_backend == "nccl" else "gloo")
             run(3)
             elapsed = timed()
             replicas_identical = replicas_agree()

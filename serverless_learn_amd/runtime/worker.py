@@ -416,6 +416,8 @@ class Worker:
         self._drop_xgmi(healthy=not self.group.broken)
         self._ensure_resumed(v.get("resume_file", 0))
         with trace.span("regroup", epoch=v["epoch"], world=v["world"]):
+            if self.trainer is not None:
+                self.trainer.graph = None  # a captured step may embed the old communicator
             ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"])
             if not ok:
                 self._stop.wait(0.2)
@@ -521,7 +523,8 @@ class Worker:
             if bucketed:
                 t.bucket_hook = want_hook
                 t.bucket_wait = self._bucket_wait if want_hook else None
-                t.graph = None
+            if hasattr(t, "graph"):
+                t.graph = None  # the captured step must be re-captured with (or without) the collective
             self._set_world(max(1, self.group.world) if self.group.active and self.group.world > 1 else 1)
 
     def _bucket_hook(self, view: torch.Tensor):
@@ -540,10 +543,17 @@ class Worker:
     # ---- training ------------------------------------------------------------------
     def _use_graph(self) -> bool:
         """hipGraph replay of whole steps: the fused GPU engines, with no host-side collective
-        inside the step (world 1, or the xGMI exchange, which is itself captured)."""
+        inside the step.  World 1 and the xGMI exchange have none; an RCCL group's all-reduce
+        (the MLP hook, the ResNet bucket all-reduces and their stream waits) is device work
+        ordered on the stream and is captured into the step graph with the kernels
+        (tests/test_rccl_gpu.py).  A gloo group's collectives run on the host: eager steps.
+        The captured graph embeds the communicator, so every re-form drops it
+        (``_maybe_regroup``)."""
         t = self.trainer
-        return (self.cfg.graph and self.device.type == "cuda" and hasattr(t, "capture")
-                and t.allreduce is None and getattr(t, "bucket_hook", None) is None)
+        if not (self.cfg.graph and self.device.type == "cuda" and hasattr(t, "capture")):
+            return False
+        host_hooks = t.allreduce is not None or getattr(t, "bucket_hook", None) is not None
+        return not host_hooks or (self.group.active and self.group.backend == "nccl")
 
     def _run_chunk(self, n: int) -> int:
         """Run exactly ``min(n, graph_steps)`` steps and return that count.

@@ -192,3 +192,35 @@ def test_training_is_deterministic_at_full_batch():
     assert bool(torch.isfinite(p1).all())
     assert torch.equal(p1, p2)
     assert s1.loss < 1.5, s1.loss
+
+
+def test_gradients_match_reference_at_headline_config():
+    """The bench configuration itself (B = 65,536, the default rows tile and the default split-K
+    slice count of the weight gradient) against the fp32 autograd reference and the
+    bf16-rounding emulation, with the bounds of test_gradients_match_reference.  The
+    references run in fp32 on the GPU (torch matmul, no reduced-precision path on gfx950)."""
+    from serverless_learn_amd.ops import _native
+
+    B = 65536
+    x, y = _data(B, seed=13)
+    flat = M.init_params(6)
+    tr = M.FusedMLPTrainer(batch=B, flat=flat, momentum=0.0)
+    assert tr.slices == M.default_slices(B)
+    assert _native.lib().sl_mlp_rows_bm(B) in (64, 128, 256)
+    tr.load_shard(x, y)
+    g = tr.compute_grads().double().cpu()
+    torch.cuda.synchronize()
+    xd, yd, fd = x.cuda(), y.cuda(), flat.cuda()
+    loss, correct, gref = M.reference_grads(fd, xd, yd, 1.0 / B)
+    _, _, gemu = M.reference_grads_bf16(fd, xd, yd, 1.0 / B)
+    gref, gemu = gref.double().cpu(), gemu.double().cpu()
+    for name, shape, off, n in M.param_layout():
+        a, b, e = g[off:off + n], gref[off:off + n], gemu[off:off + n]
+        cos = torch.nn.functional.cosine_similarity(a, b, dim=0)
+        assert cos > 0.995, (name, float(cos))
+        assert float((a - b).norm() / b.norm()) < 5e-2, (name, float((a - b).norm() / b.norm()))
+        assert float((a - e).norm() / e.norm()) < 5e-3, (name, float((a - e).norm() / e.norm()))
+        assert _rel(a, e) < 2e-2, (name, _rel(a, e))
+    st = tr.stats()
+    assert abs(st.loss - float(loss) / B) < 2e-2
+    assert abs(st.accuracy - float(correct) / B) < 0.02
