@@ -336,6 +336,8 @@ def main(argv=None) -> int:
 
         tr = FusedMLPTrainer(batch=B, device=dev, lr=args.lr, momentum=args.momentum, world_size=world, seed=0)
         n_params, model_name = N_PARAMS, "mlp-784-256-256-10"
+        if os.environ.get("SL_CLOCK_PROBE") == "1":  # diagnostics: per-step wall time + shader clock
+            tr.enable_clock_probe()
     else:
         from serverless_learn_amd.models.resnet_engine import FusedResNetTrainer
 
@@ -519,6 +521,12 @@ def main(argv=None) -> int:
         out["settled_samples_per_s"] = round(args.batch * args.steps / settled, 1)
     if xgmi_fallback:
         out["xgmi_fallback"] = xgmi_fallback
+    if getattr(tr, "probe", None) is not None:
+        rec = tr.clock_probe_records()
+        iv = [((b[1] - a[1]) / 100.0, (b[0] - a[0]) / max(1, b[1] - a[1]) * 0.1) for a, b in zip(rec, rec[1:])]
+        w0 = min(args.warmup, 3) + (args.warmup - min(args.warmup, 3))  # steps before the timed region
+        out["clock_probe"] = {"n": len(rec), "timed_from": w0,
+                              "intervals_us_ghz": [[round(u, 2), round(gz, 3)] for u, gz in iv[:w0 + args.steps + 40]]}
     if autotune:
         out["allreduce_autotune"] = autotune
     if rank == 0:

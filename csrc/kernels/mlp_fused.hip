@@ -1974,6 +1974,7 @@ struct SgdArgs {
   float xa, xb;
   int mode;  // 0: refresh bf16 shadows from w; 1: reduce only (grad_out); 2: reduce/read + update
   uint16_t *w1h, *w2h, *w2th, *w3h, *w3th;
+  uint16_t* w1f;  // optional fp16 copy of W1 in the same fragment order (mlp_fwd1.hip's operand)
   int* cursor;
   // xGMI hand-off (mode 1 only): grad_out / grad_out_alt are this rank's exchange slots 0 / 1,
   // picked by the parity of the step in flight (xgmi.h)
@@ -1986,6 +1987,7 @@ __device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) 
   if (p < P_B1) {
     const int o = (int)(p / D_IN), i = (int)(p - (long)o * D_IN);
     a.w1h[frag_off(o, i, KS1)] = h;                     // layer 1: B[k=i][n=o]
+    if (a.w1f) a.w1f[frag_off(o, i, KS1)] = __builtin_bit_cast(uint16_t, (_Float16)w);
   } else if (p >= P_W2 && p < P_B2) {
     const int q = (int)(p - P_W2), o = q >> 8, i = q & 255;
     a.w2h[frag_off(o, i, KS2)] = h;                     // layer 2: B[k=i][n=o]
@@ -2366,8 +2368,9 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
 int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_stride, const float* grad_in,
                float* grad_out, float lr, float mu, float wd, float xa, float xb, int mode, uint16_t* w1h,
                uint16_t* w2h,
-               uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, hipStream_t stream) {
-  SgdArgs a;
+               uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, uint16_t* w1f, int* cursor, hipStream_t stream) {
+  SgdArgs a = {};
+  a.w1f = w1f;
   a.w = w; a.mom = mom; a.slab = slab; a.slices = slices; a.slab_stride = slab_stride;
   a.grad_in = grad_in; a.grad_out = grad_out; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = mode;
   a.xa = xa; a.xb = xb;
@@ -2398,15 +2401,15 @@ int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa
 }
 
 int sl_mlp_sgd_xgmi(float* w, float* mom, float lr, float mu, float wd, uint16_t* w1h, uint16_t* w2h,
-                    uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, char* const* bases, unsigned* ctl,
-                    long slot_bytes, int rank, int world, long chunk4, hipStream_t stream) {
+                    uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, uint16_t* w1f, int* cursor, char* const* bases,
+                    unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, hipStream_t stream) {
   if (!w || !bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return -1;
   if (slot_bytes < ((P_N + 3) / 4) * 16 || (slot_bytes & 255)) return -1;
   if (chunk4 < 0 || (chunk4 > 0 && (chunk4 * world * 16 < slot_bytes || (chunk4 & 63)))) return -1;
   if (((uintptr_t)w | (uintptr_t)(mom ? mom : w)) & 15) return -2;
   SgdArgs a = {};
   a.w = w; a.mom = mom; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = 2;
-  a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
+  a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.w1f = w1f; a.cursor = cursor;
   XgArgs x;
   x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world; x.chunk4 = chunk4;
   const long groups = (P_N + 3) / 4;

@@ -5,10 +5,10 @@ Separate bench processes on one box spread by +-2-3 %, more than the effects bei
 measured.  Here one trainer on one batch re-captures its step graph for each arm and the
 arms alternate over R rounds of K timed steps; medians and per-round ratios are printed.
 
-Arms: rows-kernel tile heights (default "64,256"), or kernel libraries given as
-so=<path> (each loaded in-process through its own ctypes handle is not possible, so
-library arms need separate runs: use scripts/ab_env.sh for those).
-Usage: python scripts/ab_mlp_inproc.py [--bm 64,256] [--rounds 8] [--steps 50] [--batch 65536]
+Arms: rows-kernel tile heights ("--bm 64,256"), or layer-1 kernels ("--l1 fwd1,none": the
+256 x 256-tile mlp_fwd1 GEMM vs layer 1 inside the rows kernel).  Kernel libraries cannot be
+loaded side by side in one process: use scripts/ab_env.sh for those.
+Usage: python scripts/ab_mlp_inproc.py [--bm 64,256 | --l1 fwd1,none] [--rounds 8] [--steps 50] [--batch 65536]
 """
 import argparse
 import json
@@ -25,11 +25,12 @@ from serverless_learn_amd.ops import _native
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--bm", default="64,256")
+ap.add_argument("--l1", default=None, help="comma list of layer-1 kernels: fwd1, l1, none")
 ap.add_argument("--rounds", type=int, default=8)
 ap.add_argument("--steps", type=int, default=50)
 ap.add_argument("--batch", type=int, default=65536)
 a = ap.parse_args()
-arms = [int(v) for v in a.bm.split(",")]
+arms = a.l1.split(",") if a.l1 else [int(v) for v in a.bm.split(",")]
 B = a.batch
 ap_nb = int(os.environ.get("SL_AB_BATCHES", "4"))  # shard size in batches (4: X streams from HBM, as in bench.py)
 x, y = make_mnist_like(B * ap_nb, seed=0)
@@ -39,7 +40,10 @@ t = {bm: [] for bm in arms}
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for r in range(a.rounds):
     for bm in arms:
-        _native.call("sl_mlp_set_rows_bm", bm)
+        if a.l1:
+            tr.l1_kernel = None if bm == "none" else bm
+        else:
+            _native.call("sl_mlp_set_rows_bm", bm)
         tr.graph = None
         tr._lc = None
         tr._lkey = None
@@ -54,5 +58,5 @@ for r in range(a.rounds):
 res = {str(bm): {"median_us": statistics.median(v), "min_us": min(v), "all": [round(u, 2) for u in v]} for bm, v in t.items()}
 if len(arms) == 2:
     ratios = [t[arms[0]][i] / t[arms[1]][i] for i in range(a.rounds)]
-    res["ratio_%d_over_%d" % (arms[0], arms[1])] = {"median": statistics.median(ratios), "all": [round(q, 4) for q in ratios]}
+    res["ratio_%s_over_%s" % (arms[0], arms[1])] = {"median": statistics.median(ratios), "all": [round(q, 4) for q in ratios]}
 print(json.dumps(res, indent=1))

@@ -58,6 +58,7 @@ def param_layout():
 
 
 N_PARAMS = sum(math.prod(s) for _, s in LAYOUT)  # 269,322
+N_PARAMS_B1 = HIDDEN * D_IN  # offset of fc1.bias in the flat vector
 
 
 def norm_coeffs(mean: float = MNIST_MEAN, std: float = MNIST_STD) -> tuple[float, float]:
@@ -117,18 +118,25 @@ def reference_grads(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor,
     return losses.detach().sum(), correct.detach(), w.grad.detach()
 
 
-def reference_grads_bf16(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor, grad_scale: float):
+def reference_grads_bf16(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor, grad_scale: float,
+                         l1: str = "bf16"):
     """fp32 math with bf16 rounding at exactly the points the fused kernels round.
 
     A tight check of csrc/kernels/mlp_fused.hip: any indexing/layout bug shows
     up as an O(1) error, while legitimate differences are fp32 summation order.
-    Returns (loss_sum, correct, grad_flat).
+    ``l1="fp16"`` rounds layer 1 the way mlp_fwd1.hip does (exact normalised pixels,
+    fp16 W1) instead of bf16 Xn and bf16 W1.  Returns (loss_sum, correct, grad_flat).
     """
     r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
     v = {k: t.detach().float() for k, t in views(flat).items()}
     a, b = norm_coeffs()
-    xn = r(x_u8.reshape(-1, D_IN).float() * a + b)
-    w1, w2, w3 = r(v["fc1.weight"]), r(v["fc2.weight"]), r(v["fc3.weight"])
+    if l1 == "fp16":
+        xn = x_u8.reshape(-1, D_IN).float() * a + b
+        w1 = v["fc1.weight"].to(torch.float16).float()
+    else:
+        xn = r(x_u8.reshape(-1, D_IN).float() * a + b)
+        w1 = r(v["fc1.weight"])
+    w2, w3 = r(v["fc2.weight"]), r(v["fc3.weight"])
     p1 = xn @ w1.t() + v["fc1.bias"]
     h1 = r(torch.relu(p1))
     p2 = h1 @ w2.t() + v["fc2.bias"]
@@ -306,10 +314,15 @@ class FusedMLPTrainer:
         self.slab = torch.empty(self.slices, self.slab_stride, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
-        # layer 1 of the train step as a separate 128-row-tile GEMM (mlp_l1_kernel) when SL_MLP_L1=1.
-        # Off by default: it takes 49 us against the ~32 us that layer 1 costs inside the row-fused
-        # kernel (22 % MFMA busy, latency-bound; profiles/r01_v10)
-        self.l1_gemm = batch % 128 == 0 and os.environ.get("SL_MLP_L1", "0") == "1"
+        # fp16 copy of W1 in the same fragment order, written with the bf16 shadows (k >= 784 stays 0)
+        self.w1f = torch.zeros(HIDDEN, D_IN_PAD, dtype=torch.float16, device=dev)
+        # Layer 1 of the train step: with SL_MLP_FWD1=1 (batch % 256 == 0) its own 256 x 256-tile
+        # GEMM, mlp_fwd1_kernel (csrc/kernels/mlp_fwd1.hip: exact fp16 (1024 + u) pixels, LDS-DMA
+        # ring), after which the rows kernel starts at layer 2 from H1; by default layer 1 runs
+        # inside the rows kernel; SL_MLP_L1=1 selects the older 128-row-tile GEMM (profiles/r01_v10).
+        l1 = os.environ.get("SL_MLP_L1", "0") == "1" and batch % 128 == 0
+        fwd1 = os.environ.get("SL_MLP_FWD1", "0") == "1" and batch % 256 == 0 and not l1
+        self.l1_kernel = "fwd1" if fwd1 else ("l1" if l1 else None)
         self.allreduce = None  # callable(grad_tensor) -> None, sums in place (RCCL)
         self.xgmi = None       # parallel.xgmi.XgmiExchange: all-reduce fused into the update (no RCCL)
         self.x = self.y = None
@@ -319,6 +332,16 @@ class FusedMLPTrainer:
 
     n_params = N_PARAMS
     model_name = "mlp-784-256-256-10"
+
+    @property
+    def l1_gemm(self) -> bool:
+        """Layer 1 runs as its own launch (mlp_fwd1 or mlp_l1) and the rows kernel starts at H1."""
+        return self.l1_kernel is not None
+
+    @property
+    def l1_numerics(self) -> str:
+        """Where layer 1 rounds: "fp16" (mlp_fwd1: exact pixels, fp16 W1) or "bf16" (bf16 Xn and W1)."""
+        return "fp16" if self.l1_kernel == "fwd1" else "bf16"
 
     def layout(self):
         return [[n, list(s), o] for n, s, o, _ in param_layout()]
@@ -345,7 +368,7 @@ class FusedMLPTrainer:
         n = self._n
         n.call("sl_mlp_sgd", n.ptr(self.params), None, None, 0, 0, None, None, 0.0, 0.0, 0.0, self.xa, self.xb, 0,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
-               None, n.stream_ptr())
+               n.ptr(self.w1f), None, n.stream_ptr())
 
     @property
     def dh1_scale(self) -> float:
@@ -358,11 +381,12 @@ class FusedMLPTrainer:
     def _launches(self):
         """Cached launches for the current buffers/hyper-parameters (rebuilt on change)."""
         key = (self.x.data_ptr() if self.x is not None else 0, self.n_batches, self.grad_scale, self.lr,
-               self.momentum, self.weight_decay, id(self.xgmi), bool(self.xgmi and self.xgmi.two_shot))
+               self.momentum, self.weight_decay, id(self.xgmi), bool(self.xgmi and self.xgmi.two_shot),
+               self.l1_kernel)
         if getattr(self, "_lkey", None) == key:
             return self._lc
         n, p = self._n, self._n.ptr
-        ws = (p(self.w1h), p(self.w2h), p(self.w2th), p(self.w3h), p(self.w3th))
+        ws = (p(self.w1h), p(self.w2h), p(self.w2th), p(self.w3h), p(self.w3th), p(self.w1f))
         lc = {
             "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
                              p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
@@ -373,7 +397,10 @@ class FusedMLPTrainer:
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
                               self.slices, self.slab_stride),
         }
-        if self.l1_gemm:
+        if self.l1_kernel == "fwd1":
+            lc["l1"] = n.Launch("sl_mlp_fwd1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1f),
+                                p(self.params[N_PARAMS_B1:]), self.xa, self.xb, p(self.h1t))
+        elif self.l1_kernel == "l1":
             lc["l1"] = n.Launch("sl_mlp_l1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1h),
                                 p(self.params), self.xa, self.xb, p(self.h1t))
         for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
@@ -452,7 +479,23 @@ class FusedMLPTrainer:
         self.graph = None
         self._lkey = None
 
+    def enable_clock_probe(self, cap: int = 4096) -> None:
+        """Diagnostics (bench.py SL_CLOCK_PROBE=1): a one-lane kernel stamps (shader clock,
+        100 MHz wall clock) at the start of every step, inside the captured graphs too."""
+        self.probe_buf = torch.zeros(2 * cap, dtype=torch.int64, device=self.device)
+        self.probe_cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.probe = self._n.Launch("sl_clock_probe", self._n.ptr(self.probe_buf), self._n.ptr(self.probe_cnt), cap)
+        self.graph = None
+
+    def clock_probe_records(self) -> list:
+        """[(shader_ticks, wall_ticks_100MHz)] in launch order."""
+        n = min(int(self.probe_cnt.item()), self.probe_buf.numel() // 2)
+        v = self.probe_buf[:2 * n].view(n, 2).cpu().tolist()
+        return [tuple(t) for t in v]
+
     def _step_eager(self) -> None:
+        if getattr(self, "probe", None) is not None:
+            self.probe()
         self._rows(True)
         self._wgrad()
         if self.xgmi is not None:

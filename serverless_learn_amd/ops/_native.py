@@ -40,9 +40,11 @@ _SIGS: dict[str, list] = {
     "sl_conv_set_phase": [I],
     "sl_mlp_rows_bm": [I],
     "sl_mlp_set_stamps": [P],
-    "sl_mlp_sgd": [P, P, P, I, L, P, P, F, F, F, F, F, I, P, P, P, P, P, P, P],
+    "sl_mlp_sgd": [P, P, P, I, L, P, P, F, F, F, F, F, I, P, P, P, P, P, P, P, P],
     "sl_mlp_reduce_xgmi": [P, I, L, F, F, P, P, P, P],
-    "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, L, P],
+    "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, P, L, I, I, L, P],
+    "sl_mlp_fwd1": [P, P, I, I, P, P, F, F, P, P],
+    "sl_clock_probe": [P, P, I, P],
 }
 _RESTYPE = {"sl_mlp_param_count": ctypes.c_long, "sl_mlp_slab_stride": ctypes.c_long}
 

@@ -163,7 +163,7 @@ class WgradWorkspace:
     (:func:`wgrad_side_begin`) does not block the next weight gradient's slab."""
 
     def __init__(self, device, floats: int = 0, alternate: bool = False):
-        self.device = device
+        self.device = torch.device(device)
         self.bufs = [torch.empty(max(4, floats), dtype=torch.float32, device=device)
                      for _ in range(2 if alternate else 1)]
         self.i = 0

@@ -37,9 +37,9 @@ def rows_bm():
     _native.call("sl_mlp_set_rows_bm", 0)
 
 
-@pytest.mark.parametrize("batch,bm,l1", [(64, 64, True), (512, 64, True), (2048, 64, True), (512, 128, True),
-                                         (2048, 128, True), (2048, 64, False), (512, 128, False),
-                                         (512, 256, False), (2048, 256, False)])
+@pytest.mark.parametrize("batch,bm,l1", [(64, 64, None), (512, 64, "fwd1"), (2048, 64, "fwd1"), (512, 128, "fwd1"),
+                                         (2048, 128, "l1"), (512, 64, "l1"), (2048, 64, None), (512, 128, None),
+                                         (512, 256, None), (2048, 256, None)])
 def test_gradients_match_reference(batch, bm, l1, rows_bm):
     from serverless_learn_amd.ops import _native
 
@@ -48,12 +48,12 @@ def test_gradients_match_reference(batch, bm, l1, rows_bm):
     x, y = _data(batch, seed=3)
     flat = M.init_params(2)
     tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
-    tr.l1_gemm = l1 and batch % 128 == 0  # layer 1 as the separate GEMM or inside the rows kernel
+    tr.l1_kernel = l1  # layer 1 as mlp_fwd1 / mlp_l1, or inside the rows kernel (None)
     tr.load_shard(x, y)
     g = tr.compute_grads().cpu()
     torch.cuda.synchronize()
     loss, correct, gref = M.reference_grads(flat, x, y, 1.0 / batch)
-    _, _, gemu = M.reference_grads_bf16(flat, x, y, 1.0 / batch)
+    _, _, gemu = M.reference_grads_bf16(flat, x, y, 1.0 / batch, l1=tr.l1_numerics)
     for name, shape, off, n in M.param_layout():
         a, b, e = g[off:off + n], gref[off:off + n], gemu[off:off + n]
         # vs the true fp32 gradient: bf16 operand rounding only
@@ -74,14 +74,41 @@ def test_layer1_gemm_matches_row_fused_layer1():
     x, y = _data(batch, seed=7)
     flat = M.init_params(4)
     h = []
-    for l1 in (True, False):
+    for l1 in ("l1", None):
         tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
-        tr.l1_gemm = l1
+        tr.l1_kernel = l1
         tr.load_shard(x, y)
         tr.compute_grads()
         torch.cuda.synchronize()
         h.append(tr.h1t.clone())
     assert torch.equal(h[0], h[1]), float((h[0].float() - h[1].float()).abs().max())
+
+
+def test_fwd1_layer1_matches_fp32_reference():
+    """mlp_fwd1_kernel (exact fp16 (1024 + u) pixels against fp16 W1, S-corrected) gives
+    H1 = relu(Xn W1^T + b1) to fp16-weight precision, on a batch whose rows come from the
+    second batch of the shard (device cursor), including the padded K chunk."""
+    batch = 1024
+    x, y = _data(batch * 2, seed=17)
+    flat = M.init_params(8)
+    tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
+    tr.l1_kernel = "fwd1"
+    tr.load_shard(x, y)
+    tr.cursor.fill_(1)
+    tr._launches()["l1"]()
+    torch.cuda.synchronize()
+    h = tr.h1t.float().cpu()
+    v = M.views(flat)
+    a, b = M.norm_coeffs()
+    xn = x[batch:].float() * a + b
+    w16 = v["fc1.weight"].to(torch.float16).float()
+    ref = torch.relu(xn.double() @ w16.double().t() + v["fc1.bias"].double()).float()
+    ref_bf = ref.to(torch.bfloat16).float()
+    # bf16 output rounding (2^-9 relative) plus fp32 accumulation of the 1024-offset products
+    err = (h - ref).abs()
+    assert float(err.max()) < 1e-2 * float(ref.abs().max()), float(err.max())
+    assert float((h - ref_bf).abs().max()) <= 2 * float((ref - ref_bf).abs().max()) + 1e-4
+    assert (h > 0).eq(ref > 1e-3).float().mean() > 0.999
 
 
 def test_sgd_step_matches_reference():
