@@ -39,65 +39,6 @@
 
 using namespace sl;
 
-#ifndef SL_MLP_RING4
-#define SL_MLP_RING4 4
-#endif
-#ifndef SL_MLP_RING2
-#define SL_MLP_RING2 4
-#endif
-#ifndef SL_ROWS128_WMG
-#define SL_ROWS128_WMG 2  // row groups of the 128-row rows-kernel tile (1: each wave 128 rows x 32 features)
-#endif
-#ifndef SL_MLP_SLICES
-#define SL_MLP_SLICES 28  // weight-gradient K slices: 9 tiles x 28 = 252 GEMM workgroups
-#endif
-#ifndef SL_L1_KO
-#define SL_L1_KO 0  // timing knockouts of mlp_l1_kernel (1 X loads, 2 X conversion, 3 MFMAs, 4 W1 loads)
-#endif
-#ifndef SL_WG_W128
-#define SL_WG_W128 1  // wgrad waves cover 128 m x 32 n (2 x 4 waves; half the u8 conversions) instead of 64 x 64
-#endif
-#ifndef SL_WG_CVT
-#define SL_WG_CVT 1  // wgrad u8 B-fragment conversions scheduled under the MFMAs of the previous k-step
-#endif
-#ifndef SL_WG_MFMA32
-#define SL_WG_MFMA32 0  // weight gradient on v_mfma_f32_32x32x16 (4 x 1 tiles of 32 x 32 per wave) instead of 16x16x32
-#endif
-#ifndef SL_WG_PIPE
-#define SL_WG_PIPE 1  // software-pipelined wgrad main loop (0: the plain loop)
-#endif
-#ifndef SL_WG_KO
-#define SL_WG_KO 0  // timing knockouts of mlp_wgrad_kernel (1 no MFMAs, 2 no LDS-DMA after stage 0)
-#endif
-#ifndef SL_MLP_ONEIMG
-#define SL_MLP_ONEIMG 0  // rows kernel: one activation image (3 workgroups per CU)
-#endif
-#ifndef SL_MLP_RING_ONE
-#define SL_MLP_RING_ONE 3  // weight ring depth of the one-image kernel (register budget 168)
-#endif
-#ifndef SL_MLP_APF
-#define SL_MLP_APF 1  // rows kernel: prefetch the next k-step's A fragments (3-slot X ring)
-#endif
-#ifndef SL_ROWS_KO
-#define SL_ROWS_KO 0  // timing knockouts of mlp_rows_kernel (1: every wave streams wave 0's weight columns, 2: no X loads,
-                     // 3: 256-row tile, no W1 reloads in layer 1, 4: 256-row tile, no barriers in layer 1)
-#endif
-#ifndef SL_MLP_XW
-#define SL_MLP_XW 128  // rows kernel layer 1: X chunk width (128: one barrier per 4 k-steps, ring over R0+R1; 64: per 2)
-#endif
-#ifndef SL_MLP_XQ
-#define SL_MLP_XQ 13  // X prefetch distance in 64-column chunks: 13 = every chunk's load issued up front
-                      // (+1.5 % MLP over 4, profiles/r03_xq; 4 measured +1 % over 2 in round 1)
-#endif
-#ifndef SL_MLP_XQ256
-#define SL_MLP_XQ256 2  // the same for the 256-row tile (2 uint4 per thread and chunk: registers are short)
-#endif
-#ifndef SL_MLP_APF256
-#define SL_MLP_APF256 0  // A-fragment prefetch in the 256-row tile (64 more VGPRs)
-#endif
-#ifndef SL_MLP_RING256
-#define SL_MLP_RING256 2  // weight ring depth of the 256-row tile
-#endif
 namespace {
 constexpr int D_IN = 784;   // input features (28x28)
 constexpr int D_INP = 832;  // layer-1 K padded to 13 chunks of 64 (w1h row stride)
@@ -316,41 +257,29 @@ __device__ __forceinline__ void copy_part_buf(const uint16_t* src, int ld, __amd
   }
 }
 
-// BM batch rows per workgroup, BM/16 waves.  Wave w owns 16*NF output columns
-// (NF = 256 / (16 * waves)) for ALL BM rows, so one weight fragment a wave
-// streams from L2 feeds MF = BM/16 MFMAs: BM = 128 halves the weight traffic
-// per FLOP of BM = 64 (the rows kernel's limiter, profiles/r01_v6).
-// WMG > 1 splits the waves into WMG row groups (each 16 * MF rows) so that the
-// NF weight fragments a wave streams feed MF m-fragments while halving the
-// LDS A-fragment traffic of the 1 x 8 layout at BM = 128.
-// L1 = false: H1 was already computed by mlp_l1_kernel (train path); the tile is
-// staged from global into R1 and layer 1 / its H1 write are skipped.
-// ONE (SL_MLP_ONEIMG, 64-row tiles): a single activation image instead of two --
-// H2 overwrites H1 after layer 2 (the H1 ReLU mask survives as 4-bit bytes) and
-// dH1 overwrites dH2 -- so the LDS footprint drops from 72.7 KB to 42.8 KB and
-// three workgroups fit on a CU.
-//
-// BM = 256 (one 8-wave workgroup per CU, 2 x 4 waves of 128 rows x 64 features): every
-// weight fragment a wave streams from L2 feeds 8 MFMAs instead of 4, so the weight stream
-// per CU is half that of the 64- and 128-row tiles (32 KB per 1,024 MFMA cycles per SIMD
-// instead of per 512: those tiles ask the CU's vector-memory path for ~64 B/clk, its
-// limit).  At B = 65,536 the grid is exactly one workgroup per CU.  It runs the ONE
-// layout (one activation image + H1 nibble mask + a 16-column dZ image = 156 KB of LDS),
-// two X row passes per thread, a 2-deep weight ring and no A prefetch (register budget:
-// 128 accumulators of 256).
+// Two tile heights.  BM = 64 (the default): 4 waves, wave w owns features 64 w .. 64 w + 63
+// for all 64 rows, two workgroups per CU overlap each other's epilogues.  BM = 256 (opt-in,
+// SL_MLP_ROWS_BM=256; one 8-wave workgroup per CU, 2 x 4 waves of 128 rows x 64 features):
+// every weight fragment a wave streams from L2 feeds 8 MFMAs instead of 4, half the weight
+// stream per CU; it runs one activation image + an H1 nibble mask + a 16-column dZ image
+// (156 KB of LDS), two X row passes per thread, a 2-deep weight ring and no A prefetch
+// (register budget: 128 accumulators of 256); profiles/r03_big.
+// L1 = false (BM = 64 only): H1 was already computed by mlp_fwd1_kernel (mlp_fwd1.hip);
+// the tile is staged from global into R1 and layer 1 / its H1 write are skipped.
 template <int BM> constexpr int rows_nwv() { return BM == 256 ? 8 : BM / 16; }
 template <bool TRAIN, int BM, int WMG, bool L1 = true>
-__global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 : 2) : 1) void mlp_rows_kernel(MlpRowArgs a) {
+__global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpRowArgs a) {
   constexpr int NWV = rows_nwv<BM>();  // waves per workgroup
   constexpr int MF = BM / 16 / WMG;    // m-fragments per wave
   constexpr int NT = NWV * 64;         // threads
   constexpr int NF = 16 * WMG / NWV;   // n-fragments per wave
   constexpr bool BIG = BM == 256;
-  constexpr bool ONE = ((SL_MLP_ONEIMG && BM == 64) || BIG) && L1;
+  static_assert(BM == 64 || BM == 256, "64- or 256-row tiles");
+  constexpr bool ONE = BIG;  // one activation image (+ H1 nibble mask)
   static_assert(!BIG || L1, "the 256-row tile has no train == 2 form");
-  constexpr int RING = BIG ? SL_MLP_RING256 : ONE ? SL_MLP_RING_ONE : (NF >= 4 ? SL_MLP_RING4 : SL_MLP_RING2);  // weight ring depth (k-steps)
-  constexpr bool APF = BIG ? SL_MLP_APF256 : SL_MLP_APF;  // prefetch the next k-step's A fragments
-  constexpr int XQ = BIG ? SL_MLP_XQ256 : SL_MLP_XQ;      // X chunks waiting in registers
+  constexpr int RING = BIG ? 2 : 4;  // weight ring depth (k-steps)
+  constexpr bool APF = !BIG;         // prefetch the next k-step's A fragments
+  constexpr int XQ = 2;              // BIG: X chunks waiting in registers
   constexpr int XP = BM * 4 / NT;                          // X row passes per thread (16 columns each)
   constexpr int DZL = BIG ? DZ_LD256 : DZ_LD;
   constexpr int SPW = BM / 16 / NWV;                       // 16-row softmax blocks per wave
@@ -416,22 +345,8 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
   const float nxa = a.xa + 0.f * (float)lane, nxb = a.xb + 0.f * (float)lane;
   // X row pass p covers rows xrow + p * NT / 4
   auto xload = [&](int c, int p = 0) -> uint4 {
-    if (SL_ROWS_KO == 2) return make_uint4(c, xrow, 7, 9);
-    if (SL_ROWS_KO == 5)  // timing knockout: the same bytes as contiguous 16 KB blocks per chunk (wrong data)
-      return *reinterpret_cast<const uint4*>(a.x + (srow0 - row0 + row0) * D_IN +
-                                             ((long)c * BM * 64 + (long)p * NT * 16 + tid * 16) % ((long)BM * D_IN));
     return (c * 64 + xcol < D_IN) ? *reinterpret_cast<const uint4*>(xg + (long)p * (NT / 4) * D_IN + c * 64)
                                   : make_uint4(0, 0, 0, 0);
-  };
-  auto xstore = [&](int c, uint4 v, int p = 0) {
-    uint16_t* d = R0 + (APF ? c % 3 : c & 1) * BM * XC_LD + (xrow + p * (NT / 4)) * XC_LD + xcol;
-    short8_t lo = zero8(), hi = zero8();
-    if (c * 64 + xcol < D_IN) {
-      lo = u8x8_to_bf16(make_uint2(v.x, v.y), nxa, nxb);
-      hi = u8x8_to_bf16(make_uint2(v.z, v.w), nxa, nxb);
-    }
-    *reinterpret_cast<short8_t*>(d) = lo;
-    *reinterpret_cast<short8_t*>(d + 8) = hi;
   };
   auto zero_acc = [&]() {
 #pragma unroll
@@ -538,7 +453,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
     }
   };
 
-  const int wcol = SL_ROWS_KO == 1 ? 0 : NF * wng;
+  const int wcol = NF * wng;
   const FragSrc f_w1(a.w1h, HID * D_INP * 2, wcol, KS1, lane);
   const FragSrc f_w2(a.w2h, HID * HID * 2, wcol, KS2, lane);
   const FragSrc f_w2t(a.w2th, HID * HID * 2, wcol, KS2, lane);
@@ -560,7 +475,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
     stamp(1);
   } else {
   zero_acc();
-  constexpr bool XWIDE = SL_MLP_XW == 128 && APF && !ONE;
+  constexpr bool XWIDE = APF && !ONE;
   if constexpr (XWIDE) {
     // 128-column X chunks: 7 chunks, one barrier per four k-steps instead of per
     // two. The 3-slot ring (144-element rows: ds_read_b128 conflict-free) spans
@@ -612,26 +527,9 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
           }
         });
   } else {
-    // X chunks c+1 .. c+XQ wait in registers (slot chunk % XQ): the u8 input
-    // comes from HBM, so its prefetch distance is set apart from the weight ring
-    uint4 xq[XQ][XP];
-    if constexpr (!BIG) {
-#pragma unroll
-      for (int i = 1; i <= XQ; ++i)
-#pragma unroll
-        for (int p = 0; p < XP; ++p) xq[i % XQ][p] = i < NCHUNK ? xload(i, p) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int p = 0; p < XP; ++p) xstore(0, xload(0, p), p);
-      bar();
-    }
-    auto xnext = [&](int c) {  // convert chunk c+1 into its ring slot, refill its register slot
-#pragma unroll
-      for (int p = 0; p < XP; ++p) {
-        if (c + 1 < NCHUNK) xstore(c + 1, xq[(c + 1) % XQ][p], p);
-        if (c + 1 + XQ < NCHUNK) xq[(c + 1) % XQ][p] = xload(c + 1 + XQ, p);
-      }
-    };
-    if constexpr (BIG) {
+    static_assert(BIG, "the 64-row tile runs the 128-column X ring above");
+    uint4 xq[XQ][XP];  // X chunks waiting in registers (the u8 input comes from HBM)
+    {
       // 256-row tile: a 4-slot ring of unpadded 64-column bf16 chunks (4 x 32 KB; 16-B
       // pieces XOR-swizzled by (row / 2) % 8, which keeps the A-fragment ds_read_b128
       // conflict-free without the 144-B padded rows), so the waves meet at one barrier
@@ -703,7 +601,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
         }
         if (conv) xput(cc, q & 1, pk);
         __builtin_amdgcn_sched_barrier(0);
-        if (st + RING < L1_KSTEPS_ROWS && SL_ROWS_KO != 3) {  // knockout 3: no W1 reloads (wrong numerics)
+        if (st + RING < L1_KSTEPS_ROWS) {
 #pragma unroll
           for (int n = 0; n < NF; ++n) r[st % RING][n] = f_w1(n, st + RING, KS1);
         }
@@ -712,46 +610,8 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
           for (int p = 0; p < XP; ++p) xq[cc & 1][p] = xload(cc + 2, p);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (q == 3 && SL_ROWS_KO != 4) bar();  // publishes chunks 2k+2, 2k+3; period k's slots are free
+        if (q == 3) bar();  // publishes chunks 2k+2, 2k+3; period k's slots are free
       }
-    } else if constexpr (APF) {
-      // 3-slot X ring: chunk c+1 is converted after the first k-step of chunk c and
-      // published by the barrier right after it, so step 2c+1 can prefetch step
-      // 2c+2's fragments; its slot last held chunk c-2, read before the barrier of
-      // step 2c-2
-      kloop_ring_a<L1_KSTEPS_ROWS, NF, MF, RING>(
-          [&](short8_t (&r)[NF], int st) {
-#pragma unroll
-            for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
-          },
-          [&](short8_t (&af)[MF], int st) {
-            const uint16_t* ab = R0 + ((st >> 1) % 3) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg;
-#pragma unroll
-            for (int m = 0; m < MF; ++m) af[m] = lds8(ab + (rw + m * 16) * XC_LD);
-          },
-          mfma_ab,
-          [&](int st) {
-            if (!(st & 1)) {
-              xnext(st >> 1);
-              bar();
-            }
-          });
-    } else {
-      kloop_ring<L1_KSTEPS_ROWS, NF, RING>(
-          [&](short8_t (&r)[NF], int st) {
-#pragma unroll
-            for (int n = 0; n < NF; ++n) r[n] = f_w1(n, st, KS1);
-          },
-          [&](int st, short8_t (&b)[NF]) {
-            mfma_step(R0 + ((st >> 1) & 1) * BM * XC_LD + lr * XC_LD + (st & 1) * 32 + 8 * lg, XC_LD, b);
-          },
-          [&](int st) {
-            // chunk c+1 is converted into the free ring slot after the FIRST k-step of
-            // chunk c (that slot's readers all passed the barrier that ended chunk c-1);
-            // the barrier after the second k-step publishes it
-            if (!(st & 1)) xnext(st >> 1);
-            else bar();
-          });
     }
   }
   stamp(1);
@@ -1038,177 +898,6 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? (SL_MLP_ONEIMG ? 3 
 
 
 // ---------------------------------------------------------------------------
-// Layer-1 forward of the train step as a weight-efficient GEMM:
-//   H1 = relu(Xn W1^T + b1)   (bf16 [batch][256] for the rows kernel and wgrad)
-// 128 x 128 tiles, 4 waves of 64 x 64, two workgroups per CU.  Inside the row-fused kernel every
-// 64-row workgroup streams all of W1 (426 KB) from L2 -- 32 KB per 64-wide K
-// chunk per 64 rows, more than L2 can feed the MFMAs (layer 1 was 47 % of that
-// kernel's cycles, profiles/r01_v11).  Here one staging of a W1 chunk in LDS
-// serves 128 rows (2x less L2 traffic per row) and every X element is
-// normalised once.  Two workgroups per CU: with one 8-wave 256-row workgroup
-// the per-chunk barrier kept both waves of a SIMD in phase (MFMA bursts, then
-// conversion bursts) and the MFMA pipe was busy 22 % of the time.  The two
-// column tiles of a row block are adjacent in the XCD remap, so they read
-// their X rows through one L2.  Register-staged double buffer: the W1 pieces of chunk c+1
-// and the X pieces of chunk c+2 (HBM) are in flight during chunk c's MFMAs.
-// ---------------------------------------------------------------------------
-constexpr int L1_BM = 128, L1_BN = 128, L1_NT = 256;
-constexpr int L1_A_LD = 72;                  // [128][72] bf16 A image (144-B rows, conflict-free b128 reads)
-constexpr int L1_A = L1_BM * L1_A_LD;        // elements
-constexpr int L1_B = 16 * 512;               // 8 n-tiles x 2 k-steps of fragment-ordered W1 (16 KB)
-constexpr int L1_SLOT = L1_A + L1_B;
-constexpr int L1_KSTEPS = (D_IN + 31) / 32;  // 25: the last holds 16 real columns
-constexpr int L1_NCH = (L1_KSTEPS + 1) / 2;  // 13 chunks of 64
-constexpr int L1_O_LD = L1_BN + 8;          // epilogue image row stride
-static_assert(L1_BM * L1_O_LD <= 2 * L1_SLOT, "epilogue image must fit the ring");
-
-struct L1Args {
-  const uint8_t* x;
-  const int* cursor;
-  int n_batches, batch;
-  const uint16_t* w1h;
-  const float* b1;
-  float xa, xb;
-  uint16_t* h1;
-};
-
-__global__ __launch_bounds__(L1_NT, 2) void mlp_l1_kernel(L1Args a) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * L1_SLOT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 15, lg = lane >> 4;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const long row0 = (long)(tile >> 1) * L1_BM;
-  const int col0 = (tile & 1) * L1_BN, nt0 = col0 >> 4;
-  const long srow0 = batch_base(a.cursor, a.n_batches, a.batch) + row0;
-  const int wr = (wave & 1) * 64, wc = (wave >> 1) * 64;
-  const float nxa = a.xa + 0.f * (float)lane, nxb = a.xb + 0.f * (float)lane;  // VGPRs (constant-bus limit)
-
-  // X: 512 16-B pieces per chunk, rows tid/4 and tid/4 + 64
-  const int xr = tid >> 2, xc = (tid & 3) * 16;
-  const uint8_t* xg = a.x + (srow0 + xr) * D_IN + xc;
-  auto xload = [&](int c, uint4 (&v)[2]) {
-    const bool ok = c * 64 + xc < D_IN;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#if SL_L1_KO == 1
-      v[j] = make_uint4(c, j, 0, 0);
-#else
-      v[j] = ok ? *reinterpret_cast<const uint4*>(xg + (long)j * 64 * D_IN + c * 64) : make_uint4(0, 0, 0, 0);
-#endif
-  };
-  auto xstore = [&](int slot, int c, const uint4 (&v)[2]) {
-    const bool ok = c * 64 + xc < D_IN;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      uint16_t* d = smem + slot * L1_SLOT + (xr + 64 * j) * L1_A_LD + xc;
-#if SL_L1_KO == 2
-      *reinterpret_cast<uint4*>(d) = v[j];
-      *reinterpret_cast<uint4*>(d + 8) = v[j];
-#else
-      *reinterpret_cast<short8_t*>(d) = ok ? u8x8_to_bf16(make_uint2(v[j].x, v[j].y), nxa, nxb) : zero8();
-      *reinterpret_cast<short8_t*>(d + 8) = ok ? u8x8_to_bf16(make_uint2(v[j].z, v[j].w), nxa, nxb) : zero8();
-#endif
-    }
-  };
-  // W1: 16 fragments of 1 KB per chunk, 4 x 16 B per thread, copied in fragment order
-  auto wload = [&](int c, short8_t (&v)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = tid + L1_NT * i, blk = p >> 6, l = p & 63;
-#if SL_L1_KO == 4
-      v[i] = zero8(); v[i][0] = (short)(c + blk + l);
-#else
-      v[i] = ld8(a.w1h + (long)((nt0 + (blk >> 1)) * KS1 + 2 * c + (blk & 1)) * 512 + l * 8);
-#endif
-    }
-  };
-  auto wstore = [&](int slot, const short8_t (&v)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = tid + L1_NT * i;
-      *reinterpret_cast<short8_t*>(smem + slot * L1_SLOT + L1_A + p * 8) = v[i];
-    }
-  };
-
-  floatx4_t acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
-  auto compute = [&](int slot, int nks) {
-    const uint16_t* A = smem + slot * L1_SLOT;
-    const uint16_t* B = A + L1_A;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      if (kk < nks) {
-        short8_t af[4], bf[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) af[m] = lds8(A + (wr + m * 16 + lr) * L1_A_LD + kk * 32 + 8 * lg);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) bf[n] = lds8(B + (((wc >> 4) + n) * 2 + kk) * 512 + lane * 8);
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-#if SL_L1_KO == 3
-            acc[m][n][0] += (float)af[m][0] * (float)bf[n][1];
-#else
-            acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
-#endif
-          }
-      }
-    }
-  };
-
-  // prefetch distances (chunks): X from HBM L1_XD ahead, W1 (L2-resident) L1_WD ahead;
-  // one chunk of MFMAs is ~0.5 us, HBM latency under load ~2 us
-  constexpr int XD = 4, WD = 2;
-  uint4 xq[XD][2];
-  short8_t wq[WD][4];
-#pragma unroll
-  for (int i = 0; i < XD; ++i) xload(i, xq[i]);
-#pragma unroll
-  for (int i = 0; i < WD; ++i) wload(i, wq[i]);
-  xstore(0, 0, xq[0]);
-  wstore(0, wq[0]);
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < L1_NCH; ++c) {
-    if (c + XD < L1_NCH) xload(c + XD, xq[c % XD]);
-    if (c + WD < L1_NCH) wload(c + WD, wq[c % WD]);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(c & 1, L1_KSTEPS - 2 * c);
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < L1_NCH) {
-      xstore((c + 1) & 1, c + 1, xq[(c + 1) % XD]);
-      wstore((c + 1) & 1, wq[(c + 1) % WD]);
-    }
-    __syncthreads();
-  }
-
-  // bias + ReLU -> bf16 image over the ring, then coalesced 16-B row stores
-  uint16_t* img = smem;
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int col = wc + n * 16 + lr;
-    const float bias = a.b1[col0 + col];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        img[(wr + m * 16 + 4 * lg + r) * L1_O_LD + col] = f2bf(fmaxf(acc[m][n][r] + bias, 0.f));
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = tid; q < L1_BM * (L1_BN / 8); q += L1_NT) {
-    const int r = q >> 4, c8 = (q & 15) * 8;
-    *reinterpret_cast<short8_t*>(a.h1 + (row0 + r) * HID + col0 + c8) =
-        *reinterpret_cast<const short8_t*>(img + r * L1_O_LD + c8);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Weight-gradient grouped split-K GEMM:  G[m][n] = sum_b A[b][m] * Bop[b][n],
 // A = dH1 / dH2 ([batch][256]; dH1 fp16 scaled, dH2 bf16), Bop = raw u8 X / bf16 H1, row-major over b.
 //
@@ -1238,10 +927,7 @@ __global__ __launch_bounds__(L1_NT, 2) void mlp_l1_kernel(L1Args a) {
 // band of those columns over its slice's stages into the slice's slab, so the
 // slab carries every gradient and mlp_sgd_kernel needs no special case.
 // ---------------------------------------------------------------------------
-#ifndef SL_WG_TILED
-#define SL_WG_TILED 1  // slab in the weight-gradient kernel's register order (contiguous 1 KB per store)
-#endif
-// Tiled slab layout (SL_WG_TILED): per slice, the 9 weight-gradient tiles in the order the
+// Tiled slab layout (1): per slice, the 9 weight-gradient tiles in the order the
 // accumulators sit in the waves' registers -- tile t, wave w, store instruction (i, j), lane l,
 // 4 floats -- so every epilogue store is 1 KB of contiguous memory, then the rows kernel's
 // partial-row sums in their own layout [dW3 | db3 | pad | db1 | db2].  The row-major form wrote
@@ -1274,37 +960,26 @@ struct WgArgs {
 constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages in flight
 constexpr int WG_IMG = 64 * 128;          // one [64 k][128] bf16 image, unpadded (swizzled)
 constexpr int WG_SLOT = 3 * WG_IMG;       // A half 0, A half 1, B = 48 KB
-#ifndef SL_WG_RING4
-#define SL_WG_RING4 0  // u8 (dW1) tiles: 4 slots of 40 KB (three stages in flight) instead of 3 of 48 KB; A/B neutral (profiles/r01_v15)
-#endif
 // u8 tiles need only 8 KB of B per slot: 4 x 40 KB fill the 160 KB of LDS exactly
-constexpr int WG_NSLOT8 = SL_WG_RING4 ? 4 : WG_NSLOT;
-constexpr int WG_SLOT8 = SL_WG_RING4 ? 2 * WG_IMG + WG_IMG / 2 : WG_SLOT;
+constexpr int WG_NSLOT8 = 0 ? 4 : WG_NSLOT;
+constexpr int WG_SLOT8 = 0 ? 2 * WG_IMG + WG_IMG / 2 : WG_SLOT;
 constexpr int WG_LDS = WG_NSLOT8 * WG_SLOT8 > WG_NSLOT * WG_SLOT ? WG_NSLOT8 * WG_SLOT8 : WG_NSLOT * WG_SLOT;
 template <bool U8> constexpr int wg_ns() { return U8 ? WG_NSLOT8 : WG_NSLOT; }
 template <bool U8> constexpr int wg_slot() { return U8 ? WG_SLOT8 : WG_SLOT; }
-#if SL_WG_RING4 && !SL_WG_PIPE
-#error "SL_WG_RING4 needs the pipelined main loop"
-#endif
 
 // 16-B chunk position inside a 256-B image row.  XOR on chunk-pair bits with
 // f(r) = (r & 3) | ((r >> 3) & 1) << 2 makes every ds_read_b64_tr_b16 of the
 // transposed fragment read (rows k..k+3 and k+8..k+11 per 32-lane half)
 // conflict-free; LDS-DMA writes the image linearly, so the same involution is
 // applied to the per-lane SOURCE address (cdna_hip_programming.md rule 21).
-// The 32x32x16 form's reads (SL_WG_MFMA32) cover 4 rows x 4 chunks per 32-lane half
+// The 32x32x16 form's reads (0) cover 4 rows x 4 chunks per 32-lane half
 // (rows 8 (l >> 5) + q, columns of two 16-lane groups), on which that XOR leaves 2-way
 // bank conflicts: there chunk ^ ((r & 3) << 2) spreads the 16 (row, chunk) pairs of a half
 // over 16 distinct chunks, and the u8 image uses chunk ^ (((r >> 1) & 3) << 1).
-#if SL_WG_MFMA32
-__device__ __forceinline__ int wg_swz(int c, int r) { return c ^ ((r & 3) << 2); }
-__device__ __forceinline__ int wg_swz8(int c, int r) { return c ^ (((r >> 1) & 3) << 1); }
-#else
 __device__ __forceinline__ int wg_swz(int c, int r) { return c ^ (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
 // u8 image: 128-B rows of 8 chunks; chunk ^ ((r >> 1) & 7) puts the 16 rows a
 // 32-lane half of ds_read_b64_tr_b8 touches on 16 distinct 4-bank groups.
 __device__ __forceinline__ int wg_swz8(int c, int r) { return c ^ ((r >> 1) & 7); }
-#endif
 
 // Transposed B-style fragment (8 consecutive k rows of one column) from a
 // swizzled image.  Issued as inline asm on purpose: hipcc treats a visible
@@ -1400,18 +1075,15 @@ __device__ __forceinline__ void wg_vmcnt(int younger) {
 }
 
 constexpr int WG_NT = 512;
-constexpr int WG_MI = SL_WG_W128 ? 8 : 4;  // 16-row A (dZ) fragments per wave
-constexpr int WG_NJ = SL_WG_W128 ? 2 : 4;  // 16-column B fragments per wave
+constexpr int WG_MI = 1 ? 8 : 4;  // 16-row A (dZ) fragments per wave
+constexpr int WG_NJ = 1 ? 2 : 4;  // 16-column B fragments per wave
 constexpr int WG_NF = WG_MI + WG_NJ;       // fragments per wave per k-step
-#if SL_WG_W128 && !SL_WG_PIPE
-#error "SL_WG_W128 needs the pipelined main loop"
-#endif
 
 __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
-  const int wm = SL_WG_W128 ? (wave & 1) : (wave & 3), wn = SL_WG_W128 ? (wave >> 1) : (wave >> 2);
+  const int wm = 1 ? (wave & 1) : (wave & 3), wn = 1 ? (wave >> 1) : (wave >> 2);
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int s = logical / A.total_tiles;
@@ -1450,9 +1122,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   }
   auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % NS
     constexpr bool U8 = decltype(u8_c)::value;
-#if SL_WG_KO == 2 || SL_WG_KO == 4  // timing knockout: no operand movement (stage 0 only)
-    if (st > 0) return;
-#endif
     uint16_t* Ai = smem + (st % wg_ns<U8>()) * wg_slot<U8>();
     uint16_t* Bi = Ai + 2 * WG_IMG;
 #pragma unroll
@@ -1500,61 +1169,9 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     b_addr[j] = 2 * WG_IMG * 2 + (u8b ? wg_tr8_addr(c, lane) : wg_tr_addr(c, lane));
   }
 
-  // Instantiated per (u8, live n-blocks) and selected by a scalar branch OUTSIDE
-  // the loop (conditions inside made hipcc copy every accumulator AGPR<->VGPR).
-  auto mainloop = [&](auto u8_c, auto nb_c) {
-    constexpr bool U8 = decltype(u8_c)::value;
-    constexpr int NB = decltype(nb_c)::value;
-    constexpr int PPS = U8 ? 5 : 6;  // LDS-DMA pieces per wave per stage
-    constexpr int KB = U8 ? 4096 : 8192;  // byte offset of k-step 1 in the B image
-    for (int st = 0; st < nst; ++st) {
-      wg_vmcnt<PPS>(min(WG_NSLOT - 2, nst - 1 - st));  // this wave's pieces of stage st have landed
-      __builtin_amdgcn_s_barrier();  // ... everyone's have; the slot of stage st-1 is free
-      if (st + WG_NSLOT - 1 < nst) issue(st + WG_NSLOT - 1, u8_c);
-      if constexpr (NB > 0) {
-        const uint32_t sb = lds_base + (uint32_t)((st % WG_NSLOT) * WG_SLOT * 2);
-        short8_t a0[4], a1[4], b0[NB], b1[NB];
-        uint2v_t r0[NB], r1[NB];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a0[i] = wg_tr8<0>(sb + a_addr[i]);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if constexpr (U8) r0[j] = ds_tr8_off<0>(sb + b_addr[j]);
-          else b0[j] = wg_tr8<0>(sb + b_addr[j]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a1[i] = wg_tr8<8192>(sb + a_addr[i]);
-        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // k-step 0's reads (a1's 8 still in flight)
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (U8) {
-#pragma unroll
-          for (int j = 0; j < NB; ++j) b0[j] = u8x8_f16_biased(r0[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if constexpr (U8) r1[j] = ds_tr8_off<KB>(sb + b_addr[j]);
-          else b1[j] = wg_tr8<KB>(sb + b_addr[j]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) acc[i][j] = wg_mma<U8>(b0[j], a0[i], acc[i][j]);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (U8) {
-#pragma unroll
-          for (int j = 0; j < NB; ++j) b1[j] = u8x8_f16_biased(r1[j]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) acc[i][j] = wg_mma<U8>(b1[j], a1[i], acc[i][j]);
-      }
-    }
-  };
-  // Software-pipelined form: the fragment reads of stage st+1 are issued right
+  // Instantiated per (u8, live n-blocks) and selected by a scalar branch OUTSIDE the loop
+  // (conditions inside made hipcc copy every accumulator AGPR<->VGPR).
+  // Software-pipelined: the fragment reads of stage st+1 are issued right
   // after the barrier that publishes it and run under stage st's MFMAs (two
   // register sets).  Without it the 8 waves of the workgroup read LDS in
   // lockstep and then ran their MFMAs: ~1,000 LDS cycles + 1,024 MFMA cycles
@@ -1571,9 +1188,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     short8_t fa[2][2][WG_MI]; // [set][k-step][m-block]
     short8_t fb[2][2][NBR];   // bf16 B fragments
     uint2v_t fr[2][2][NBR];   // raw u8 B fragments (converted next to their MFMAs)
-#if SL_WG_CVT
-    short8_t fc[2][2][NBR];   // converted u8 B fragments (SL_WG_CVT schedule)
-#endif
+    short8_t fc[2][2][NBR];   // converted u8 B fragments (1 schedule)
     auto read_stage = [&](int st, auto set_c) {
       constexpr int S = decltype(set_c)::value;
       if constexpr (NB > 0) {
@@ -1652,7 +1267,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       }
       const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % NS) * SLOT * 2);
       __builtin_amdgcn_sched_barrier(0);
-#if SL_WG_CVT
       if constexpr (U8 && NB > 0) {
         // u8 -> bf16 conversions off the MFMA critical path: k-step 1's fragments
         // (landed at the end of the previous step) are converted under k-step 0's
@@ -1684,29 +1298,19 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
           }
         }
       } else
-#endif
       if constexpr (NB > 0) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           short8_t b[NBR];
 #pragma unroll
           for (int j = 0; j < NB; ++j) {
-#if SL_WG_KO == 5  // timing knockout: no u8 -> bf16 conversion (wrong numerics)
-            if constexpr (U8) {
-              typedef uint32_t u32x4k __attribute__((ext_vector_type(4)));
-              b[j] = __builtin_bit_cast(short8_t, u32x4k{fr[C][k][j][0], fr[C][k][j][1], fr[C][k][j][0], fr[C][k][j][1]});
-            }
-#else
             if constexpr (U8) b[j] = u8x8_f16_biased(fr[C][k][j]);
-#endif
             else b[j] = fb[C][k][j];
           }
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int i = q / WG_NJ, j = q % WG_NJ;
-#if SL_WG_KO != 4  // 4: no DMA and no MFMAs (reads + barriers only)
             if (j < NB) acc[i][j] = wg_mma<U8>(b[j], fa[C][k][i], acc[i][j]);
-#endif
             reads_after(sbn, k, q, nxt_c);
           }
         }
@@ -1723,12 +1327,10 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     read_stage(0, S0{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-#if SL_WG_CVT
     if constexpr (U8) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) fc[0][0][j] = u8x8_f16_biased(fr[0][0][j]);
     }
-#endif
     for (int st = 0; st < nst; st += 2) {
       step(st, S0{}, S1{});
       if (st + 1 < nst) step(st + 1, S1{}, S0{});
@@ -1737,104 +1339,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   using I4 = std::integral_constant<int, WG_NJ>;  // all n-blocks live
   using I1 = std::integral_constant<int, 1>;
   using I0 = std::integral_constant<int, 0>;
-#if SL_WG_MFMA32
-  // ---- 32x32x16 form: each wave's 128 (m) x 32 (n) output is 4 tiles of 32 x 32; a
-  // 64-row stage is 4 k-substeps of 16 x 4 MFMAs (16 per stage instead of 32) reading the
-  // same 16 A + 4 B fragments.  The next stage's 20 fragment reads are spread over the
-  // stage's 16 MFMAs (32-cycle gaps, profiles/r03_mfma). ----
-  floatx16_t acc32[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc32[i][r] = 0.f;
-  uint32_t a32[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = wm * 128 + i * 32;
-    a32[i] = (r >> 7) * WG_IMG * 2 + wg_tr_addr32(r & 127, lane);
-  }
-  const uint32_t b32 = 2 * WG_IMG * 2 + (u8b ? wg_tr8_addr32(wn * 32, lane) : wg_tr_addr32(wn * 32, lane));
-  const int live32 = __builtin_amdgcn_readfirstlane(P.n_real - n0 - wn * 32 > 0 ? 1 : 0);
-  auto mainloop32 = [&](auto u8_c, auto nb_c) {
-    constexpr bool U8 = decltype(u8_c)::value;
-    constexpr int NB = decltype(nb_c)::value;
-    constexpr int PPS = U8 ? 5 : 6;
-    constexpr int NS = wg_ns<U8>(), SLOT = wg_slot<U8>();
-    short8_t fa[2][4][4];  // [set][k-substep][m-tile]
-    short8_t fb[2][4];     // bf16 B fragments [set][k-substep]
-    uint2v_t fr[2][4];     // raw u8 B fragments
-    // fragment f of a stage: 0..15 A (substep f / 4, m-tile f % 4), 16..19 B (substep f - 16)
-    auto read_frag = [&](uint32_t sb, auto f_c, auto set_c) {
-      constexpr int f = decltype(f_c)::value, S = decltype(set_c)::value;
-      if constexpr (f < 16) {
-        fa[S][f >> 2][f & 3] = wg_tr8<(f >> 2) * 4096>(sb + a32[f & 3]);
-      } else if constexpr (NB > 0) {
-        if constexpr (U8) fr[S][f - 16] = ds_tr8_off<(f - 16) * 2048>(sb + b32);
-        else fb[S][f - 16] = wg_tr8<(f - 16) * 4096>(sb + b32);
-      }
-    };
-    auto read_stage = [&](int st, auto set_c) {
-      const uint32_t sb = lds_base + (uint32_t)((st % NS) * SLOT * 2);
-      static_for<0, 20>([&](auto f_c) { read_frag(sb, f_c, set_c); });
-    };
-    auto step = [&](int st, auto cur_c, auto nxt_c) {
-      constexpr int C = decltype(cur_c)::value;
-      if (st + 1 < nst) {
-        wg_vmcnt<PPS>(min(NS - 2, nst - 2 - st));  // stage st+1 has landed (st+2 .. may be in flight)
-        __builtin_amdgcn_s_barrier();          // ... for everyone; every wave is done reading stage st
-        if (st + NS < nst) issue(st + NS, u8_c);
-      }
-      const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % NS) * SLOT * 2);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (NB > 0) {
-        // u8 B fragments: substep s+1's conversion (4 v_perm) is issued behind substep s's
-        // first MFMA, so no MFMA waits on its own operand's conversion
-        short8_t bq[4];
-        if constexpr (U8) bq[0] = u8x8_f16_biased(fr[C][0]);
-        else bq[0] = fb[C][0];
-        static_for<0, 4>([&](auto s_c) {
-          constexpr int sub = decltype(s_c)::value;
-          static_for<0, 4>([&](auto i_c) {
-            constexpr int i = decltype(i_c)::value, q = 4 * sub + i;
-            acc32[i] = wg_mma32<U8>(bq[sub], fa[C][sub][i], acc32[i]);
-            if constexpr (i == 0 && sub + 1 < 4) {
-              if constexpr (U8) bq[sub + 1] = u8x8_f16_biased(fr[C][sub + 1]);
-              else bq[sub + 1] = fb[C][sub + 1];
-            }
-            constexpr int f0 = q * 20 / 16, f1 = (q + 1) * 20 / 16;
-            static_for<f0, f1>([&](auto f_c) { read_frag(sbn, f_c, nxt_c); });
-            if constexpr (f1 > f0) __builtin_amdgcn_sched_barrier(0);
-          });
-        });
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
-    wg_vmcnt<PPS>(min(NS - 2, nst - 1));
-    __builtin_amdgcn_s_barrier();
-    if (NS - 1 < nst) issue(NS - 1, u8_c);
-    read_stage(0, S0{});
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    for (int st = 0; st < nst; st += 2) {
-      step(st, S0{}, S1{});
-      if (st + 1 < nst) step(st + 1, S1{}, S0{});
-    }
-  };
-  if (u8b) {
-    if (live32) mainloop32(T_{}, I1{});
-    else mainloop32(T_{}, I0{});
-  } else {
-    mainloop32(F_{}, I1{});
-  }
-#elif SL_WG_KO == 1  // timing knockout: no fragment reads / MFMAs
-  if (u8b) mainloop(T_{}, I0{});
-  else mainloop(F_{}, I0{});
-#elif SL_WG_KO == 3  // timing knockout: no main loop (prologue sums + epilogue only)
-#elif SL_WG_PIPE
   if (u8b) {
     if (nvalid >= WG_NJ) mainloop_pipe(T_{}, I4{});
     else if (nvalid >= 1) mainloop_pipe(T_{}, I1{});
@@ -1842,15 +1346,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   } else {
     mainloop_pipe(F_{}, I4{});
   }
-#else
-  if (u8b) {
-    if (nvalid >= 4) mainloop(T_{}, I4{});
-    else if (nvalid >= 1) mainloop(T_{}, I1{});
-    else mainloop(T_{}, I0{});
-  } else {
-    mainloop(F_{}, I4{});
-  }
-#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
@@ -1876,44 +1371,16 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // ---- epilogue: the MFMAs took their operands swapped (B first), so each lane holds
   // 4 consecutive n of one m row: float4 stores straight from registers into slab slice
   // s (no LDS staging, no barriers) ----
-#if SL_WG_TILED
-  static_assert(SL_WG_W128 && WG_MI == 8 && WG_NJ == 2, "tiled slab assumes 2 x 4 waves of 128 x 32");
+  static_assert(1 && WG_MI == 8 && WG_NJ == 2, "tiled slab assumes 2 x 4 waves of 128 x 32");
   float* out = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096 + lane * 4;
-#else
-  float* out = A.slab + (long)s * A.slab_stride + P.w_off;
-#endif
-#if SL_WG_MFMA32
-  // register r = 4 g + t of tile i: n = 8 g + 4 (lane >> 5) + t, m = 32 i + (lane & 31);
-  // store (i, g) is 1 KB of contiguous slab (sgd_tiled decodes the same order)
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = n0 + wn * 32 + 8 * g + 4 * (lane >> 5);
-      if (n < P.n_real)
-        *reinterpret_cast<floatx4_t*>(out + (i * 4 + g) * 256) =
-            floatx4_t{acc32[i][4 * g], acc32[i][4 * g + 1], acc32[i][4 * g + 2], acc32[i][4 * g + 3]};
-    }
-  if (false)
-#endif
 #pragma unroll
   for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
     for (int j = 0; j < WG_NJ; ++j) {
       const int n = n0 + wn * 16 * WG_NJ + j * 16 + 4 * lg;
-#if SL_WG_KO == 7  // 7: epilogue stores knocked out; asm keeps every accumulator (and its MFMAs) live
-      asm volatile("" ::"v"(acc[i][j]));
-#else
-#if SL_WG_TILED
       if (n < P.n_real) *reinterpret_cast<floatx4_t*>(out + (i * WG_NJ + j) * 256) = acc[i][j];
-#else
-      if (n < P.n_real)
-        *reinterpret_cast<floatx4_t*>(out + (long)(wm * 16 * WG_MI + i * 16 + lr) * P.n_real + n) = acc[i][j];
-#endif
-#endif
     }
 
-#if SL_WG_KO != 6  // 6: no partial-row sums
   float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
   if (g < G) {
     if (pr_regs) {
@@ -1944,16 +1411,9 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q = 4 * (c0 + col) + j;
-#if SL_WG_TILED
       if (q < W3P_N || q >= W3P_DB1) srow[TL_SMALL + q] = tv[j];
-#else
-      if (q < W3P_N) srow[P_W3 + q] = tv[j];
-      else if (q >= W3P_DB1 && q < W3P_DB2) srow[P_B1 + q - W3P_DB1] = tv[j];
-      else if (q >= W3P_DB2) srow[P_B2 + q - W3P_DB2] = tv[j];
-#endif
     }
   }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2020,24 +1480,13 @@ __device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p,
   }
   w -= a.lr * d;
   a.w[p] = w;
-#if SL_SGD_KO != 1  // timing knockout 1: no bf16 shadow writes
   write_shadow(a, p, w);
-#endif
 }
 
 // SGD_TPG threads per float4 group of parameters: each sums every SGD_TPG-th
 // slab slice, the group combines by DPP (quad perms, then row_half_mirror for 8).
-#ifndef SL_SGD_KO
-#define SL_SGD_KO 0  // timing knockouts of mlp_sgd_kernel (1: no shadow writes, 2: no slab reads, 3: empty)
-#endif
-#ifndef SL_SGD_TPG
-#define SL_SGD_TPG 4
-#endif
-constexpr int SGD_TPG = SL_SGD_TPG;
-#ifndef SL_SGD_NT
-#define SL_SGD_NT 1024  // threads per mlp_sgd_kernel workgroup (1024: 9.8 us vs 11.5 us at 256, profiles/r02_sgdnt)
-#endif
-constexpr int SGD_NT = SL_SGD_NT;
+constexpr int SGD_TPG = 4;
+constexpr int SGD_NT = 1024;
 static_assert(SGD_TPG == 4 || SGD_TPG == 8, "4 or 8 threads per group");
 __device__ __forceinline__ float group_sum(float v) {
   v = quad_sum(v);
@@ -2045,8 +1494,7 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-#if SL_WG_TILED
-// Slab reduction + update over a tiled slab (SL_WG_TILED): the threads walk the slab in its
+// Slab reduction + update over a tiled slab (1): the threads walk the slab in its
 // own order (float4 unit u of every slice: coalesced 1 KB per wave and slice), each unit's 4
 // floats map back to 4 consecutive parameters of one weight row (or, in the small region, to
 // single parameters).  w / mom / the shadows are then touched in a scattered order, but they
@@ -2060,13 +1508,8 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
     const int tile = (int)(off / TL_TILE), within = (int)(off % TL_TILE);
     const int wave = within >> 12, rem = within & 4095;
     const int ins = rem >> 8, lane = (rem & 255) >> 2;
-#if SL_WG_MFMA32  // store (tile i = ins / 4, register group g = ins % 4) of mlp_wgrad_kernel's 32x32x16 form
-    const int m = (wave & 1) * 128 + (ins >> 2) * 32 + (lane & 31);
-    const int nn = (wave >> 1) * 32 + (ins & 3) * 8 + (lane >> 5) * 4;
-#else
     const int m = (wave & 1) * 128 + (ins >> 1) * 16 + (lane & 15);
     const int nn = (wave >> 1) * 32 + (ins & 1) * 16 + (lane >> 4) * 4;
-#endif
     if (tile < 7) {
       const int n = tile * 128 + nn;
       if (n >= D_IN) return;  // dW1's last tile: 16 real columns (whole group exits together)
@@ -2118,24 +1561,20 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
   if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
   sgd_apply(a, gout, pe, gme, w0, m0);
 }
-#endif
 
 // float4 units a launch of mlp_sgd_kernel walks: the slab's (tiled) or the parameters'
 __host__ __device__ constexpr long sgd_units(bool slab) {
-  return (SL_WG_TILED && slab) ? TL_STRIDE / 4 : (P_N + 3) / 4;
+  return (1 && slab) ? TL_STRIDE / 4 : (P_N + 3) / 4;
 }
 
 __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
-  if (SL_SGD_KO == 3) return;  // timing knockout 3: launch + kernel-boundary floor
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int part = (int)(t % SGD_TPG);
-#if SL_WG_TILED
   if (a.slab && a.mode != 0) {
     sgd_tiled(a, t / SGD_TPG, part);
     return;
   }
-#endif
   const long p0 = (t / SGD_TPG) * 4;
   if (p0 >= a.n) return;  // whole groups exit together (n groups are group-aligned in t)
   const long p = p0 + part;
@@ -2168,11 +1607,6 @@ __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int sidx = s0 + u * SGD_TPG;
-#if SL_SGD_KO == 2  // timing knockout 2: no slab reads
-          v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-          d[u] = 0.f;
-          continue;
-#endif
           v[u] = sidx < a.slices ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
                                  : make_float4(0.f, 0.f, 0.f, 0.f);
           d[u] = (w1row && sidx < a.slices) ? dbs[(long)sidx * a.slab_stride] : 0.f;
@@ -2250,29 +1684,25 @@ extern "C" {
 long sl_mlp_param_count() { return P_N; }
 
 // floats per slice of the weight-gradient slab (the tiled layout is larger than the parameters)
-long sl_mlp_slab_stride() { return SL_WG_TILED ? TL_STRIDE : (P_N + 3) / 4 * 4; }
+long sl_mlp_slab_stride() { return 1 ? TL_STRIDE : (P_N + 3) / 4 * 4; }
 
 static unsigned long long* g_stamps = nullptr;
 int sl_mlp_set_stamps(unsigned long long* p) {
   g_stamps = p;
   return 0;
 }
-static int g_rows_bm = 0;  // 0: auto; 64 / 128 force a tile height (benchmarks, tests)
+static int g_rows_bm = 0;  // 0: auto; 64 / 256 force a tile height (benchmarks, tests)
 int sl_mlp_set_rows_bm(int bm) {
   g_rows_bm = bm;
   return 0;
 }
 
-// Rows per workgroup (64 by default; 128 = one 8-wave workgroup per CU on request).
+// Rows per workgroup: 64 by default (two co-resident workgroups per CU overlap each other's
+// epilogues; 2 % ahead of the 256-row tile in the in-process interleaved A/B at B = 65,536,
+// scripts/ab_mlp_inproc.py, profiles/r03_big), 256 on request (SL_MLP_ROWS_BM=256).  The
+// 128-row tiles measured slower (r01_v7, r02_rows_w4) and were removed in round 4.
 int sl_mlp_rows_bm(int batch) {
-  if (g_rows_bm == 64 || (g_rows_bm == 128 && batch % 128 == 0) || (g_rows_bm == 256 && batch % 256 == 0))
-    return g_rows_bm;
-  // 64 (two co-resident workgroups per CU overlap each other's epilogues) measured ahead
-  // of 128 at every batch size tried (r01_v7), and 2 % ahead of the 256-row tile in the
-  // in-process interleaved A/B at B = 65,536 (scripts/ab_mlp_inproc.py, profiles/r03_big:
-  // the 256-row tile spends fewer cycles per CU but loses them back at the clock and
-  // its serialized epilogues), so 256 stays opt-in (SL_MLP_ROWS_BM=256).
-  (void)batch;
+  if (g_rows_bm == 256 && batch % 256 == 0) return 256;
   return 64;
 }
 
@@ -2291,15 +1721,11 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.loss = loss; a.correct = correct; a.logits = logits;
   a.stamps = g_stamps;
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
-  // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_l1 (same batch rows)
+  // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_fwd1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);
   if (bm == 256 && train != 2) {
     if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 256, 2>), dim3(batch / 256), dim3(512), 0, stream, a);
     else hipLaunchKernelGGL((mlp_rows_kernel<false, 256, 2>), dim3(batch / 256), dim3(512), 0, stream, a);
-  } else if (bm == 128) {
-    if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, SL_ROWS128_WMG, false>), dim3(batch / 128), dim3(512), 0, stream, a);
-    else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, SL_ROWS128_WMG>), dim3(batch / 128), dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, SL_ROWS128_WMG>), dim3(batch / 128), dim3(512), 0, stream, a);
   } else {
     if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1, false>), dim3(batch / 64), dim3(256), 0, stream, a);
     else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
@@ -2309,26 +1735,12 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   return 0;
 }
 
-// Layer-1 forward GEMM of the train step (batch % 256 == 0): H1 for the rows
-// kernel's train == 2 mode and for the weight gradient.
-int sl_mlp_l1(const uint8_t* x, const int* cursor, int n_batches, int batch, const uint16_t* w1h,
-              const float* params, float xa, float xb, uint16_t* h1, hipStream_t stream) {
-  if (batch <= 0 || batch % L1_BM != 0 || !x || !h1 || !w1h || !params) return -1;
-  if (((uintptr_t)x & 15) != 0 || ((uintptr_t)h1 & 15) != 0) return -2;
-  L1Args a;
-  a.x = x; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
-  a.w1h = w1h; a.b1 = params + P_B1; a.xa = xa; a.xb = xb; a.h1 = h1;
-  hipLaunchKernelGGL(mlp_l1_kernel, dim3(batch / L1_BM * (HID / L1_BN)), dim3(L1_NT), 0, stream, a);
-  SL_CHECK_LAUNCH();
-  return 0;
-}
-
 // Effective slice count for a batch: whole 64-row stages, equal-length
 // slices except the last (the slab array holds this many partial gradients).
 int sl_mlp_wgrad_slices(int batch, int requested) {
   if (batch <= 0 || batch % 64 != 0) return -1;
   const int total = batch / 64;
-  int req = requested > 0 ? requested : SL_MLP_SLICES;  // one GEMM WG per CU (128 KB LDS each)
+  int req = requested > 0 ? requested : 28;  // one GEMM WG per CU (128 KB LDS each)
   if (req > total) req = total;
   const int spp = (total + req - 1) / req;
   return (total + spp - 1) / spp;
@@ -2340,7 +1752,7 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
                  const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
                  long slab_stride, hipStream_t stream) {
   if (!w3p || n_w3p != batch / 64) return -1;
-  if (SL_WG_TILED && slab_stride < TL_STRIDE) return -1;
+  if (slab_stride < TL_STRIDE) return -1;
   const int s_eff = sl_mlp_wgrad_slices(batch, slices);
   if (s_eff <= 0 || s_eff != slices) return -1;
   WgArgs a;
@@ -2379,7 +1791,7 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   if (mode != 0 && !slab && !grad_in) return -1;
   if (mode == 1 && !grad_out) return -1;
   if (slab && (slab_stride & 3)) return -1;
-  if (SL_WG_TILED && slab && slab_stride < TL_STRIDE) return -1;
+  if (slab && slab_stride < TL_STRIDE) return -1;
   const long groups = sgd_units(slab != nullptr && mode != 0);
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
@@ -2393,7 +1805,7 @@ int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa
   SgdArgs a = {};
   a.slab = slab; a.slices = slices; a.slab_stride = slab_stride; a.grad_out = slot0; a.grad_out_alt = slot1;
   a.ar_ctl = ctl; a.n = P_N; a.xa = xa; a.xb = xb; a.mode = 1;
-  if (SL_WG_TILED && slab_stride < TL_STRIDE) return -1;
+  if (slab_stride < TL_STRIDE) return -1;
   const long groups = sgd_units(true);
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();

@@ -318,11 +318,10 @@ class FusedMLPTrainer:
         self.w1f = torch.zeros(HIDDEN, D_IN_PAD, dtype=torch.float16, device=dev)
         # Layer 1 of the train step: with SL_MLP_FWD1=1 (batch % 256 == 0) its own 256 x 256-tile
         # GEMM, mlp_fwd1_kernel (csrc/kernels/mlp_fwd1.hip: exact fp16 (1024 + u) pixels, LDS-DMA
-        # ring), after which the rows kernel starts at layer 2 from H1; by default layer 1 runs
-        # inside the rows kernel; SL_MLP_L1=1 selects the older 128-row-tile GEMM (profiles/r01_v10).
-        l1 = os.environ.get("SL_MLP_L1", "0") == "1" and batch % 128 == 0
-        fwd1 = os.environ.get("SL_MLP_FWD1", "0") == "1" and batch % 256 == 0 and not l1
-        self.l1_kernel = "fwd1" if fwd1 else ("l1" if l1 else None)
+        # ring), after which the rows kernel starts at layer 2 from H1; otherwise layer 1 runs
+        # inside the rows kernel.
+        fwd1 = os.environ.get("SL_MLP_FWD1", "0") == "1" and batch % 256 == 0
+        self.l1_kernel = "fwd1" if fwd1 else None
         self.allreduce = None  # callable(grad_tensor) -> None, sums in place (RCCL)
         self.xgmi = None       # parallel.xgmi.XgmiExchange: all-reduce fused into the update (no RCCL)
         self.x = self.y = None
@@ -335,7 +334,7 @@ class FusedMLPTrainer:
 
     @property
     def l1_gemm(self) -> bool:
-        """Layer 1 runs as its own launch (mlp_fwd1 or mlp_l1) and the rows kernel starts at H1."""
+        """Layer 1 runs as its own launch (mlp_fwd1) and the rows kernel starts at H1."""
         return self.l1_kernel is not None
 
     @property
@@ -400,9 +399,6 @@ class FusedMLPTrainer:
         if self.l1_kernel == "fwd1":
             lc["l1"] = n.Launch("sl_mlp_fwd1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1f),
                                 p(self.params[N_PARAMS_B1:]), self.xa, self.xb, p(self.h1t))
-        elif self.l1_kernel == "l1":
-            lc["l1"] = n.Launch("sl_mlp_l1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1h),
-                                p(self.params), self.xa, self.xb, p(self.h1t))
         for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
                                                         "reduce": (1, False, True, False),
                                                         "update": (2, True, False, True)}.items():

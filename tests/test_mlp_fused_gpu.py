@@ -17,7 +17,7 @@ def _rel(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
 
-@pytest.mark.parametrize("bm", [64, 128, 256])
+@pytest.mark.parametrize("bm", [64, 256])
 def test_logits_match_reference(bm, rows_bm):
     rows_bm(bm)
     x, y = _data(256)
@@ -37,8 +37,7 @@ def rows_bm():
     _native.call("sl_mlp_set_rows_bm", 0)
 
 
-@pytest.mark.parametrize("batch,bm,l1", [(64, 64, None), (512, 64, "fwd1"), (2048, 64, "fwd1"), (512, 128, "fwd1"),
-                                         (2048, 128, "l1"), (512, 64, "l1"), (2048, 64, None), (512, 128, None),
+@pytest.mark.parametrize("batch,bm,l1", [(64, 64, None), (512, 64, "fwd1"), (2048, 64, "fwd1"), (2048, 64, None),
                                          (512, 256, None), (2048, 256, None)])
 def test_gradients_match_reference(batch, bm, l1, rows_bm):
     from serverless_learn_amd.ops import _native
@@ -48,7 +47,7 @@ def test_gradients_match_reference(batch, bm, l1, rows_bm):
     x, y = _data(batch, seed=3)
     flat = M.init_params(2)
     tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
-    tr.l1_kernel = l1  # layer 1 as mlp_fwd1 / mlp_l1, or inside the rows kernel (None)
+    tr.l1_kernel = l1  # layer 1 as mlp_fwd1, or inside the rows kernel (None)
     tr.load_shard(x, y)
     g = tr.compute_grads().cpu()
     torch.cuda.synchronize()
@@ -66,22 +65,6 @@ def test_gradients_match_reference(batch, bm, l1, rows_bm):
     st = tr.stats()
     assert abs(st.loss - float(loss) / batch) < 2e-2
     assert abs(st.accuracy - float(correct) / batch) < 0.05
-
-
-def test_layer1_gemm_matches_row_fused_layer1():
-    """mlp_l1_kernel's H1 is bit-identical to the rows kernel's own layer 1 (same k order)."""
-    batch = 1024
-    x, y = _data(batch, seed=7)
-    flat = M.init_params(4)
-    h = []
-    for l1 in ("l1", None):
-        tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
-        tr.l1_kernel = l1
-        tr.load_shard(x, y)
-        tr.compute_grads()
-        torch.cuda.synchronize()
-        h.append(tr.h1t.clone())
-    assert torch.equal(h[0], h[1]), float((h[0].float() - h[1].float()).abs().max())
 
 
 def test_fwd1_layer1_matches_fp32_reference():
