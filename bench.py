@@ -387,9 +387,39 @@ def main(argv=None) -> int:
             tr.capture(warmup=0, unroll=args.unroll)
         else:
             tr.capture(warmup=0)
+
+    def upload_graph():
+        # upload the K-step executable graph before the clock starts, as any graph about to be
+        # replayed in a loop is (hipGraphUpload); otherwise its first replay pays the upload
+        if not (use_graph and mlp and getattr(tr, "graph_unrolled", None) is not None and args.steps <= args.unroll):
+            return
+        try:
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            rc = hip.hipGraphUpload(ctypes.c_void_p(tr.graph_unrolled.raw_cuda_graph_exec()),
+                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            if rc != 0:
+                print(f"hipGraphUpload failed ({rc})", file=sys.stderr)
+        except (AttributeError, OSError) as e:
+            print(f"graph upload unavailable: {e}", file=sys.stderr)
+        torch.cuda.synchronize()
+
+    # One-time host work goes BEFORE the rest of the warm-up, not between it and the timed
+    # region: the first tr.stats() loads torch's reduction kernels lazily (the GPU sat idle for
+    # ~27 ms there, profiles/r04_a/tr20), and the graph upload.  A GPU idle for >= 10 ms runs the
+    # next replay ~9 % slower than one idle for 1 ms (profiles/r04_a/graph_overhead_probe.json),
+    # so the remaining warm-up steps run right before the clock starts.  The warm-up is still
+    # exactly --warmup steps.
+    legacy_order = os.environ.get("SL_BENCH_LEGACY_ORDER") == "1"  # round-3 order, for same-box A/B only
+    if not legacy_order:
+        torch.cuda.synchronize()
+        first_loss = tr.stats().loss  # after the eager warm-up steps
+        upload_graph()
     run(args.warmup - warm_eager)
-    torch.cuda.synchronize()
-    first_loss = tr.stats().loss
+    if legacy_order:
+        torch.cuda.synchronize()
+        first_loss = tr.stats().loss
+        upload_graph()
 
     def pg_mode():
         tr.enable_xgmi(None)
@@ -470,19 +500,8 @@ def main(argv=None) -> int:
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         return bool(torch.equal(lo, hi))
 
-    if use_graph and mlp and getattr(tr, "graph_unrolled", None) is not None and args.steps <= args.unroll:
-        # upload the K-step executable graph before the clock starts, as any graph about to be
-        # replayed in a loop is (hipGraphUpload); otherwise its first replay pays the upload
-        try:
-            import ctypes
-            hip = ctypes.CDLL("libamdhip64.so")
-            rc = hip.hipGraphUpload(ctypes.c_void_p(tr.graph_unrolled.raw_cuda_graph_exec()),
-                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-            if rc != 0:
-                print(f"hipGraphUpload failed ({rc})", file=sys.stderr)
-        except (AttributeError, OSError) as e:
-            print(f"graph upload unavailable: {e}", file=sys.stderr)
-        torch.cuda.synchronize()
+    if autotune is not None:
+        upload_graph()  # the autotune re-captured the chosen mode's graph
     elapsed = timed()
     replicas_identical = replicas_agree() if world > 1 else None
     st_timed = tr.stats()
