@@ -404,19 +404,18 @@ def main(argv=None) -> int:
             print(f"graph upload unavailable: {e}", file=sys.stderr)
         torch.cuda.synchronize()
 
-    # One-time host work goes BEFORE the rest of the warm-up, not between it and the timed
-    # region: the first tr.stats() loads torch's reduction kernels lazily (the GPU sat idle for
-    # ~27 ms there, profiles/r04_a/tr20), and the graph upload.  A GPU idle for >= 10 ms runs the
-    # next replay ~9 % slower than one idle for 1 ms (profiles/r04_a/graph_overhead_probe.json),
-    # so the remaining warm-up steps run right before the clock starts.  The warm-up is still
-    # exactly --warmup steps.
-    legacy_order = os.environ.get("SL_BENCH_LEGACY_ORDER") == "1"  # round-3 order, for same-box A/B only
-    if not legacy_order:
+    # SL_BENCH_PRELOAD=1 moves the one-time host work (the first tr.stats() loads torch's
+    # reduction kernels lazily: the GPU sits idle ~27 ms there, profiles/r04_a/tr20; the graph
+    # upload) before the last warm-up steps instead of after them.  Same-box A/B: no gain
+    # (484-496 M vs 496-505 M, profiles/r04_c), so the default keeps the round-3 order.  The
+    # warm-up is exactly --warmup steps either way.
+    preload = os.environ.get("SL_BENCH_PRELOAD") == "1"
+    if preload:
         torch.cuda.synchronize()
         first_loss = tr.stats().loss  # after the eager warm-up steps
         upload_graph()
     run(args.warmup - warm_eager)
-    if legacy_order:
+    if not preload:
         torch.cuda.synchronize()
         first_loss = tr.stats().loss
         upload_graph()
@@ -541,11 +540,16 @@ def main(argv=None) -> int:
     if xgmi_fallback:
         out["xgmi_fallback"] = xgmi_fallback
     if getattr(tr, "probe", None) is not None:
-        rec = tr.clock_probe_records()
-        iv = [((b[1] - a[1]) / 100.0, (b[0] - a[0]) / max(1, b[1] - a[1]) * 0.1) for a, b in zip(rec, rec[1:])]
-        w0 = min(args.warmup, 3) + (args.warmup - min(args.warmup, 3))  # steps before the timed region
-        out["clock_probe"] = {"n": len(rec), "timed_from": w0,
-                              "intervals_us_ghz": [[round(u, 2), round(gz, 3)] for u, gz in iv[:w0 + args.steps + 40]]}
+        # per step: wall us between consecutive probes and the shader clock over it (GHz), per XCD
+        # where both probes ran a workgroup on that XCD (median over those XCDs)
+        import statistics
+        steps = tr.clock_probe_steps()
+        iv = []
+        for (w0_, t0), (w1_, t1) in zip(steps, steps[1:]):
+            ghz = [(t1[x][0] - t0[x][0]) / max(1, t1[x][1] - t0[x][1]) * 0.1 for x in t0 if x in t1]
+            iv.append([round((w1_ - w0_) / 100.0, 2), round(statistics.median(ghz), 3) if ghz else None])
+        w0 = args.warmup  # steps before the timed region
+        out["clock_probe"] = {"n": len(steps), "timed_from": w0, "intervals_us_ghz": iv[:w0 + args.steps + 40]}
     if autotune:
         out["allreduce_autotune"] = autotune
     if rank == 0:

@@ -1,26 +1,30 @@
-// Diagnostics: a one-lane clock probe for timelines inside captured step graphs.
+// Diagnostics: a clock probe for timelines inside captured step graphs.
 //
-// clock_probe_kernel appends (s_memtime, s_memrealtime) to a device buffer when it runs.  Put
-// between the kernels of a step it gives, without a profiler attached, the wall time of each
-// step (s_memrealtime ticks at a constant 100 MHz) and the average shader clock over it
-// (delta s_memtime / delta s_memrealtime x 100 MHz; MI355X_MICROARCH.md "DVFS give-back" item 6).
-// Only the bench's diagnostic mode (SL_CLOCK_PROBE=1) launches it.
+// clock_probe_kernel runs one lane in each of its workgroups (the grid spans every XCD) and
+// appends (XCC id, s_memtime, s_memrealtime) records.  s_memrealtime ticks at a constant
+// 100 MHz on every XCD; s_memtime counts shader clocks on the XCD it is read on (the counters
+// of different XCDs are not aligned), so the clock over an interval between two probes is
+// delta s_memtime / delta s_memrealtime x 100 MHz taken per XCD
+// (MI355X_MICROARCH.md "DVFS give-back" item 6).  Only the bench's diagnostic mode
+// (SL_CLOCK_PROBE=1) launches it.
 #include "common.h"
 
 __global__ void clock_probe_kernel(unsigned long long* buf, unsigned* cnt, int cap) {
   if (threadIdx.x != 0) return;
   const unsigned long long t = __builtin_amdgcn_s_memtime();
   const unsigned long long w = __builtin_amdgcn_s_memrealtime();
+  const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 15u;  // HW_REG_XCC_ID
   const unsigned i = atomicAdd(cnt, 1u);
   if ((int)i < cap) {
-    buf[2 * i] = t;
-    buf[2 * i + 1] = w;
+    buf[3 * i] = xcc;
+    buf[3 * i + 1] = t;
+    buf[3 * i + 2] = w;
   }
 }
 
 extern "C" int sl_clock_probe(unsigned long long* buf, unsigned* cnt, int cap, hipStream_t stream) {
   if (!buf || !cnt || cap <= 0) return -1;
-  hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, stream, buf, cnt, cap);
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(16), dim3(64), 0, stream, buf, cnt, cap);
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -266,17 +266,19 @@ __device__ __forceinline__ void copy_part_buf(const uint16_t* src, int ld, __amd
 // (register budget: 128 accumulators of 256); profiles/r03_big.
 // L1 = false (BM = 64 only): H1 was already computed by mlp_fwd1_kernel (mlp_fwd1.hip);
 // the tile is staged from global into R1 and layer 1 / its H1 write are skipped.
-template <int BM> constexpr int rows_nwv() { return BM == 256 ? 8 : BM / 16; }
+template <int BM> constexpr int rows_nwv() { return BM == 256 ? 8 : 4; }
 template <bool TRAIN, int BM, int WMG, bool L1 = true>
-__global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? 2 : 1) void mlp_rows_kernel(MlpRowArgs a) {
+__global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_rows_kernel(MlpRowArgs a) {
   constexpr int NWV = rows_nwv<BM>();  // waves per workgroup
   constexpr int MF = BM / 16 / WMG;    // m-fragments per wave
   constexpr int NT = NWV * 64;         // threads
   constexpr int NF = 16 * WMG / NWV;   // n-fragments per wave
-  constexpr bool BIG = BM == 256;
-  static_assert(BM == 64 || BM == 256, "64- or 256-row tiles");
+  // WIDE: 128 rows x 64 features per wave (the 256-row tile and the 4-wave 128-row tile)
+  constexpr bool BIG = BM >= 128;
+  static_assert(BM == 64 || BM == 128 || BM == 256, "64-, 128- or 256-row tiles");
   constexpr bool ONE = BIG;  // one activation image (+ H1 nibble mask)
-  static_assert(!BIG || L1, "the 256-row tile has no train == 2 form");
+  static_assert(!BIG || L1, "the wide tiles have no train == 2 form");
+  static_assert(!BIG || (MF == 8 && NF == 4), "wide tiles: 128 x 64 per wave");
   constexpr int RING = BIG ? 2 : 4;  // weight ring depth (k-steps)
   constexpr bool APF = !BIG;         // prefetch the next k-step's A fragments
   constexpr int XQ = 2;              // BIG: X chunks waiting in registers
@@ -286,7 +288,11 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? 2 : 1) void mlp_row
   constexpr int REGB = BM * HS_LD;   // one LDS region (elements)
   static_assert(3 * BM * XC_LD <= REGB, "X ring must fit region 0");
   constexpr int SMEM = ONE ? REGB + BM * DZL + BM * 32 : 2 * REGB + BM * DZL;
-  constexpr int BSZ = BIG ? (2 * HID + 16) * 2 : 0;  // BIG: b1 | b2 | b3 staged in LDS (fp32, as uint16 pairs)
+  // BIG: b1 | b2 (| b3: 256-row tile) staged in LDS (fp32, as uint16 pairs); the 128-row tile
+  // reads b3 from global so that two workgroups fit one CU's 160 KB
+  constexpr bool B3LDS = BM == 256;
+  constexpr int BSZ = BIG ? (2 * HID + (B3LDS ? 16 : 0)) * 2 : 0;
+  constexpr bool W3LDS = BIG && BM * DZL >= 16 * HID;  // W3 staged in the dZ image until layer 3 (256-row tile)
   static_assert((SMEM + BSZ) * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM + BSZ];
   float* BS = reinterpret_cast<float*>(smem + SMEM);
@@ -327,10 +333,12 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? 2 : 1) void mlp_row
   if constexpr (BIG) {  // the epilogues read the biases from LDS (published by layer 1's barriers)
     if (tid < 2 * HID / 4)
       reinterpret_cast<float4*>(BS)[tid] = reinterpret_cast<const float4*>(tid < HID / 4 ? a.b1 : a.b2 - HID)[tid];
-    else if (tid < 2 * HID / 4 + NC)
+    else if (B3LDS && tid < 2 * HID / 4 + NC)
       BS[2 * HID + tid - 2 * HID / 4] = a.b3[tid - 2 * HID / 4];
-    static_assert(!BIG || NT * 8 == 16 * HID && BM * DZL >= 16 * HID, "W3 staging: one 16-B piece per thread into RZ");
-    reinterpret_cast<uint4*>(RZ)[tid] = reinterpret_cast<const uint4*>(a.w3h)[tid];
+    if constexpr (W3LDS) {
+      static_assert(NT * 8 == 16 * HID, "W3 staging: one 16-B piece per thread into RZ");
+      reinterpret_cast<uint4*>(RZ)[tid] = reinterpret_cast<const uint4*>(a.w3h)[tid];
+    }
   }
   if (a.stamps && tid == 0) {  // placement: HW_ID (CU / SH / SE) and XCC_ID
     a.stamps[(long)blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -654,7 +662,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? 2 : 1) void mlp_row
   if constexpr (ONE) bar();  // every wave is done reading H1: H2 replaces it
   stamp(14);
   relu_out(BIG ? BS + HID : a.b2, R0, false);
-  if constexpr (BIG) {  // from the copy of W3 staged in the dZ image at the start (no global load)
+  if constexpr (W3LDS) {  // from the copy of W3 staged in the dZ image at the start (no global load)
 #pragma unroll
     for (int ks = 0; ks < KS2; ++ks) w3f[ks] = lds8(RZ + ks * 512 + lane * 8);
   } else if constexpr (ONE) {  // after the epilogue: the 32 registers would push past the 168 budget
@@ -676,13 +684,13 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 64 ? 2 : 1) void mlp_row
 #pragma unroll
     for (int sp = 0; sp < SPW; ++sp)
       z3[sp] = mfma16(lds8(R0 + ((sp * NWV + wave) * 16 + lr) * HS_LD + 8 * lg + ks * 32), w3f[ks], z3[sp]);
-  if constexpr (BIG) bar();  // every wave holds W3 in registers: dZ may overwrite its staging copy
+  if constexpr (W3LDS) bar();  // every wave holds W3 in registers: dZ may overwrite its staging copy
 #pragma unroll
   for (int sp = 0; sp < SPW; ++sp) {
     const int rb = (sp * NWV + wave) * 16;  // this pass's 16 rows
     const floatx4_t z = z3[sp];
     const int c = lr;
-    const float bias3 = c < NC ? (BIG ? BS[2 * HID + c] : a.b3[c]) : 0.f;
+    const float bias3 = c < NC ? (B3LDS ? BS[2 * HID + c] : a.b3[c]) : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = rb + 4 * lg + r;
@@ -1702,7 +1710,7 @@ int sl_mlp_set_rows_bm(int bm) {
 // scripts/ab_mlp_inproc.py, profiles/r03_big), 256 on request (SL_MLP_ROWS_BM=256).  The
 // 128-row tiles measured slower (r01_v7, r02_rows_w4) and were removed in round 4.
 int sl_mlp_rows_bm(int batch) {
-  if (g_rows_bm == 256 && batch % 256 == 0) return 256;
+  if ((g_rows_bm == 256 || g_rows_bm == 128) && batch % g_rows_bm == 0) return g_rows_bm;
   return 64;
 }
 
@@ -1723,7 +1731,10 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
   // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_fwd1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);
-  if (bm == 256 && train != 2) {
+  if (bm == 128 && train != 2) {
+    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 1>), dim3(batch / 128), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, 1>), dim3(batch / 128), dim3(256), 0, stream, a);
+  } else if (bm == 256 && train != 2) {
     if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 256, 2>), dim3(batch / 256), dim3(512), 0, stream, a);
     else hipLaunchKernelGGL((mlp_rows_kernel<false, 256, 2>), dim3(batch / 256), dim3(512), 0, stream, a);
   } else {

@@ -23,5 +23,6 @@ if [ $rc -eq 0 ]; then
   SL_MLP_FWD1=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_fwd1 -o run -- python3 bench.py --steps 50 --warmup 5 --ingest local > $O/prof_fwd1.log 2>&1 || exit 1
   python scripts/rocprof_summary.py $O/prof_fwd1/run_results.db | head -6
 fi
+bash scripts/r04_d.sh || exit 1
 timeout -k 10 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/pytest_gpu.log 2>&1
 echo "gpu tests rc=$?"; tail -5 $O/pytest_gpu.log

@@ -12,6 +12,8 @@ from serverless_learn_amd.models.mlp import FusedMLPTrainer
 from serverless_learn_amd.ops import _native
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+if len(sys.argv) > 2:  # force a rows-kernel tile height (64 / 128 / 256)
+    _native.call("sl_mlp_set_rows_bm", int(sys.argv[2]))
 x, y = make_mnist_like(B * 2, seed=0)
 tr = FusedMLPTrainer(batch=B, device="cuda:0")
 tr.load_shard(torch.from_numpy(x), torch.from_numpy(y))

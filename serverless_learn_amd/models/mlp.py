@@ -475,19 +475,28 @@ class FusedMLPTrainer:
         self.graph = None
         self._lkey = None
 
-    def enable_clock_probe(self, cap: int = 4096) -> None:
-        """Diagnostics (bench.py SL_CLOCK_PROBE=1): a one-lane kernel stamps (shader clock,
-        100 MHz wall clock) at the start of every step, inside the captured graphs too."""
-        self.probe_buf = torch.zeros(2 * cap, dtype=torch.int64, device=self.device)
+    def enable_clock_probe(self, cap: int = 16 * 2048) -> None:
+        """Diagnostics (bench.py SL_CLOCK_PROBE=1): a 16-workgroup kernel stamps (XCC id,
+        shader clock, 100 MHz wall clock) at the start of every step, inside the captured
+        graphs too (csrc/kernels/diag.hip)."""
+        self.probe_buf = torch.zeros(3 * cap, dtype=torch.int64, device=self.device)
         self.probe_cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.probe = self._n.Launch("sl_clock_probe", self._n.ptr(self.probe_buf), self._n.ptr(self.probe_cnt), cap)
         self.graph = None
 
-    def clock_probe_records(self) -> list:
-        """[(shader_ticks, wall_ticks_100MHz)] in launch order."""
-        n = min(int(self.probe_cnt.item()), self.probe_buf.numel() // 2)
-        v = self.probe_buf[:2 * n].view(n, 2).cpu().tolist()
-        return [tuple(t) for t in v]
+    def clock_probe_steps(self) -> list:
+        """Per probed step boundary: (wall time in us of the 100 MHz clock, {xcc: shader ticks})."""
+        n = min(int(self.probe_cnt.item()), self.probe_buf.numel() // 3)
+        rec = self.probe_buf[:3 * n].view(n, 3).cpu().tolist()
+        out = []
+        for i in range(0, n - n % 16, 16):  # one launch = 16 consecutive records
+            grp = rec[i:i + 16]
+            wall = min(r[2] for r in grp)
+            ticks = {}
+            for x, t, w in grp:
+                ticks.setdefault(x, (t, w))
+            out.append((wall, ticks))
+        return out
 
     def _step_eager(self) -> None:
         if getattr(self, "probe", None) is not None:

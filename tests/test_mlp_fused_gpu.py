@@ -17,7 +17,7 @@ def _rel(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
 
-@pytest.mark.parametrize("bm", [64, 256])
+@pytest.mark.parametrize("bm", [64, 128, 256])
 def test_logits_match_reference(bm, rows_bm):
     rows_bm(bm)
     x, y = _data(256)
@@ -38,7 +38,7 @@ def rows_bm():
 
 
 @pytest.mark.parametrize("batch,bm,l1", [(64, 64, None), (512, 64, "fwd1"), (2048, 64, "fwd1"), (2048, 64, None),
-                                         (512, 256, None), (2048, 256, None)])
+                                         (512, 128, None), (2048, 128, None), (512, 256, None), (2048, 256, None)])
 def test_gradients_match_reference(batch, bm, l1, rows_bm):
     from serverless_learn_amd.ops import _native
 
@@ -180,12 +180,14 @@ def test_allreduce_hook_path_matches_single_rank():
     assert torch.allclose(a.get_flat(), b.get_flat(), rtol=1e-5, atol=1e-6)
 
 
-def test_training_is_deterministic_at_full_batch():
+@pytest.mark.parametrize("bm", [64, 128, 256])
+def test_training_is_deterministic_at_full_batch(bm, rows_bm):
     """Two 30-step runs from the same start give bit-identical, finite parameters at the
-    bench batch (B = 65,536: the 256-row rows tile on a 256-CU part).  A one-step gradient
-    check alone missed a store hazard that only broke multi-step training."""
+    bench batch (B = 65,536) for every rows-kernel tile height.  A one-step gradient check
+    alone missed a store hazard that only broke multi-step training."""
     from serverless_learn_amd.ops import _native
 
+    rows_bm(bm)
     B = 65536
     x, y = _data(B * 2, seed=5)
     flat = M.init_params(4)
@@ -197,7 +199,7 @@ def test_training_is_deterministic_at_full_batch():
             t.step()
         torch.cuda.synchronize()
         out.append((t.params.clone(), t.stats()))
-    assert _native.lib().sl_mlp_rows_bm(B) in (64, 256)
+    assert _native.lib().sl_mlp_rows_bm(B) == bm
     (p1, s1), (p2, s2) = out
     assert bool(torch.isfinite(p1).all())
     assert torch.equal(p1, p2)
