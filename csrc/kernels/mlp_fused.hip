@@ -1705,13 +1705,15 @@ int sl_mlp_set_rows_bm(int bm) {
   return 0;
 }
 
-// Rows per workgroup: 64 by default (two co-resident workgroups per CU overlap each other's
-// epilogues; 2 % ahead of the 256-row tile in the in-process interleaved A/B at B = 65,536,
-// scripts/ab_mlp_inproc.py, profiles/r03_big), 256 on request (SL_MLP_ROWS_BM=256).  The
-// 128-row tiles measured slower (r01_v7, r02_rows_w4) and were removed in round 4.
+// Rows per workgroup: 128 by default (4 waves of 128 rows x 64 features, two workgroups per
+// CU: each weight fragment streamed from L2 feeds 8 MFMAs, half the weight stream of the
+// 64-row tile, and the two co-resident workgroups overlap each other's epilogues).  In-process
+// interleaved A/B at B = 65,536 (scripts/ab_mlp_inproc.py, profiles/r04_e): 114.0 us/step vs
+// 122.7 for the 64-row tile and 123.2 for the 8-wave 256-row tile.  64 for batches that are not
+// a multiple of 128; SL_MLP_ROWS_BM=64 / 256 force the others.
 int sl_mlp_rows_bm(int batch) {
-  if ((g_rows_bm == 256 || g_rows_bm == 128) && batch % g_rows_bm == 0) return g_rows_bm;
-  return 64;
+  if ((g_rows_bm == 64 || g_rows_bm == 128 || g_rows_bm == 256) && batch % g_rows_bm == 0) return g_rows_bm;
+  return batch % 128 == 0 ? 128 : 64;
 }
 
 int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_batches, int batch,
