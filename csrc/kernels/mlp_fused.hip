@@ -100,6 +100,7 @@ struct MlpRowArgs {
   const int* cursor;
   int n_batches, batch;
   const uint16_t *w1h, *w2h, *w3h, *w2th, *w3th;
+  const uint16_t* w1f;                 // fp16 W1, fragment order (the wide tiles' layer 1)
   const float *b1, *b2, *b3;
   float xa, xb, grad_scale;
   float dh1_scale;                     // dH1 goes to HBM as fp16 of dH1 * dh1_scale (a power of two)
@@ -313,6 +314,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   const int cw = wng * 16 * NF;  // this wave's output columns
   const int rw = wmg * 16 * MF;  // ... and rows
   floatx4_t acc[MF][NF];
+  float sp[NF] = {};  // wide tiles: S[n] partial sums of the fp16 W1 fragments (layer 1)
   auto stamp = [&](int i) {
     if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
   };
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
     }
   };
   // bias + ReLU epilogue into a [BM][HS_LD] image (+ the nibble mask of H > 0)
-  auto relu_out = [&](const float* bias_v, uint16_t* img, bool with_mask) {
+  auto relu_out = [&](const float* bias_v, uint16_t* img, bool with_mask, float sc = 1.f) {
 #pragma unroll
     for (int n = 0; n < NF; ++n) {
       const int col = cw + n * 16 + 4 * lg;
@@ -413,8 +415,8 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
 #pragma unroll
       for (int m = 0; m < MF; ++m) {
         uint2 v;
-        v.x = pack2(fmaxf(acc[m][n][0] + bias.x, 0.f), fmaxf(acc[m][n][1] + bias.y, 0.f));
-        v.y = pack2(fmaxf(acc[m][n][2] + bias.z, 0.f), fmaxf(acc[m][n][3] + bias.w, 0.f));
+        v.x = pack2(fmaxf(fmaf(sc, acc[m][n][0], bias.x), 0.f), fmaxf(fmaf(sc, acc[m][n][1], bias.y), 0.f));
+        v.y = pack2(fmaxf(fmaf(sc, acc[m][n][2], bias.z), 0.f), fmaxf(fmaf(sc, acc[m][n][3], bias.w), 0.f));
         *reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col) = v;
         if (ONE && with_mask)
           M1[(rw + m * 16 + lr) * 64 + (col >> 2)] =
@@ -462,7 +464,8 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   };
 
   const int wcol = NF * wng;
-  const FragSrc f_w1(a.w1h, HID * D_INP * 2, wcol, KS1, lane);
+  // the wide tiles run layer 1 in fp16 on exact (1024 + u) pixels against fp16 W1 (see below)
+  const FragSrc f_w1(BIG ? a.w1f : a.w1h, HID * D_INP * 2, wcol, KS1, lane);
   const FragSrc f_w2(a.w2h, HID * HID * 2, wcol, KS2, lane);
   const FragSrc f_w2t(a.w2th, HID * HID * 2, wcol, KS2, lane);
   const FragSrc f_w3(a.w3h, 16 * HID * 2, 0, KS2, lane);
@@ -557,12 +560,25 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
         *reinterpret_cast<uint4*>(d + ((ch ^ sw) << 3)) = real ? make_uint4(pk[0], pk[1], pk[2], pk[3]) : make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4*>(d + (((ch + 1) ^ sw) << 3)) = real ? make_uint4(pk[4], pk[5], pk[6], pk[7]) : make_uint4(0, 0, 0, 0);
       };
+      // Pixels go to LDS as fp16 of (1024 + u): exact (fp16 steps by 1 over [1024, 2048)), one
+      // v_perm per two pixels instead of a convert + FMA + round per pixel.  Against fp16 W1:
+      //   Xn W1^T = xa (1024 + u) W1^T + (xb - 1024 xa) S,  S[n] = sum_k W1f[n][k],
+      // S summed in fp32 from the very fragments the MFMAs read (sp below), so the 1024 S terms
+      // cancel to fp32 rounding of the accumulator (profiles/r04_rows128).
+      auto pk8 = [&](uint32_t w, int half) {
+        return __builtin_amdgcn_perm(0x64646464u, w, half ? 0x04030402u : 0x04010400u);
+      };
       auto xcvt = [&](const uint4& v, uint32_t (&pk)[8]) {
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int m = 0; m < 8; ++m)
-          pk[m] = pack2((float)((w[m >> 1] >> ((m & 1) * 16)) & 0xffu) * nxa + nxb,
-                        (float)((w[m >> 1] >> ((m & 1) * 16 + 8)) & 0xffu) * nxa + nxb);
+        for (int m = 0; m < 8; ++m) pk[m] = pk8(w[m >> 1], m & 1);
+      };
+      auto wsum = [&](const short8_t& w, int n) {  // feature cw + 16 n + lr, this lane's k range
+        typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+        const u32x4s d = __builtin_bit_cast(u32x4s, w);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)  // v_dot2_f32_f16 against (1, 1): two fp16 weights into fp32
+          asm volatile("v_dot2_f32_f16 %0, %1, %2, %0" : "+v"(sp[n]) : "v"(d[j]), "v"(0x3c003c00u));
       };
       // prologue: chunks 0, 1 converted, 2, 3 waiting in registers
 #pragma unroll
@@ -601,10 +617,9 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
         for (int m = 0; m < MF; ++m) {
           if (m + 2 < MF) af[m + 2] = lds8(ab + (rw + (m + 2) * 16) * 64);
 #pragma unroll
-          for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(r[st % RING][n], af[m], acc[m][n]);
-          if (conv)  // piece m of the pass: bytes 2m, 2m+1
-            pk[m] = pack2((float)((xw[m >> 1] >> ((m & 1) * 16)) & 0xffu) * nxa + nxb,
-                          (float)((xw[m >> 1] >> ((m & 1) * 16 + 8)) & 0xffu) * nxa + nxb);
+          for (int n = 0; n < NF; ++n) acc[m][n] = mfma16h(r[st % RING][n], af[m], acc[m][n]);
+          if (conv) pk[m] = pk8(xw[m >> 1], m & 1);  // piece m of the pass: bytes 2m, 2m+1
+          if (m < NF) wsum(r[st % RING][m], m);
           __builtin_amdgcn_sched_barrier(0);
         }
         if (conv) xput(cc, q & 1, pk);
@@ -623,9 +638,21 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
     }
   }
   stamp(1);
-  if constexpr (ONE) bar();  // the X ring shares the image H1 goes to
+  if constexpr (BIG) {
+    // S over the lane's four 16-lane groups (k ranges); BS[f] = (xb - 1024 xa) S[f] + b1[f]
+#pragma unroll
+    for (int n = 0; n < NF; ++n) {
+      sp[n] += __shfl_xor(sp[n], 16);
+      sp[n] += __shfl_xor(sp[n], 32);
+    }
+    if (wmg == 0 && lg == 0) {
+#pragma unroll
+      for (int n = 0; n < NF; ++n) BS[cw + 16 * n + lr] = fmaf(a.xb - 1024.f * a.xa, sp[n], BS[cw + 16 * n + lr]);
+    }
+  }
+  if constexpr (ONE) bar();  // the X ring shares the image H1 goes to; BS holds the layer-1 constants
   stamp(12);
-  relu_out(BIG ? BS : a.b1, R1, true);
+  relu_out(BIG ? BS : a.b1, R1, true, BIG ? a.xa : 1.f);
   stamp(13);
   }
   bar();
@@ -1718,13 +1745,14 @@ int sl_mlp_rows_bm(int batch) {
 
 int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_batches, int batch,
                 const uint16_t* w1h, const uint16_t* w2h, const uint16_t* w3h, const uint16_t* w2th,
-                const uint16_t* w3th, const float* params, float xa, float xb, float grad_scale, float dh1_scale,
+                const uint16_t* w3th, const uint16_t* w1f, const float* params, float xa, float xb,
+                float grad_scale, float dh1_scale,
                 uint16_t* h1, float* w3p, uint16_t* dh2, uint16_t* dh1,
                 float* loss, float* correct, float* logits, int train, hipStream_t stream) {
   if (batch <= 0 || batch % BM != 0) return -1;
   MlpRowArgs a;
   a.x = x; a.y = y; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
-  a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th;
+  a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th; a.w1f = w1f;
   a.b1 = params + P_B1; a.b2 = params + P_B2; a.b3 = params + P_B3;
   a.xa = xa; a.xb = xb; a.grad_scale = grad_scale; a.dh1_scale = dh1_scale;
   a.h1 = h1; a.w3p = w3p; a.dh2 = dh2; a.dh1 = dh1;
@@ -1733,6 +1761,7 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
   // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_fwd1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);
+  if (bm != 64 && train != 2 && !w1f) return -3;  // the wide tiles read the fp16 W1 shadow
   if (bm == 128 && train != 2) {
     if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 1>), dim3(batch / 128), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, 1>), dim3(batch / 128), dim3(256), 0, stream, a);

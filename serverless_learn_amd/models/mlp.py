@@ -339,8 +339,11 @@ class FusedMLPTrainer:
 
     @property
     def l1_numerics(self) -> str:
-        """Where layer 1 rounds: "fp16" (mlp_fwd1: exact pixels, fp16 W1) or "bf16" (bf16 Xn and W1)."""
-        return "fp16" if self.l1_kernel == "fwd1" else "bf16"
+        """Where layer 1 rounds: "fp16" (mlp_fwd1 and the 128- / 256-row rows tiles: exact pixels,
+        fp16 W1) or "bf16" (the 64-row rows tile: bf16 Xn and W1)."""
+        if self.l1_kernel == "fwd1":
+            return "fp16"
+        return "bf16" if int(self._n.lib().sl_mlp_rows_bm(self.batch)) == 64 else "fp16"
 
     def layout(self):
         return [[n, list(s), o] for n, s, o, _ in param_layout()]
@@ -388,7 +391,7 @@ class FusedMLPTrainer:
         ws = (p(self.w1h), p(self.w2h), p(self.w2th), p(self.w3h), p(self.w3th), p(self.w1f))
         lc = {
             "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
-                             p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
+                             p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th), p(self.w1f),
                              p(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                              p(self.h1t), p(self.w3p), p(self.dh2t), p(self.dh1t),
                              p(self.loss), p(self.correct), None, 2 if self.l1_gemm else 1),
@@ -426,7 +429,7 @@ class FusedMLPTrainer:
         n = self._n
         n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
+               n.ptr(self.w1f), n.ptr(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                n.ptr(self.h1t), n.ptr(self.w3p), n.ptr(self.dh2t), n.ptr(self.dh1t),
                n.ptr(self.loss), n.ptr(self.correct), None, 0, n.stream_ptr())
 
@@ -552,7 +555,7 @@ class FusedMLPTrainer:
         corr = torch.zeros(rows, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
+               n.ptr(self.w1f), n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
                n.ptr(loss), n.ptr(corr), None, 0, n.stream_ptr())
         return StepStats(float(loss.mean()), float(corr.mean()), rows)
 
@@ -565,7 +568,7 @@ class FusedMLPTrainer:
         out = torch.empty(rows, CLASSES, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
+               n.ptr(self.w1f), n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
                None, None, n.ptr(out), 0, n.stream_ptr())
         return out
 

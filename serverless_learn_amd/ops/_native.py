@@ -31,7 +31,7 @@ F = ctypes.c_float
 _SIGS: dict[str, list] = {
     "sl_mlp_param_count": [],
     "sl_mlp_slab_stride": [],
-    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P],
+    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P],
     "sl_mlp_wgrad": [I, P, P, I, P, P, P, P, I, P, I, L, P],
     "sl_mlp_wgrad_slices": [I, I],
     "sl_mlp_set_rows_bm": [I],

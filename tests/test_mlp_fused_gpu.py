@@ -224,7 +224,7 @@ def test_gradients_match_reference_at_headline_config():
     torch.cuda.synchronize()
     xd, yd, fd = x.cuda(), y.cuda(), flat.cuda()
     loss, correct, gref = M.reference_grads(fd, xd, yd, 1.0 / B)
-    _, _, gemu = M.reference_grads_bf16(fd, xd, yd, 1.0 / B)
+    _, _, gemu = M.reference_grads_bf16(fd, xd, yd, 1.0 / B, l1=tr.l1_numerics)
     gref, gemu = gref.double().cpu(), gemu.double().cpu()
     for name, shape, off, n in M.param_layout():
         a, b, e = g[off:off + n], gref[off:off + n], gemu[off:off + n]
