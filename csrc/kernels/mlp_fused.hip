@@ -39,6 +39,13 @@
 
 using namespace sl;
 
+// Cache policy of the step's bulk activation / slab stores (buffer-store aux bits, gfx950:
+// 16 = sc1, write-through).  A kernel boundary writes back every line its predecessor left dirty
+// in the XCDs' L2s (MI355X_MICROARCH.md price list, row "boundary": + dirty bytes / 6 TB/s); sc1
+// stores do not keep the line, so the write-back happens under the kernel instead of after it.
+#ifndef SL_STORE_POLICY
+#define SL_STORE_POLICY 16
+#endif
 namespace {
 constexpr int D_IN = 784;   // input features (28x28)
 constexpr int D_INP = 832;  // layer-1 K padded to 13 chunks of 64 (w1h row stride)
@@ -100,7 +107,7 @@ struct MlpRowArgs {
   const int* cursor;
   int n_batches, batch;
   const uint16_t *w1h, *w2h, *w3h, *w2th, *w3th;
-  const uint16_t* w1f;                 // fp16 W1, fragment order (the wide tiles' layer 1)
+  const uint16_t* w1f;                 // fp16 W1, fragment order (unused by the rows kernel's bf16 layer 1)
   const float *b1, *b2, *b3;
   float xa, xb, grad_scale;
   float dh1_scale;                     // dH1 goes to HBM as fp16 of dH1 * dh1_scale (a power of two)
@@ -254,7 +261,7 @@ __device__ __forceinline__ void copy_part_buf(const uint16_t* src, int ld, __amd
     const short8_t v = *reinterpret_cast<const short8_t*>(src + rr * ld + c);
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), dst, (r * gld + c) * 2,
-                                           (it * PER + i) * RPP * gld * 2, 0);
+                                           (it * PER + i) * RPP * gld * 2, SL_STORE_POLICY);
   }
 }
 
@@ -314,7 +321,6 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   const int cw = wng * 16 * NF;  // this wave's output columns
   const int rw = wmg * 16 * MF;  // ... and rows
   floatx4_t acc[MF][NF];
-  float sp[NF] = {};  // wide tiles: S[n] partial sums of the fp16 W1 fragments (layer 1)
   auto stamp = [&](int i) {
     if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
   };
@@ -464,8 +470,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   };
 
   const int wcol = NF * wng;
-  // the wide tiles run layer 1 in fp16 on exact (1024 + u) pixels against fp16 W1 (see below)
-  const FragSrc f_w1(BIG ? a.w1f : a.w1h, HID * D_INP * 2, wcol, KS1, lane);
+  const FragSrc f_w1(a.w1h, HID * D_INP * 2, wcol, KS1, lane);
   const FragSrc f_w2(a.w2h, HID * HID * 2, wcol, KS2, lane);
   const FragSrc f_w2t(a.w2th, HID * HID * 2, wcol, KS2, lane);
   const FragSrc f_w3(a.w3h, 16 * HID * 2, 0, KS2, lane);
@@ -560,25 +565,12 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
         *reinterpret_cast<uint4*>(d + ((ch ^ sw) << 3)) = real ? make_uint4(pk[0], pk[1], pk[2], pk[3]) : make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4*>(d + (((ch + 1) ^ sw) << 3)) = real ? make_uint4(pk[4], pk[5], pk[6], pk[7]) : make_uint4(0, 0, 0, 0);
       };
-      // Pixels go to LDS as fp16 of (1024 + u): exact (fp16 steps by 1 over [1024, 2048)), one
-      // v_perm per two pixels instead of a convert + FMA + round per pixel.  Against fp16 W1:
-      //   Xn W1^T = xa (1024 + u) W1^T + (xb - 1024 xa) S,  S[n] = sum_k W1f[n][k],
-      // S summed in fp32 from the very fragments the MFMAs read (sp below), so the 1024 S terms
-      // cancel to fp32 rounding of the accumulator (profiles/r04_rows128).
-      auto pk8 = [&](uint32_t w, int half) {
-        return __builtin_amdgcn_perm(0x64646464u, w, half ? 0x04030402u : 0x04010400u);
-      };
       auto xcvt = [&](const uint4& v, uint32_t (&pk)[8]) {
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int m = 0; m < 8; ++m) pk[m] = pk8(w[m >> 1], m & 1);
-      };
-      auto wsum = [&](const short8_t& w, int n) {  // feature cw + 16 n + lr, this lane's k range
-        typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
-        const u32x4s d = __builtin_bit_cast(u32x4s, w);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)  // v_dot2_f32_f16 against (1, 1): two fp16 weights into fp32
-          asm volatile("v_dot2_f32_f16 %0, %1, %2, %0" : "+v"(sp[n]) : "v"(d[j]), "v"(0x3c003c00u));
+        for (int m = 0; m < 8; ++m)
+          pk[m] = pack2((float)((w[m >> 1] >> ((m & 1) * 16)) & 0xffu) * nxa + nxb,
+                        (float)((w[m >> 1] >> ((m & 1) * 16 + 8)) & 0xffu) * nxa + nxb);
       };
       // prologue: chunks 0, 1 converted, 2, 3 waiting in registers
 #pragma unroll
@@ -617,9 +609,10 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
         for (int m = 0; m < MF; ++m) {
           if (m + 2 < MF) af[m + 2] = lds8(ab + (rw + (m + 2) * 16) * 64);
 #pragma unroll
-          for (int n = 0; n < NF; ++n) acc[m][n] = mfma16h(r[st % RING][n], af[m], acc[m][n]);
-          if (conv) pk[m] = pk8(xw[m >> 1], m & 1);  // piece m of the pass: bytes 2m, 2m+1
-          if (m < NF) wsum(r[st % RING][m], m);
+          for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(r[st % RING][n], af[m], acc[m][n]);
+          if (conv)  // piece m of the pass: bytes 2m, 2m+1
+            pk[m] = pack2((float)((xw[m >> 1] >> ((m & 1) * 16)) & 0xffu) * nxa + nxb,
+                          (float)((xw[m >> 1] >> ((m & 1) * 16 + 8)) & 0xffu) * nxa + nxb);
           __builtin_amdgcn_sched_barrier(0);
         }
         if (conv) xput(cc, q & 1, pk);
@@ -638,21 +631,9 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
     }
   }
   stamp(1);
-  if constexpr (BIG) {
-    // S over the lane's four 16-lane groups (k ranges); BS[f] = (xb - 1024 xa) S[f] + b1[f]
-#pragma unroll
-    for (int n = 0; n < NF; ++n) {
-      sp[n] += __shfl_xor(sp[n], 16);
-      sp[n] += __shfl_xor(sp[n], 32);
-    }
-    if (wmg == 0 && lg == 0) {
-#pragma unroll
-      for (int n = 0; n < NF; ++n) BS[cw + 16 * n + lr] = fmaf(a.xb - 1024.f * a.xa, sp[n], BS[cw + 16 * n + lr]);
-    }
-  }
-  if constexpr (ONE) bar();  // the X ring shares the image H1 goes to; BS holds the layer-1 constants
+  if constexpr (ONE) bar();  // the X ring shares the image H1 goes to
   stamp(12);
-  relu_out(BIG ? BS : a.b1, R1, true, BIG ? a.xa : 1.f);
+  relu_out(BIG ? BS : a.b1, R1, true);
   stamp(13);
   }
   bar();
@@ -879,7 +860,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
       for (int n = 0; n < NF; ++n) {
         typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
         const u32x2_t h = {hv[n][0], hv[n][1]};
-        __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, SL_STORE_POLICY);
       }
     }
     // Transpose-reduce of the 32 column partials over the 16 rows of a DPP row: each
@@ -1408,12 +1389,20 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // s (no LDS staging, no barriers) ----
   static_assert(1 && WG_MI == 8 && WG_NJ == 2, "tiled slab assumes 2 x 4 waves of 128 x 32");
   float* out = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096 + lane * 4;
+  // buffer stores of this wave's 16 KB of the tile (a wave-uniform base): lane offset + constant per store
+  float* out_base = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096;
+  const auto out_rs = __builtin_amdgcn_make_buffer_rsrc(out_base, 0, WG_MI * WG_NJ * 1024, 0x00020000);
+  const int out_voff = lane * 16;
 #pragma unroll
   for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
     for (int j = 0; j < WG_NJ; ++j) {
       const int n = n0 + wn * 16 * WG_NJ + j * 16 + 4 * lg;
-      if (n < P.n_real) *reinterpret_cast<floatx4_t*>(out + (i * WG_NJ + j) * 256) = acc[i][j];
+      if (n < P.n_real) {
+        typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4w, acc[i][j]), out_rs, out_voff,
+                                               (i * WG_NJ + j) * 1024, SL_STORE_POLICY);
+      }
     }
 
   float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1761,7 +1750,6 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
   // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_fwd1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);
-  if (bm != 64 && train != 2 && !w1f) return -3;  // the wide tiles read the fp16 W1 shadow
   if (bm == 128 && train != 2) {
     if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 1>), dim3(batch / 128), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, 1>), dim3(batch / 128), dim3(256), 0, stream, a);

@@ -339,11 +339,10 @@ class FusedMLPTrainer:
 
     @property
     def l1_numerics(self) -> str:
-        """Where layer 1 rounds: "fp16" (mlp_fwd1 and the 128- / 256-row rows tiles: exact pixels,
-        fp16 W1) or "bf16" (the 64-row rows tile: bf16 Xn and W1)."""
-        if self.l1_kernel == "fwd1":
-            return "fp16"
-        return "bf16" if int(self._n.lib().sl_mlp_rows_bm(self.batch)) == 64 else "fp16"
+        """Where layer 1 rounds: "fp16" (mlp_fwd1: exact pixels, fp16 W1) or "bf16" (the rows
+        kernel's own layer 1: bf16 Xn and W1).  An fp16 layer 1 inside the 128-row tile measured
+        3.5 % slower (the in-loop S sums), profiles/r04_rows128."""
+        return "fp16" if self.l1_kernel == "fwd1" else "bf16"
 
     def layout(self):
         return [[n, list(s), o] for n, s, o, _ in param_layout()]
