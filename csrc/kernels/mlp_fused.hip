@@ -424,30 +424,24 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
       }
     }
   };
-  // Wide tiles: bias add, bf16 pack, then ReLU as a packed int16 max with 0 (a bf16 is negative
-  // exactly when its int16 bits are; -0 becomes +0), and the H1 mask goes out as one dword of
-  // four nibbles per m-fragment: byte wng * 16 + lg * 4 + n of the row (read back the same way
-  // by the dH1 epilogue) instead of 32 byte stores per lane.
-  auto relu_out_wide = [&](uint16_t* img, bool with_mask, const float* bias_v) {
-    typedef short short2v __attribute__((ext_vector_type(2)));
-    const short2v z2 = {0, 0};
-    auto relu2 = [&](float x0, float x1) {
-      return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(short2v, pack2(x0, x1)), z2));
-    };
+  // ONE: write acc * 1[H1 > 0] from the nibble mask.  The byte base is made opaque so
+  // that hipcc recomputes it here instead of keeping relu_out's 32 mask addresses
+  // alive across the whole kernel (it spilled them, and each spill reload's vmcnt(0)
+  // drained the dH2 stores in flight).
+  auto masked_bits_out = [&](uint16_t* img) {
+    int mbo = (rw + lr) * 64 + (cw >> 2) + lg;
+    asm volatile("" : "+v"(mbo));
+    const uint8_t* M1b = M1 + mbo;
 #pragma unroll
     for (int n = 0; n < NF; ++n) {
       const int col = cw + n * 16 + 4 * lg;
-      const float4 b = *reinterpret_cast<const float4*>(bias_v + col);
 #pragma unroll
       for (int m = 0; m < MF; ++m) {
+        const uint32_t b = M1b[(m * 16) * 64 + n * 4];
         uint2 v;
-        v.x = relu2(acc[m][n][0] + b.x, acc[m][n][1] + b.y);
-        v.y = relu2(acc[m][n][2] + b.z, acc[m][n][3] + b.w);
+        v.x = pack2((b & 1u) ? acc[m][n][0] : 0.f, (b & 2u) ? acc[m][n][1] : 0.f);
+        v.y = pack2((b & 4u) ? acc[m][n][2] : 0.f, (b & 8u) ? acc[m][n][3] : 0.f);
         *reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col) = v;
-        if (with_mask)
-          M1[(rw + m * 16 + lr) * 64 + wng * 16 + lg * 4 + n] =
-              (uint8_t)(((v.x & 0xffffu) != 0) | (((v.x >> 16) != 0) << 1) | (((v.y & 0xffffu) != 0) << 2) |
-                        (((v.y >> 16) != 0) << 3));
       }
     }
   };
@@ -632,8 +626,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   stamp(1);
   if constexpr (ONE) bar();  // the X ring shares the image H1 goes to
   stamp(12);
-  if constexpr (BIG) relu_out_wide(R1, true, BS);
-  else relu_out(a.b1, R1, true);
+  relu_out(BIG ? BS : a.b1, R1, true);
   stamp(13);
   }
   bar();
@@ -663,17 +656,19 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   }
   stamp(3);
   short8_t w3f[KS2];  // layer-3 weights, prefetched under the ReLU-2 epilogue
-  if constexpr (!W3LDS) {
+  if constexpr (!ONE) {
 #pragma unroll
     for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
   }
   if constexpr (ONE) bar();  // every wave is done reading H1: H2 replaces it
   stamp(14);
-  if constexpr (BIG) relu_out_wide(R0, false, BS + HID);
-  else relu_out(a.b2, R0, false);
+  relu_out(BIG ? BS + HID : a.b2, R0, false);
   if constexpr (W3LDS) {  // from the copy of W3 staged in the dZ image at the start (no global load)
 #pragma unroll
     for (int ks = 0; ks < KS2; ++ks) w3f[ks] = lds8(RZ + ks * 512 + lane * 8);
+  } else if constexpr (ONE) {  // after the epilogue: the 32 registers would push past the 168 budget
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
   }
   bar();
   stamp(4);
@@ -824,7 +819,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
     // HBM (8 B per fragment row), and the db1 partial as fp32 column sums (DPP over the
     // 16 rows of a fragment).  The LDS image + barrier + re-read of the other tiles cost
     // ~16k cycles here with every CU in this phase at once (profiles/r03_big).
-    int mbo = (rw + lr) * 64 + wng * 16 + lg * 4;
+    int mbo = (rw + lr) * 64 + (cw >> 2) + lg;
     asm volatile("" : "+v"(mbo));
     const uint8_t* M1b = M1 + mbo;
     const auto dst = __builtin_amdgcn_make_buffer_rsrc(a.dh1 + (long)row0 * HID, 0, BM * HID * 2, 0x00020000);
@@ -842,13 +837,13 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
       for (int n = 0; n < NF; ++n) cs[hr][n] = zero4();
 #pragma unroll
     for (int m = 0; m < MF; ++m) {
-      const int b4 = *reinterpret_cast<const int*>(M1b + (m * 16) * 64);  // the 4 nibbles of n = 0..3
 #pragma unroll
       for (int n = 0; n < NF; ++n) {
+        const int b = M1b[(m * 16) * 64 + n * 4];
         floatx4_t v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)  // bit 8 n + r sign-extended to an all-ones / zero mask
-          v[r] = __int_as_float(__float_as_int(acc[m][n][r]) & __builtin_amdgcn_sbfe(b4, 8 * n + r, 1));
+        for (int r = 0; r < 4; ++r)  // bit r sign-extended to an all-ones / zero mask
+          v[r] = __int_as_float(__float_as_int(acc[m][n][r]) & __builtin_amdgcn_sbfe(b, r, 1));
         cs[m >> 2][n] += v;
         const floatx4_t vs = v * sc;
         hv[n][0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(vs[0], vs[1]));
@@ -896,7 +891,12 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
     }
     stamp(15);
   } else {
-    masked_out(R1);
+    if constexpr (ONE) {
+      bar();  // every wave is done reading dH2: dH1 replaces it
+      masked_bits_out(R1);
+    } else {
+      masked_out(R1);
+    }
     bar();
     stamp(15);
     copy_out_f16<BM, NT, HID>(R1, HS_LD, a.dh1 + (long)row0 * HID, HID, tid, a.dh1_scale);
