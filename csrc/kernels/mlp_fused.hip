@@ -109,6 +109,7 @@ struct MlpRowArgs {
   uint16_t *dh2, *dh1;                 // row-major [batch][256]: dH2 bf16, dH1 fp16 (scaled)
   float *loss, *correct, *logits;
   unsigned long long* stamps;  // diagnostics: per-workgroup phase timestamps (nullptr in production)
+  int stagger;                 // experiment: s_sleep(127) rounds before the second half of the grid starts
 };
 
 // Fully unrolled K loop with a D-deep register ring for the per-wave B operand
@@ -317,6 +318,10 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   auto stamp = [&](int i) {
     if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
   };
+  // Stagger experiment: the grid's second half (the second workgroup of each CU when the first
+  // half fills the chip) starts later, so the two co-resident workgroups are out of phase.
+  if (a.stagger > 0 && blockIdx.x >= gridDim.x / 2)
+    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   stamp(0);
   // Workgroup barrier.  The 256-row tile (one workgroup per CU) waits only for LDS
   // traffic: __syncthreads() also drains every outstanding global store (vmcnt(0)), and
@@ -1708,6 +1713,11 @@ int sl_mlp_set_stamps(unsigned long long* p) {
   g_stamps = p;
   return 0;
 }
+static int g_stagger = 0;
+int sl_mlp_set_stagger(int n) {
+  g_stagger = n;
+  return 0;
+}
 static int g_rows_bm = 0;  // 0: auto; 64 / 256 force a tile height (benchmarks, tests)
 int sl_mlp_set_rows_bm(int bm) {
   g_rows_bm = bm;
@@ -1740,6 +1750,7 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.h1 = h1; a.w3p = w3p; a.dh2 = dh2; a.dh1 = dh1;
   a.loss = loss; a.correct = correct; a.logits = logits;
   a.stamps = g_stamps;
+  a.stagger = g_stagger;
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
   // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_fwd1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);

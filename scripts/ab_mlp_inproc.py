@@ -26,11 +26,12 @@ from serverless_learn_amd.ops import _native
 ap = argparse.ArgumentParser()
 ap.add_argument("--bm", default="64,256")
 ap.add_argument("--l1", default=None, help="comma list of layer-1 kernels: fwd1, l1, none")
+ap.add_argument("--stagger", default=None, help="comma list of rows-kernel stagger counts (s_sleep(127) rounds)")
 ap.add_argument("--rounds", type=int, default=8)
 ap.add_argument("--steps", type=int, default=50)
 ap.add_argument("--batch", type=int, default=65536)
 a = ap.parse_args()
-arms = a.l1.split(",") if a.l1 else [int(v) for v in a.bm.split(",")]
+arms = a.l1.split(",") if a.l1 else ([int(v) for v in a.stagger.split(",")] if a.stagger else [int(v) for v in a.bm.split(",")])
 B = a.batch
 ap_nb = int(os.environ.get("SL_AB_BATCHES", "4"))  # shard size in batches (4: X streams from HBM, as in bench.py)
 x, y = make_mnist_like(B * ap_nb, seed=0)
@@ -42,6 +43,8 @@ for r in range(a.rounds):
     for bm in arms:
         if a.l1:
             tr.l1_kernel = None if bm == "none" else bm
+        elif a.stagger:
+            _native.call("sl_mlp_set_stagger", bm)
         else:
             _native.call("sl_mlp_set_rows_bm", bm)
         tr.graph = None

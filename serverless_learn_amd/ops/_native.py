@@ -35,6 +35,7 @@ _SIGS: dict[str, list] = {
     "sl_mlp_wgrad": [I, P, P, I, P, P, P, P, I, P, I, L, P],
     "sl_mlp_wgrad_slices": [I, I],
     "sl_mlp_set_rows_bm": [I],
+    "sl_mlp_set_stagger": [I],
     "sl_conv_set_halo": [I],
     "sl_conv_set_phase": [I],
     "sl_mlp_rows_bm": [I],
