@@ -934,10 +934,12 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
 // lane map, scripts/probes/tr8_probe.hip: per 16-lane group, lane 2q+p
 // addresses row q bytes 8p..8p+7; lane i receives column i of the 8 rows).
 // dW1 has 784 columns: its 7th tile holds 16 real ones, and the waves past
-// them skip their MFMAs (the tile count per slice stays 9).
+// them skip their MFMAs.  dW1's 7 tiles and dW2's 2 tiles may be split into
+// different slice counts (WgProblem::slices; slab regions of slices a problem
+// does not have are never read).
 //
 // The rows kernel writes per-64-row partial rows: [dW3 | db3] and the column
-// sums of dH1 / dH2 (db1 / db2).  Before its main loop each workgroup sums a
+// sums of dH1 / dH2 (db1 / db2).  After its main loop each dW1 workgroup sums a
 // band of those columns over its slice's stages into the slice's slab, so the
 // slab carries every gradient and mlp_sgd_kernel needs no special case.
 // ---------------------------------------------------------------------------
@@ -958,11 +960,15 @@ struct WgProblem {
   int n_real, tiles_n, tile_base;
   long w_off, b_off;  // flat destinations of dW ([256][n_real]) and db
   int bias_part;      // this problem's db partial inside the rows kernel's partial rows
+  // Split-K per problem: a dW2 stage moves 48 KB into LDS, a dW1 stage 40 KB (u8 X), so the
+  // two problems may cut the batch into different slice counts.  The problem's workgroups are
+  // logical ids [wg_base, wg_base + slices * tiles_n), slice-major (a slice's tiles are
+  // consecutive: the same XCD, sharing the A rows in its L2).
+  int slices, steps_per_slice, wg_base;
 };
 struct WgArgs {
   WgProblem p[2];  // dW1 (u8 X), dW2 (H1); dW3 comes from the rows kernel's partials
-  int total_tiles;
-  int steps_per_slice, total_steps;  // 64-row stages
+  int total_steps;  // 64-row stages
   float* slab;
   long slab_stride;
   const int* cursor;  // X is the resident shard: rows start at batch_base(cursor)
@@ -1100,14 +1106,13 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int wm = 1 ? (wave & 1) : (wave & 3), wn = 1 ? (wave >> 1) : (wave >> 2);
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int s = logical / A.total_tiles;
-  const int t = logical - s * A.total_tiles;
-  const int pi = t >= A.p[1].tile_base ? 1 : 0;
+  const int pi = logical >= A.p[1].wg_base ? 1 : 0;
   const WgProblem& P = A.p[pi];
-  const int tn = t - P.tile_base;
+  const int s = (logical - P.wg_base) / P.tiles_n;
+  const int tn = logical - P.wg_base - s * P.tiles_n;
   const int n0 = tn * 128;
-  const int st0 = s * A.steps_per_slice;
-  const int nst = min(A.steps_per_slice, A.total_steps - st0);
+  const int st0 = s * P.steps_per_slice;
+  const int nst = min(P.steps_per_slice, A.total_steps - st0);
   const bool u8b = pi == 0;
   // n-blocks of this wave that hold real columns (dW1's last tile: 16 columns)
   const int nvalid = __builtin_amdgcn_readfirstlane(min(WG_NJ, max(0, (P.n_real - n0 - wn * 16 * WG_NJ + 15) / 16)));
@@ -1363,7 +1368,8 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
-  // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
+  // 64 rows), by the dW1 workgroups only (their slices own the slab's partial-row region):
+  // dW1 tile tn of the slice takes a band of float4 columns, G row groups per column,
   // a fixed-order sum through LDS (deterministic).  Done HERE, around the slab stores: the
   // loads are issued first (every row of the band at once, clamped indices so no branch
   // splits them), the accumulator stores go out while they are in flight, and the sum
@@ -1371,11 +1377,11 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // main loop; the store tail is issue-bound (~16 us, profiles/r03_wgrad) and hides it. ----
   constexpr int NC4 = W3P_LD / 4;
   constexpr int PR_MAX = 12;  // partial rows per thread held in registers (else a plain loop)
-  const int per = (NC4 + A.total_tiles - 1) / A.total_tiles;
-  const int c0 = t * per, nc = min(NC4, c0 + per) - c0;
-  const int G = WG_NT / nc, col = tid % nc, g = tid / nc;
+  const int per = (NC4 + A.p[0].tiles_n - 1) / A.p[0].tiles_n;
+  const int c0 = tn * per, nc = pi == 0 ? min(NC4, c0 + per) - c0 : 1;
+  const int G = pi == 0 ? WG_NT / nc : 0, col = tid % nc, g = tid / nc;
   const float4* psrc = reinterpret_cast<const float4*>(A.w3p + (long)st0 * W3P_LD) + c0 + col;
-  const bool pr_regs = (nst + G - 1) / G <= PR_MAX;
+  const bool pr_regs = G > 0 && (nst + G - 1) / G <= PR_MAX;
   float4 pv[PR_MAX];
   if (g < G && pr_regs) {
 #pragma unroll
@@ -1422,7 +1428,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __syncthreads();  // every wave is done with the ring
   if (g < G) red[g * nc + col] = sum;
   __syncthreads();
-  if (g == 0) {
+  if (g == 0 && G > 0) {
     float4 tot = red[col];
     for (int i = 1; i < G; ++i) {
       const float4 v = red[i * nc + col];
@@ -1445,7 +1451,7 @@ struct SgdArgs {
   float* w;
   float* mom;
   const float* slab;
-  int slices;
+  int slices, slices2;   // slab slices of the dW1 tiles + partial-row region / of the dW2 tiles
   long slab_stride;
   const float* grad_in;  // used when slab == nullptr
   float* grad_out;       // reduced gradient written here (all-reduce hand-off)
@@ -1554,16 +1560,17 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
   float db = 0.f;
   const float* src = a.slab + off;
   const float* dbs = a.slab + TL_SMALL + W3P_DB1 + (w1row >= 0 ? w1row : 0);
+  const int ns = off >= TL_W2 && off < TL_SMALL ? a.slices2 : a.slices;
   constexpr int U = 8;
-  for (int s0 = part; s0 < a.slices; s0 += SGD_TPG * U) {
+  for (int s0 = part; s0 < ns; s0 += SGD_TPG * U) {
     float4 v[U];
     float d[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const int sidx = s0 + k * SGD_TPG;
-      v[k] = sidx < a.slices ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-      d[k] = (w1row >= 0 && sidx < a.slices) ? dbs[(long)sidx * a.slab_stride] : 0.f;
+      v[k] = sidx < ns ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      d[k] = (w1row >= 0 && sidx < ns) ? dbs[(long)sidx * a.slab_stride] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
@@ -1606,54 +1613,12 @@ __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
     if (mine) write_shadow(a, p, a.w[p]);
     return;
   }
-  const bool full = p0 + 4 <= a.n;
   // the update's own operands, in flight together with the slab loads
   const bool upd = mine && a.mode != 1;
   const float w0 = upd ? a.w[p] : 0.f;
   const float m0 = upd && a.mom ? a.mom[p] : 0.f;
-  float g[4] = {0.f, 0.f, 0.f, 0.f};
-  float gme;
-  if (a.slab) {
-    if (full) {
-      // All of a thread's slab loads (and dW1's db1 loads) are issued before the first
-      // wait: the plain loop waited vmcnt(0) per slice, two chains of 7 dependent
-      // ~1 us loads (12.4 us per call).
-      const float* src = a.slab + p0;
-      const bool w1row = p0 < P_B1;  // dW1 = a * (dH1^T X) + b * db1 (x) 1; 784 % 4 == 0: one row per group
-      const float* dbs = a.slab + P_B1 + (w1row ? p0 / D_IN : 0);
-      float db = 0.f;
-      constexpr int U = 8;  // slices per thread per batch of loads (28 slices / 4 threads = 7)
-      for (int s0 = part; s0 < a.slices; s0 += SGD_TPG * U) {
-        float4 v[U];
-        float d[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int sidx = s0 + u * SGD_TPG;
-          v[u] = sidx < a.slices ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-          d[u] = (w1row && sidx < a.slices) ? dbs[(long)sidx * a.slab_stride] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          g[0] += v[u].x; g[1] += v[u].y; g[2] += v[u].z; g[3] += v[u].w;
-          db += d[u];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) g[j] = group_sum(g[j]);
-      gme = g[part & 3];
-      if (w1row) {
-        db = group_sum(db);
-        gme = a.xa * gme + a.xb * db;
-      }
-    } else {
-      gme = 0.f;
-      if (mine)
-        for (int sidx = 0; sidx < a.slices; ++sidx) gme += a.slab[(long)sidx * a.slab_stride + p];
-    }
-  } else {
-    gme = mine ? a.grad_in[p] : 0.f;
-  }
+  // (slab input took the sgd_tiled path above)
+  const float gme = mine ? a.grad_in[p] : 0.f;
   if (!mine) return;
   float* gout = a.grad_out;
   if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
@@ -1780,44 +1745,55 @@ int sl_mlp_wgrad_slices(int batch, int requested) {
   return (total + spp - 1) / spp;
 }
 
+// Slices of the dW2 tiles for dW1 slices `slices` (requested <= 0: the default split).  A dW2
+// stage moves 48 KB into LDS against 40 KB for dW1, so a finer dW2 split balances the two
+// problems' workgroups; 7 s1 + 2 s2 <= 256 keeps the grid within one workgroup per CU.
+int sl_mlp_wgrad_slices2(int batch, int slices, int requested) {
+  if (sl_mlp_wgrad_slices(batch, slices) != slices) return -1;
+  return sl_mlp_wgrad_slices(batch, requested > 0 ? requested : slices);
+}
+
 // x: the resident u8 shard [n_batches * batch][784]; the batch rows are the
 // ones the rows kernel used (cursor not yet bumped: mlp_sgd_kernel bumps it).
 int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, const uint16_t* h1,
                  const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
-                 long slab_stride, hipStream_t stream) {
+                 int slices2, long slab_stride, hipStream_t stream) {
   if (!w3p || n_w3p != batch / 64) return -1;
   if (slab_stride < TL_STRIDE) return -1;
   const int s_eff = sl_mlp_wgrad_slices(batch, slices);
-  if (s_eff <= 0 || s_eff != slices) return -1;
+  if (s_eff <= 0 || s_eff != slices || sl_mlp_wgrad_slices(batch, slices2) != slices2) return -1;
   WgArgs a;
   // dW1, db1 = dH1^T [256 x B] . X (raw u8; normalised in mlp_sgd_kernel)
   a.p[0] = WgProblem{dh1, x, D_IN, D_IN, (D_IN + 127) / 128, 0, P_W1, P_B1, W3P_DB1};
   // dW2, db2 = dH2^T . H1
   a.p[1] = WgProblem{dh2, h1, HID, HID, HID / 128, 0, P_W2, P_B2, W3P_DB2};
-  int base = 0;
-  for (int i = 0; i < 2; ++i) {
-    a.p[i].tile_base = base;
-    base += a.p[i].tiles_n;
-  }
-  a.total_tiles = base;
   a.total_steps = batch / 64;
-  a.steps_per_slice = (a.total_steps + slices - 1) / slices;
+  int base = 0, wgs = 0;
+  for (int i = 0; i < 2; ++i) {
+    WgProblem& q = a.p[i];
+    q.tile_base = base;
+    q.slices = i ? slices2 : slices;
+    q.steps_per_slice = (a.total_steps + q.slices - 1) / q.slices;
+    q.wg_base = wgs;
+    base += q.tiles_n;
+    wgs += q.tiles_n * q.slices;
+  }
   a.slab = slab; a.slab_stride = slab_stride;
   a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
   a.w3p = w3p; a.n_w3p = n_w3p;
   if (((uintptr_t)x & 15) != 0 || ((uintptr_t)w3p & 15) != 0) return -2;  // 16-B pieces / float4 reads
-  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(WG_NT), 0, stream, a);
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(wgs), dim3(WG_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
 
-int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_stride, const float* grad_in,
+int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, int slices2, long slab_stride, const float* grad_in,
                float* grad_out, float lr, float mu, float wd, float xa, float xb, int mode, uint16_t* w1h,
                uint16_t* w2h,
                uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, uint16_t* w1f, int* cursor, hipStream_t stream) {
   SgdArgs a = {};
   a.w1f = w1f;
-  a.w = w; a.mom = mom; a.slab = slab; a.slices = slices; a.slab_stride = slab_stride;
+  a.w = w; a.mom = mom; a.slab = slab; a.slices = slices; a.slices2 = slices2; a.slab_stride = slab_stride;
   a.grad_in = grad_in; a.grad_out = grad_out; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = mode;
   a.xa = xa; a.xb = xb;
   a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
@@ -1833,11 +1809,12 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
 }
 
 // Slab reduction straight into this rank's xGMI exchange slot for the step in flight.
-int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa, float xb, float* slot0,
+int sl_mlp_reduce_xgmi(const float* slab, int slices, int slices2, long slab_stride, float xa, float xb, float* slot0,
                        float* slot1, const unsigned* ctl, hipStream_t stream) {
   if (!slab || !slot0 || !slot1 || !ctl || (slab_stride & 3)) return -1;
   SgdArgs a = {};
-  a.slab = slab; a.slices = slices; a.slab_stride = slab_stride; a.grad_out = slot0; a.grad_out_alt = slot1;
+  a.slab = slab; a.slices = slices; a.slices2 = slices2; a.slab_stride = slab_stride; a.grad_out = slot0;
+  a.grad_out_alt = slot1;
   a.ar_ctl = ctl; a.n = P_N; a.xa = xa; a.xb = xb; a.mode = 1;
   if (slab_stride < TL_STRIDE) return -1;
   const long groups = sgd_units(true);

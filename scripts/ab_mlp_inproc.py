@@ -27,21 +27,39 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--bm", default="64,256")
 ap.add_argument("--l1", default=None, help="comma list of layer-1 kernels: fwd1, l1, none")
 ap.add_argument("--stagger", default=None, help="comma list of rows-kernel stagger counts (s_sleep(127) rounds)")
+ap.add_argument("--split", default=None,
+                help="comma list of s1:s2 weight-gradient splits (dW1 tiles : dW2 tiles slices), one trainer each")
 ap.add_argument("--rounds", type=int, default=8)
 ap.add_argument("--steps", type=int, default=50)
 ap.add_argument("--batch", type=int, default=65536)
 a = ap.parse_args()
-arms = a.l1.split(",") if a.l1 else ([int(v) for v in a.stagger.split(",")] if a.stagger else [int(v) for v in a.bm.split(",")])
+if a.split:
+    arms = a.split.split(",")
+elif a.l1:
+    arms = a.l1.split(",")
+else:
+    arms = [int(v) for v in a.stagger.split(",")] if a.stagger else [int(v) for v in a.bm.split(",")]
 B = a.batch
 ap_nb = int(os.environ.get("SL_AB_BATCHES", "4"))  # shard size in batches (4: X streams from HBM, as in bench.py)
 x, y = make_mnist_like(B * ap_nb, seed=0)
-tr = FusedMLPTrainer(batch=B, device="cuda:0")
-tr.load_shard(torch.from_numpy(x), torch.from_numpy(y))
+xs, ys = torch.from_numpy(x), torch.from_numpy(y)
+if a.split:
+    trs = {}
+    for arm in arms:
+        s1, s2 = (int(v) for v in arm.split(":"))
+        trs[arm] = FusedMLPTrainer(batch=B, device="cuda:0", slices=s1, slices2=s2)
+        trs[arm].load_shard(xs, ys)
+        print(arm, "->", trs[arm].slices, trs[arm].slices2, file=sys.stderr)
+else:
+    tr = FusedMLPTrainer(batch=B, device="cuda:0")
+    tr.load_shard(xs, ys)
 t = {bm: [] for bm in arms}
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for r in range(a.rounds):
     for bm in arms:
-        if a.l1:
+        if a.split:
+            tr = trs[bm]
+        elif a.l1:
             tr.l1_kernel = None if bm == "none" else bm
         elif a.stagger:
             _native.call("sl_mlp_set_stagger", bm)
