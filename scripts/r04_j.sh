@@ -22,4 +22,10 @@ for arm in 28:28 27:32 26:37; do
   echo "== $arm"; grep -E "mlp_" $O/kernels_${s1}_${s2}.csv | cut -c1-140 || true
   rm -rf $O/prof_${s1}_${s2}
 done
+timeout -k 10 300 python scripts/ab_mlp_inproc.py --stagger 0,1,3 --rounds 5 --steps 50 > $O/ab_stagger.json 2> $O/ab_stagger.err || exit 1
+python - <<'PY'
+import json
+d = json.load(open('gpurun_out/r04_j/ab_stagger.json'))
+print("stagger", {k: round(v['median_us'], 2) for k, v in d.items() if 'median_us' in v})
+PY
 echo r04_j done
