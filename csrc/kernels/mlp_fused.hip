@@ -933,8 +933,8 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
 // per 65,536-row step.  The u8 image is read with ds_read_b64_tr_b8 (probed
 // lane map, scripts/probes/tr8_probe.hip: per 16-lane group, lane 2q+p
 // addresses row q bytes 8p..8p+7; lane i receives column i of the 8 rows).
-// dW1 has 784 columns: its 7th tile holds 16 real ones, and the waves past
-// them skip their MFMAs.  dW1's 7 tiles and dW2's 2 tiles may be split into
+// dW1 has 784 columns = 6 tiles of 128 + 16: the 6th tile's workgroups also
+// compute the 16 tail columns (their slab tile is the 7th).  dW1's 6 tiles and dW2's 2 tiles may be split into
 // different slice counts (WgProblem::slices; slab regions of slices a problem
 // does not have are never read).
 //
@@ -949,7 +949,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
 // partial-row sums in their own layout [dW3 | db3 | pad | db1 | db2].  The row-major form wrote
 // 16 rows x 64 B per store instruction; that tail took ~16 us (knockout, profiles/r03_wgrad).
 constexpr long TL_TILE = 256L * 128;            // floats per 256 x 128 tile
-constexpr long TL_W2 = 7L * TL_TILE;            // dW2 tiles (dW1: tiles 0..6, tile 6 = 16 real columns)
+constexpr long TL_W2 = 7L * TL_TILE;            // dW2 tiles (dW1: tiles 0..6; tile 6 = the 16 tail columns, written by tile 5's workgroups)
 constexpr long TL_SMALL = 9L * TL_TILE;         // [dW3 | db3 | pad | db1 | db2]
 constexpr long TL_STRIDE = (TL_SMALL + W3P_LD + 63) / 64 * 64;
 
@@ -980,12 +980,9 @@ struct WgArgs {
 constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages in flight
 constexpr int WG_IMG = 64 * 128;          // one [64 k][128] bf16 image, unpadded (swizzled)
 constexpr int WG_SLOT = 3 * WG_IMG;       // A half 0, A half 1, B = 48 KB
-// u8 tiles need only 8 KB of B per slot: 4 x 40 KB fill the 160 KB of LDS exactly
-constexpr int WG_NSLOT8 = 0 ? 4 : WG_NSLOT;
-constexpr int WG_SLOT8 = 0 ? 2 * WG_IMG + WG_IMG / 2 : WG_SLOT;
-constexpr int WG_LDS = WG_NSLOT8 * WG_SLOT8 > WG_NSLOT * WG_SLOT ? WG_NSLOT8 * WG_SLOT8 : WG_NSLOT * WG_SLOT;
-template <bool U8> constexpr int wg_ns() { return U8 ? WG_NSLOT8 : WG_NSLOT; }
-template <bool U8> constexpr int wg_slot() { return U8 ? WG_SLOT8 : WG_SLOT; }
+constexpr int WG_LDS = WG_NSLOT * WG_SLOT;
+// u8 slots use 8 KB of the 16 KB B image; the dW1 tail columns (768..783) go in the rest
+constexpr int WG_TAIL = 8192;  // bytes from the B image
 
 // 16-B chunk position inside a 256-B image row.  XOR on chunk-pair bits with
 // f(r) = (r & 3) | ((r >> 3) & 1) << 2 makes every ds_read_b64_tr_b16 of the
@@ -1023,21 +1020,6 @@ __device__ __forceinline__ uint32_t wg_tr8_addr(int n0, int lane) {
   const int g = lane >> 4, q = (lane & 15) >> 1, p = lane & 1;
   const int r = 8 * g + q;
   return (uint32_t)(r * 128 + wg_swz8(n0 >> 4, r) * 16 + 8 * p);
-}
-// The same transposed reads for the 32x32x16 operand maps: lane l takes column
-// c0 + (l & 31) (16-lane group (l >> 4) & 1 holds columns 16..31) and rows 8 (l >> 5) ..
-// +7; the swizzles are unchanged, so k-substep s (16 rows) is a constant offset
-// (s * 4096 B in a bf16 image, s * 2048 B in a u8 image: f(r) and the u8 XOR ignore bit 4).
-__device__ __forceinline__ uint32_t wg_tr_addr32(int n0, int lane) {
-  const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const int c = ((n0 + (G & 1) * 16) >> 3) + (p >> 1), w = (p & 1) * 4;
-  const int ra = 8 * (G >> 1) + q;
-  return (uint32_t)((ra * 128 + wg_swz(c, ra) * 8 + w) * 2);
-}
-__device__ __forceinline__ uint32_t wg_tr8_addr32(int n0, int lane) {
-  const int G = lane >> 4, q = (lane & 15) >> 1, p = lane & 1;
-  const int r = 8 * (G >> 1) + q;
-  return (uint32_t)(r * 128 + wg_swz8((n0 + (G & 1) * 16) >> 4, r) * 16 + 8 * p);
 }
 template <int OFF>
 __device__ __forceinline__ short4_t ds_tr16_off(uint32_t a) {
@@ -1078,12 +1060,6 @@ __device__ __forceinline__ floatx4_t wg_mma(const short8_t& b, const short8_t& a
   else return mfma16(b, a, c);
 }
 
-template <bool U8>
-__device__ __forceinline__ floatx16_t wg_mma32(const short8_t& b, const short8_t& a, const floatx16_t& c) {
-  if constexpr (U8) return mfma32h(b, a, c);
-  else return mfma32(b, a, c);
-}
-
 // vmcnt needs an immediate: wait until this wave has at most N younger stages
 // (of PPS LDS-DMA pieces each) in flight.
 template <int PPS>
@@ -1095,15 +1071,15 @@ __device__ __forceinline__ void wg_vmcnt(int younger) {
 }
 
 constexpr int WG_NT = 512;
-constexpr int WG_MI = 1 ? 8 : 4;  // 16-row A (dZ) fragments per wave
-constexpr int WG_NJ = 1 ? 2 : 4;  // 16-column B fragments per wave
+constexpr int WG_MI = 8;  // 16-row A (dZ) fragments per wave
+constexpr int WG_NJ = 2;  // 16-column B fragments per wave
 constexpr int WG_NF = WG_MI + WG_NJ;       // fragments per wave per k-step
 
 __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
-  const int wm = 1 ? (wave & 1) : (wave & 3), wn = 1 ? (wave >> 1) : (wave >> 2);
+  const int wm = wave & 1, wn = wave >> 1;
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int pi = logical >= A.p[1].wg_base ? 1 : 0;
@@ -1114,58 +1090,68 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int st0 = s * P.steps_per_slice;
   const int nst = min(P.steps_per_slice, A.total_steps - st0);
   const bool u8b = pi == 0;
-  // n-blocks of this wave that hold real columns (dW1's last tile: 16 columns)
-  const int nvalid = __builtin_amdgcn_readfirstlane(min(WG_NJ, max(0, (P.n_real - n0 - wn * 16 * WG_NJ + 15) / 16)));
+  // dW1's last tile (columns 640..767) also computes the 16 columns 768..783 ("tail"): each
+  // wave takes them for two of its eight m-fragments (m-fragments 2 wn, 2 wn + 1), +12.5 % MFMAs,
+  // instead of a tile of its own that streamed all of dH1 for 16 columns (28 of 252 workgroups).
+  const bool tail = u8b && tn == P.tiles_n - 1;
 
   // LDS-DMA map: bf16 [64][128] images -- wave w, piece j (0..1) covers rows 4 (2w + j) .. +3,
   // lane -> row 4 (2w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row);
   // A is two such images (m 0..127, 128..255).  u8 image: wave w covers rows 8w .. 8w+7,
-  // lane -> row + lane / 8, LDS chunk lane % 8 <- global chunk swz8(lane % 8, row).
+  // lane -> row + lane / 8, LDS chunk lane % 8 <- global chunk swz8(lane % 8, row).  The tail
+  // image sits in the u8 slot's free second 8 KB: wave w's 1 KB holds 8 copies of rows
+  // 8w .. 8w+7 x 16 B (lane -> row 8w + lane % 8), so a tr read group can take its own copy.
+  // (wave-uniform 64-bit bases + 32-bit per-lane byte offsets: four fewer VGPRs than per-lane pointers)
   const int prow = lane >> 4;
-  const uint16_t* asrc[2];
-  const uint16_t* bsrc[2];
   const long xrow0 = batch_base(A.cursor, A.n_batches, A.batch);
+  const char* abase = static_cast<const char*>(P.a) + (long)st0 * 64 * HID * 2;
+  const char* bbase = static_cast<const char*>(P.b) + (u8b ? (xrow0 + st0 * 64) * P.ldb : (long)st0 * 64 * P.ldb * 2);
+  uint32_t aoff[2], boff[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int row = 4 * (2 * wave + j) + prow;
     const int c = wg_swz(lane & 15, row);
-    asrc[j] = static_cast<const uint16_t*>(P.a) + (long)(st0 * 64 + row) * HID + c * 8;
-    bsrc[j] = static_cast<const uint16_t*>(P.b) + (long)(st0 * 64 + row) * P.ldb + n0 + c * 8;
+    aoff[j] = (uint32_t)((row * HID + c * 8) * 2);
+    boff[j] = (uint32_t)((row * P.ldb + n0 + c * 8) * 2);
   }
-  const uint8_t* bsrc8;
+  uint32_t boff8, toff8;
   {
     const int row = 8 * wave + (lane >> 3);
-    const int c = wg_swz8(lane & 7, row);
-    const int col = min(n0 + c * 16, P.ldb - 16);  // columns >= 784 are don't-care columns of dW1
-    bsrc8 = static_cast<const uint8_t*>(P.b) + (xrow0 + st0 * 64 + row) * P.ldb + col;
+    boff8 = (uint32_t)(row * P.ldb + n0 + wg_swz8(lane & 7, row) * 16);
+    toff8 = (uint32_t)((8 * wave + (lane & 7)) * P.ldb + (D_IN - 16));
   }
-  auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % NS
+  auto issue = [&](int st, auto u8_c, auto tail_c) {  // stage st (relative to the slice) -> ring slot st % NS
     constexpr bool U8 = decltype(u8_c)::value;
-    uint16_t* Ai = smem + (st % wg_ns<U8>()) * wg_slot<U8>();
+    uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
     uint16_t* Bi = Ai + 2 * WG_IMG;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(asrc[j] + (long)st * 64 * HID + h * 128),
+            (const __attribute__((address_space(1))) void*)(abase + aoff[j] + (st * 64 * HID + h * 128) * 2),
             (SL_LDS void*)(Ai + h * WG_IMG + 4 * (2 * wave + j) * 128), 16, 0, 0);
     if constexpr (U8) {
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc8 + (long)st * 64 * P.ldb),
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bbase + boff8 + st * 64 * P.ldb),
                                        (SL_LDS void*)(reinterpret_cast<uint8_t*>(Bi) + 8 * wave * 128), 16, 0, 0);
+      if constexpr (decltype(tail_c)::value)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bbase + toff8 + st * 64 * P.ldb),
+                                         (SL_LDS void*)(reinterpret_cast<uint8_t*>(Bi) + WG_TAIL + wave * 1024), 16, 0, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[j] + (long)st * 64 * P.ldb),
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bbase + boff[j] + st * 64 * P.ldb * 2),
                                          (SL_LDS void*)(Bi + 4 * (2 * wave + j) * 128), 16, 0, 0);
     }
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if (u8b) {
-    for (int st = 0; st < wg_ns<true>() - 1 && st < nst; ++st) issue(st, T_{});
+  if (tail) {
+    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, T_{}, T_{});
+  } else if (u8b) {
+    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, T_{}, F_{});
   } else {
-    for (int st = 0; st < wg_ns<false>() - 1 && st < nst; ++st) issue(st, F_{});
+    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, F_{}, F_{});
   }
 
   floatx4_t acc[WG_MI][WG_NJ];
@@ -1173,6 +1159,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
     for (int j = 0; j < WG_NJ; ++j) acc[i][j] = zero4();
+  floatx4_t tacc[2] = {zero4(), zero4()};  // tail columns of m-fragments 2 wn, 2 wn + 1
 
   // per-lane tr-read byte addresses within a slot; k-step 1 is a constant offset
   const uint32_t lds_base = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
@@ -1187,8 +1174,11 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     const int c = wn * 16 * WG_NJ + j * 16;
     b_addr[j] = 2 * WG_IMG * 2 + (u8b ? wg_tr8_addr(c, lane) : wg_tr_addr(c, lane));
   }
+  // tail tr_b8 read: 16-lane group g takes rows 8g .. 8g+7 (wave block g, copy g: distinct banks),
+  // lane 2q + p row 8g + q bytes 8p..; k-step 1 (rows 32..63) is +4 KB
+  const uint32_t t_addr = 2 * WG_IMG * 2 + WG_TAIL + (lane >> 4) * (1024 + 128) + ((lane & 15) >> 1) * 16 + 8 * (lane & 1);
 
-  // Instantiated per (u8, live n-blocks) and selected by a scalar branch OUTSIDE the loop
+  // Instantiated per (u8, tail wave) and selected by a scalar branch OUTSIDE the loop
   // (conditions inside made hipcc copy every accumulator AGPR<->VGPR).
   // Software-pipelined: the fragment reads of stage st+1 are issued right
   // after the barrier that publishes it and run under stage st's MFMAs (two
@@ -1197,54 +1187,44 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // per stage back to back (knockout "reads + MFMAs only": 45.7 us).
   // The slot of stage st is refilled (stage st+3) after the barrier of step st,
   // when every wave has waited for its own reads of stage st.
-  auto mainloop_pipe = [&](auto u8_c, auto nb_c) {
+  auto mainloop_pipe = [&](auto u8_c, auto tl_c) {
     constexpr bool U8 = decltype(u8_c)::value;
-    constexpr int NB = decltype(nb_c)::value;
-    constexpr int NBR = NB > 0 ? NB : 1;
-    constexpr int PPS = U8 ? 5 : 6;
+    constexpr int TL = decltype(tl_c)::value;  // this wave's wn in the tail tile, else -1
+    constexpr bool TAIL = TL >= 0;
+    using TailC = std::integral_constant<bool, TAIL>;
+    constexpr int PPS = U8 ? (TAIL ? 6 : 5) : 6;
     constexpr int KB = U8 ? 4096 : 8192;
-    constexpr int NS = wg_ns<U8>(), SLOT = wg_slot<U8>();  // ring depth / slot stride (uint16)
+    constexpr int NS = WG_NSLOT, SLOT = WG_SLOT;  // ring depth / slot stride (uint16)
     short8_t fa[2][2][WG_MI]; // [set][k-step][m-block]
-    short8_t fb[2][2][NBR];   // bf16 B fragments
-    uint2v_t fr[2][2][NBR];   // raw u8 B fragments (converted next to their MFMAs)
-    short8_t fc[2][2][NBR];   // converted u8 B fragments (1 schedule)
-    auto read_stage = [&](int st, auto set_c) {
-      constexpr int S = decltype(set_c)::value;
-      if constexpr (NB > 0) {
-        const uint32_t sb = lds_base + (uint32_t)((st % NS) * SLOT * 2);
-#pragma unroll
-        for (int i = 0; i < WG_MI; ++i) fa[S][0][i] = wg_tr8<0>(sb + a_addr[i]);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if constexpr (U8) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
-          else fb[S][0][j] = wg_tr8<0>(sb + b_addr[j]);
-        }
-#pragma unroll
-        for (int i = 0; i < WG_MI; ++i) fa[S][1][i] = wg_tr8<8192>(sb + a_addr[i]);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if constexpr (U8) fr[S][1][j] = ds_tr8_off<KB>(sb + b_addr[j]);
-          else fb[S][1][j] = wg_tr8<KB>(sb + b_addr[j]);
-        }
+    short8_t fb[2][2][WG_NJ]; // bf16 B fragments
+    uint2v_t fr[2][2][WG_NJ]; // raw u8 B fragments (converted next to their MFMAs)
+    short8_t fc[2][2][WG_NJ]; // converted u8 B fragments (1 schedule)
+    // raw tail fragments: one set, read for the next stage after this stage's tail MFMAs took theirs
+    uint2v_t ft[2];
+    auto read_tail = [&](uint32_t sb) {
+      if constexpr (TAIL) {
+        ft[0] = ds_tr8_off<0>(sb + t_addr);
+        ft[1] = ds_tr8_off<4096>(sb + t_addr);
       }
     };
-    auto mfmas = [&](auto set_c) {
+    auto read_stage = [&](int st, auto set_c) {
       constexpr int S = decltype(set_c)::value;
-      if constexpr (NB > 0) {
+      const uint32_t sb = lds_base + (uint32_t)((st % NS) * SLOT * 2);
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          short8_t b[NBR];
+      for (int i = 0; i < WG_MI; ++i) fa[S][0][i] = wg_tr8<0>(sb + a_addr[i]);
 #pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            if constexpr (U8) b[j] = u8x8_f16_biased(fr[S][k][j]);
-            else b[j] = fb[S][k][j];
-          }
-#pragma unroll
-          for (int i = 0; i < WG_MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NB; ++j) acc[i][j] = wg_mma<U8>(b[j], fa[S][k][i], acc[i][j]);
-        }
+      for (int j = 0; j < WG_NJ; ++j) {
+        if constexpr (U8) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
+        else fb[S][0][j] = wg_tr8<0>(sb + b_addr[j]);
       }
+#pragma unroll
+      for (int i = 0; i < WG_MI; ++i) fa[S][1][i] = wg_tr8<8192>(sb + a_addr[i]);
+#pragma unroll
+      for (int j = 0; j < WG_NJ; ++j) {
+        if constexpr (U8) fr[S][1][j] = ds_tr8_off<KB>(sb + b_addr[j]);
+        else fb[S][1][j] = wg_tr8<KB>(sb + b_addr[j]);
+      }
+      read_tail(sb);
     };
     // one fragment of the next stage (f: A k0 i0..MI-1, B k0, A k1, B k1), for the interleave
     auto read_frag = [&](uint32_t sb, int f, auto set_c) {
@@ -1253,7 +1233,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       if (w < WG_MI) {
         if (k == 0) fa[S][0][w] = wg_tr8<0>(sb + a_addr[w]);
         else fa[S][1][w] = wg_tr8<8192>(sb + a_addr[w]);
-      } else if (w - WG_MI < NB) {
+      } else {
         const int j = w - WG_MI;
         if constexpr (U8) {
           if (k == 0) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
@@ -1273,6 +1253,18 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
         __builtin_amdgcn_sched_barrier(0);
       }
     };
+    // the tail's 2 MFMAs per k-step (current set)
+    auto tail_mfmas = [&](auto cur_c) {
+      constexpr int C = decltype(cur_c)::value;
+      if constexpr (TAIL) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const short8_t bt = u8x8_f16_biased(ft[k]);
+          tacc[0] = wg_mma<true>(bt, fa[C][k][2 * TL], tacc[0]);
+          tacc[1] = wg_mma<true>(bt, fa[C][k][2 * TL + 1], tacc[1]);
+        }
+      }
+    };
     // The next stage's fragment reads are interleaved one per ~two MFMAs: issued
     // as one burst after the barrier, the 8 waves' reads queued behind each other
     // and the MFMAs waited for the queue (reads and MFMAs did not overlap).  The
@@ -1282,11 +1274,13 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       if (st + 1 < nst) {
         wg_vmcnt<PPS>(min(NS - 2, nst - 2 - st));  // stage st+1 has landed (st+2 .. st+NS-1 may be in flight)
         __builtin_amdgcn_s_barrier();          // ... for everyone; every wave is done reading stage st
-        if (st + NS < nst) issue(st + NS, u8_c);  // into stage st's slot
+        if (st + NS < nst) issue(st + NS, u8_c, TailC{});  // into stage st's slot
       }
+      // the tail MFMAs first: the next stage's fragments (set N) are not live yet
+      tail_mfmas(cur_c);
       const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % NS) * SLOT * 2);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (U8 && NB > 0) {
+      if constexpr (U8) {
         // u8 -> bf16 conversions off the MFMA critical path: k-step 1's fragments
         // (landed at the end of the previous step) are converted under k-step 0's
         // MFMAs, the next stage's k-step-0 fragments under k-step 1's second half.
@@ -1297,8 +1291,8 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int j = q / WG_MI, i = q % WG_MI;
-            if (j < NB) acc[i][j] = wg_mma<U8>(fc[C][k][j], fa[C][k][i], acc[i][j]);
-            if (k == 0 && q % WG_MI == 1 && j < NB) {
+            acc[i][j] = wg_mma<U8>(fc[C][k][j], fa[C][k][i], acc[i][j]);
+            if (k == 0 && q % WG_MI == 1) {
               fc[C][1][j] = u8x8_f16_biased(fr[C][1][j]);
               asm volatile("" : "+v"(fc[C][1][j]));
             }
@@ -1308,7 +1302,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
               asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * (8 * WG_NF / 16)) : "memory");
               __builtin_amdgcn_sched_barrier(0);
             }
-            if (k == 1 && q >= 8 && (q & 1) == 0 && ((q - 8) >> 1) < NB) {
+            if (k == 1 && q >= 8 && (q & 1) == 0 && ((q - 8) >> 1) < WG_NJ) {
               short8_t& d = fc[N][0][(q - 8) >> 1];
               d = u8x8_f16_biased(fr[N][0][(q - 8) >> 1]);
               asm volatile("" : "+v"(d));  // keep it here (LLVM sinks it past the back edge otherwise)
@@ -1316,24 +1310,18 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
             reads_after(sbn, k, q, nxt_c);
           }
         }
-      } else
-      if constexpr (NB > 0) {
+      } else {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-          short8_t b[NBR];
-#pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            if constexpr (U8) b[j] = u8x8_f16_biased(fr[C][k][j]);
-            else b[j] = fb[C][k][j];
-          }
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int i = q / WG_NJ, j = q % WG_NJ;
-            if (j < NB) acc[i][j] = wg_mma<U8>(b[j], fa[C][k][i], acc[i][j]);
+            acc[i][j] = wg_mma<U8>(fb[C][k][j], fa[C][k][i], acc[i][j]);
             reads_after(sbn, k, q, nxt_c);
           }
         }
       }
+      read_tail(sbn);
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -1342,28 +1330,29 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     using S1 = std::integral_constant<int, 1>;
     wg_vmcnt<PPS>(min(NS - 2, nst - 1));  // stage 0 has landed (stages 1 .. NS-2 may be in flight)
     __builtin_amdgcn_s_barrier();
-    if (NS - 1 < nst) issue(NS - 1, u8_c);  // the last slot: free once the prologue sums are done
+    if (NS - 1 < nst) issue(NS - 1, u8_c, TailC{});  // the last slot: free once the prologue sums are done
     read_stage(0, S0{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (U8) {
 #pragma unroll
-      for (int j = 0; j < NB; ++j) fc[0][0][j] = u8x8_f16_biased(fr[0][0][j]);
+      for (int j = 0; j < WG_NJ; ++j) fc[0][0][j] = u8x8_f16_biased(fr[0][0][j]);
     }
     for (int st = 0; st < nst; st += 2) {
       step(st, S0{}, S1{});
       if (st + 1 < nst) step(st + 1, S1{}, S0{});
     }
   };
-  using I4 = std::integral_constant<int, WG_NJ>;  // all n-blocks live
-  using I1 = std::integral_constant<int, 1>;
-  using I0 = std::integral_constant<int, 0>;
-  if (u8b) {
-    if (nvalid >= WG_NJ) mainloop_pipe(T_{}, I4{});
-    else if (nvalid >= 1) mainloop_pipe(T_{}, I1{});
-    else mainloop_pipe(T_{}, I0{});
+  using IN = std::integral_constant<int, -1>;
+  if (tail) {
+    if (wn == 0) mainloop_pipe(T_{}, std::integral_constant<int, 0>{});
+    else if (wn == 1) mainloop_pipe(T_{}, std::integral_constant<int, 1>{});
+    else if (wn == 2) mainloop_pipe(T_{}, std::integral_constant<int, 2>{});
+    else mainloop_pipe(T_{}, std::integral_constant<int, 3>{});
+  } else if (u8b) {
+    mainloop_pipe(T_{}, IN{});
   } else {
-    mainloop_pipe(F_{}, I4{});
+    mainloop_pipe(F_{}, IN{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -1391,8 +1380,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // ---- epilogue: the MFMAs took their operands swapped (B first), so each lane holds
   // 4 consecutive n of one m row: float4 stores straight from registers into slab slice
   // s (no LDS staging, no barriers) ----
-  static_assert(1 && WG_MI == 8 && WG_NJ == 2, "tiled slab assumes 2 x 4 waves of 128 x 32");
-  float* out = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096 + lane * 4;
+  static_assert(WG_MI == 8 && WG_NJ == 2, "tiled slab assumes 2 x 4 waves of 128 x 32");
   // buffer stores of this wave's 16 KB of the tile (a wave-uniform base): lane offset + constant per store
   float* out_base = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096;
   const auto out_rs = __builtin_amdgcn_make_buffer_rsrc(out_base, 0, WG_MI * WG_NJ * 1024, 0x00020000);
@@ -1408,6 +1396,18 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
                                                (i * WG_NJ + j) * 1024, 0);
       }
     }
+
+  if (tail) {
+    // the tail columns go to slab tile 6 where a 16-column tile's wn = 0 waves put them
+    // (wave wm, store i * WG_NJ), the layout mlp_sgd_kernel decodes
+    float* t_base = A.slab + (long)s * A.slab_stride + 6L * TL_TILE + wm * 4096;
+    const auto t_rs = __builtin_amdgcn_make_buffer_rsrc(t_base, 0, WG_MI * WG_NJ * 1024, 0x00020000);
+    typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4w, tacc[t]), t_rs, out_voff,
+                                             (2 * wn + t) * WG_NJ * 1024, 0);
+  }
 
   float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
   if (g < G) {
@@ -1739,7 +1739,7 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
 int sl_mlp_wgrad_slices(int batch, int requested) {
   if (batch <= 0 || batch % 64 != 0) return -1;
   const int total = batch / 64;
-  int req = requested > 0 ? requested : 28;  // one GEMM WG per CU (128 KB LDS each)
+  int req = requested > 0 ? requested : 32;  // (6 + 2 tiles) x 32 = 256 workgroups: one per CU (144 KB LDS each)
   if (req > total) req = total;
   const int spp = (total + req - 1) / req;
   return (total + spp - 1) / spp;
@@ -1764,7 +1764,8 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
   if (s_eff <= 0 || s_eff != slices || sl_mlp_wgrad_slices(batch, slices2) != slices2) return -1;
   WgArgs a;
   // dW1, db1 = dH1^T [256 x B] . X (raw u8; normalised in mlp_sgd_kernel)
-  a.p[0] = WgProblem{dh1, x, D_IN, D_IN, (D_IN + 127) / 128, 0, P_W1, P_B1, W3P_DB1};
+  // (6 tiles of 128 columns; the last one also computes the 16 columns 768..783)
+  a.p[0] = WgProblem{dh1, x, D_IN, D_IN, D_IN / 128, 0, P_W1, P_B1, W3P_DB1};
   // dW2, db2 = dH2^T . H1
   a.p[1] = WgProblem{dh2, h1, HID, HID, HID / 128, 0, P_W2, P_B2, W3P_DB2};
   a.total_steps = batch / 64;
