@@ -76,9 +76,6 @@ constexpr int W3P_LD = W3P_DB2 + HID;  // 3088
 __host__ __device__ constexpr long frag_off(int n, int k, int ks_per_row) {
   return ((long)(n >> 4) * ks_per_row + (k >> 5)) * 512 + ((((k & 31) >> 3) << 4) | (n & 15)) * 8 + (k & 7);
 }
-__device__ __forceinline__ short8_t ld_frag(const uint16_t* w, int nt, int ks, int ks_per_row, int lane) {
-  return ld8(w + ((long)nt * ks_per_row + ks) * 512 + lane * 8);
-}
 // Buffer-load form for the fully unrolled k-loops: a 32-bit per-lane voffset
 // plus a constant soffset per (fragment, k-step).  With flat addresses hipcc
 // kept one 64-bit SGPR address per unrolled load and spilled ~200 SGPRs.
@@ -1593,7 +1590,7 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
 
 // float4 units a launch of mlp_sgd_kernel walks: the slab's (tiled) or the parameters'
 __host__ __device__ constexpr long sgd_units(bool slab) {
-  return (1 && slab) ? TL_STRIDE / 4 : (P_N + 3) / 4;
+  return slab ? TL_STRIDE / 4 : (P_N + 3) / 4;
 }
 
 __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
@@ -1671,7 +1668,7 @@ extern "C" {
 long sl_mlp_param_count() { return P_N; }
 
 // floats per slice of the weight-gradient slab (the tiled layout is larger than the parameters)
-long sl_mlp_slab_stride() { return 1 ? TL_STRIDE : (P_N + 3) / 4 * 4; }
+long sl_mlp_slab_stride() { return TL_STRIDE; }
 
 static unsigned long long* g_stamps = nullptr;
 int sl_mlp_set_stamps(unsigned long long* p) {

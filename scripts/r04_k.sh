@@ -10,7 +10,7 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 $O/pytest_mlp.log
 OLD=$GRAFT_REPO_ROOT/serverless_learn_amd/_native/ab/libslkernels_7tile.so
 rm -f gpurun_out/abenv/summary.txt
-bash scripts/ab_env.sh 3 "SL_KERNELS_SO=$OLD" "SL_AB_ARM=tail32" "SL_MLP_WG_S1=31 SL_MLP_WG_S2=35" \
+bash scripts/ab_env.sh 3 "SL_KERNELS_SO=$OLD" "SL_KERNELS_SO=$OLD SL_MLP_WG_S2=30" "SL_AB_ARM=tail32" "SL_MLP_WG_S1=31 SL_MLP_WG_S2=35" \
   -- --steps 200 --warmup 20 --ingest local || exit 1
 cp gpurun_out/abenv/summary.txt $O/abenv_summary.txt
 timeout -k 10 400 python scripts/ab_mlp_inproc.py --split 32:32,31:35,30:38,29:41 --rounds 6 --steps 50 \
