@@ -49,7 +49,7 @@ constexpr int BM = 64;       // batch rows granularity (the rows kernel runs 64 
 constexpr int HS_LD = 264;   // [64][256] bf16 LDS images: 528-B rows
 constexpr int XC_LD = 72;    // X chunk image rows: 64 k + 8 pad = 144 B (ds_read_b128 conflict-free)
 constexpr int DZ_LD = 40;
-constexpr int DZ_LD256 = 16;  // 256-row tile: the 10 (16) real dZ columns only; k 16..31 of the K=32 MFMA are zero registers
+constexpr int DZ_LDW = 16;    // 128-row tile: the 10 (16) real dZ columns only; k 16..31 of the K=32 MFMA are zero registers
 constexpr int KS1 = D_INP / 32, KS2 = HID / 32;  // 32-deep k-steps of layer 1 / of 256-wide layers
 // k-steps layer 1 actually runs: 25 (784 = 24.5 x 32; the 26th step of the padded K is all zeros)
 constexpr int L1_KSTEPS_ROWS = (D_IN + 31) / 32;
@@ -97,7 +97,6 @@ struct MlpRowArgs {
   const int* cursor;
   int n_batches, batch;
   const uint16_t *w1h, *w2h, *w3h, *w2th, *w3th;
-  const uint16_t* w1f;                 // fp16 W1, fragment order (unused by the rows kernel's bf16 layer 1)
   const float *b1, *b2, *b3;
   float xa, xb, grad_scale;
   float dh1_scale;                     // dH1 goes to HBM as fp16 of dH1 * dh1_scale (a power of two)
@@ -238,7 +237,7 @@ __device__ __forceinline__ void copy_part(const uint16_t* src, int ld, uint16_t*
 
 // copy_part through a buffer resource: one per-lane byte offset plus a constant SGPR
 // offset per piece (the flat form kept a 64-bit address per piece live across the
-// k-loop and spilled in the 256-row tile).  dst is the workgroup's first row.
+// k-loop and spilled in the wide tiles).  dst is the workgroup's first row.
 template <int BM, int NT, int NCOLS>
 __device__ __forceinline__ void copy_part_buf(const uint16_t* src, int ld, __amdgpu_buffer_rsrc_t dst, int gld, int tid,
                                               int it) {
@@ -256,42 +255,37 @@ __device__ __forceinline__ void copy_part_buf(const uint16_t* src, int ld, __amd
   }
 }
 
-// Two tile heights.  BM = 64 (the default): 4 waves, wave w owns features 64 w .. 64 w + 63
-// for all 64 rows, two workgroups per CU overlap each other's epilogues.  BM = 256 (opt-in,
-// SL_MLP_ROWS_BM=256; one 8-wave workgroup per CU, 2 x 4 waves of 128 rows x 64 features):
+// Two tile heights, 4 waves each, wave w owns features 64 w .. 64 w + 63 for all rows and two
+// workgroups share a CU, overlapping each other's epilogues.  BM = 128 (the default, "BIG"):
 // every weight fragment a wave streams from L2 feeds 8 MFMAs instead of 4, half the weight
-// stream per CU; it runs one activation image + an H1 nibble mask + a 16-column dZ image
-// (156 KB of LDS), two X row passes per thread, a 2-deep weight ring and no A prefetch
-// (register budget: 128 accumulators of 256); profiles/r03_big.
-// L1 = false (BM = 64 only): H1 was already computed by mlp_fwd1_kernel (mlp_fwd1.hip);
-// the tile is staged from global into R1 and layer 1 / its H1 write are skipped.
-template <int BM> constexpr int rows_nwv() { return BM == 256 ? 8 : 4; }
-template <bool TRAIN, int BM, int WMG, bool L1 = true>
-__global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_rows_kernel(MlpRowArgs a) {
-  constexpr int NWV = rows_nwv<BM>();  // waves per workgroup
-  constexpr int MF = BM / 16 / WMG;    // m-fragments per wave
+// stream per CU of BM = 64; it runs one activation image + an H1 nibble mask + a 16-column dZ
+// image (80 KB of LDS), two X row passes per thread, a 2-deep weight ring and no A prefetch
+// (profiles/r04_rows128).  BM = 64 serves batches that are not a multiple of 128.  (An 8-wave
+// 256-row form, one workgroup per CU, measured 8 % slower and was removed: profiles/r03_big,
+// r04_rows128.)
+template <bool TRAIN, int BM>
+__global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
+  constexpr int NWV = 4;               // waves per workgroup
+  constexpr int MF = BM / 16;          // m-fragments per wave
   constexpr int NT = NWV * 64;         // threads
-  constexpr int NF = 16 * WMG / NWV;   // n-fragments per wave
-  // WIDE: 128 rows x 64 features per wave (the 256-row tile and the 4-wave 128-row tile)
-  constexpr bool BIG = BM >= 128;
-  static_assert(BM == 64 || BM == 128 || BM == 256, "64-, 128- or 256-row tiles");
+  constexpr int NF = 16 / NWV;         // n-fragments per wave
+  // BIG: 128 rows x 64 features per wave
+  constexpr bool BIG = BM == 128;
+  static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
   constexpr bool ONE = BIG;  // one activation image (+ H1 nibble mask)
-  static_assert(!BIG || L1, "the wide tiles have no train == 2 form");
   static_assert(!BIG || (MF == 8 && NF == 4), "wide tiles: 128 x 64 per wave");
   constexpr int RING = BIG ? 2 : 4;  // weight ring depth (k-steps)
   constexpr bool APF = !BIG;         // prefetch the next k-step's A fragments
   constexpr int XQ = 2;              // BIG: X chunks waiting in registers
   constexpr int XP = BM * 4 / NT;                          // X row passes per thread (16 columns each)
-  constexpr int DZL = BIG ? DZ_LD256 : DZ_LD;
+  constexpr int DZL = BIG ? DZ_LDW : DZ_LD;
   constexpr int SPW = BM / 16 / NWV;                       // 16-row softmax blocks per wave
   constexpr int REGB = BM * HS_LD;   // one LDS region (elements)
   static_assert(3 * BM * XC_LD <= REGB, "X ring must fit region 0");
   constexpr int SMEM = ONE ? REGB + BM * DZL + BM * 32 : 2 * REGB + BM * DZL;
-  // BIG: b1 | b2 (| b3: 256-row tile) staged in LDS (fp32, as uint16 pairs); the 128-row tile
-  // reads b3 from global so that two workgroups fit one CU's 160 KB
-  constexpr bool B3LDS = BM == 256;
-  constexpr int BSZ = BIG ? (2 * HID + (B3LDS ? 16 : 0)) * 2 : 0;
-  constexpr bool W3LDS = BIG && BM * DZL >= 16 * HID;  // W3 staged in the dZ image until layer 3 (256-row tile)
+  // BIG: b1 | b2 staged in LDS (fp32, as uint16 pairs); b3 is read from global so that two
+  // workgroups fit one CU's 160 KB
+  constexpr int BSZ = BIG ? 2 * HID * 2 : 0;
   static_assert((SMEM + BSZ) * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM + BSZ];
   float* BS = reinterpret_cast<float*>(smem + SMEM);
@@ -308,9 +302,9 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   const int lr = lane & 15, lg = lane >> 4;
   const int row0 = blockIdx.x * BM;
   const long srow0 = batch_base(a.cursor, a.n_batches, a.batch) + row0;
-  const int wmg = wave / (NWV / WMG), wng = wave % (NWV / WMG);
+  const int wng = wave;
   const int cw = wng * 16 * NF;  // this wave's output columns
-  const int rw = wmg * 16 * MF;  // ... and rows
+  constexpr int rw = 0;          // ... and rows (all of the tile's)
   floatx4_t acc[MF][NF];
   auto stamp = [&](int i) {
     if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
@@ -320,7 +314,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   if (a.stagger > 0 && blockIdx.x >= gridDim.x / 2)
     for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   stamp(0);
-  // Workgroup barrier.  The 256-row tile (one workgroup per CU) waits only for LDS
+  // Workgroup barrier.  The 128-row tile waits only for LDS
   // traffic: __syncthreads() also drains every outstanding global store (vmcnt(0)), and
   // with all CUs storing the same activation at once that drain stalled the CU for
   // up to ~12k cycles per barrier.  No global data is exchanged through a barrier here.
@@ -336,12 +330,6 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   if constexpr (BIG) {  // the epilogues read the biases from LDS (published by layer 1's barriers)
     if (tid < 2 * HID / 4)
       reinterpret_cast<float4*>(BS)[tid] = reinterpret_cast<const float4*>(tid < HID / 4 ? a.b1 : a.b2 - HID)[tid];
-    else if (B3LDS && tid < 2 * HID / 4 + NC)
-      BS[2 * HID + tid - 2 * HID / 4] = a.b3[tid - 2 * HID / 4];
-    if constexpr (W3LDS) {
-      static_assert(NT * 8 == 16 * HID, "W3 staging: one 16-B piece per thread into RZ");
-      reinterpret_cast<uint4*>(RZ)[tid] = reinterpret_cast<const uint4*>(a.w3h)[tid];
-    }
   }
   if (a.stamps && tid == 0) {  // placement: HW_ID (CU / SH / SE) and XCC_ID
     a.stamps[(long)blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -477,14 +465,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   for (int sp = 0; sp < SPW; ++sp)
     lab4[sp] = a.y ? *reinterpret_cast<const uint32_t*>(a.y + srow0 + (sp * NWV + wave) * 16 + 4 * lg) : 0u;
 
-  if constexpr (!L1) {
-#pragma unroll
-    for (int q = tid; q < BM * (HID / 8); q += NT) {
-      const int r = q >> 5, c8 = (q & 31) * 8;
-      *reinterpret_cast<short8_t*>(R1 + r * HS_LD + c8) = ld8(a.h1 + (long)(row0 + r) * HID + c8);
-    }
-    stamp(1);
-  } else {
+  {
   zero_acc();
   constexpr bool XWIDE = APF && !ONE;
   if constexpr (XWIDE) {
@@ -541,10 +522,10 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
     static_assert(BIG, "the 64-row tile runs the 128-column X ring above");
     uint4 xq[XQ][XP];  // X chunks waiting in registers (the u8 input comes from HBM)
     {
-      // 256-row tile: a 4-slot ring of unpadded 64-column bf16 chunks (4 x 32 KB; 16-B
+      // 128-row tile: a 4-slot ring of unpadded 64-column bf16 chunks (4 x 16 KB; 16-B
       // pieces XOR-swizzled by (row / 2) % 8, which keeps the A-fragment ds_read_b128
       // conflict-free without the 144-B padded rows), so the waves meet at one barrier
-      // per two chunks (4 k-steps) instead of one per chunk: with all 8 waves in
+      // per two chunks (4 k-steps) instead of one per chunk: with all the waves in
       // lock-step each barrier exposed the slowest wave's X-load and weight latency
       // (barrier knockout: -14k of 48k layer-1 cycles).  Period k reads chunks 2k, 2k+1
       // and converts chunks 2k+2, 2k+3 (one row pass per k-step, each conversion piece
@@ -652,7 +633,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
       });
     } else {
       k256(f_w2, ha, [&](int st) {
-        if (TRAIN && L1) copy_part<BM, NT, HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid, st);
+        if (TRAIN) copy_part<BM, NT, HID>(R1, HS_LD, a.h1 + (long)row0 * HID, HID, tid, st);
       });
     }
   }
@@ -665,10 +646,7 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
   if constexpr (ONE) bar();  // every wave is done reading H1: H2 replaces it
   stamp(14);
   relu_out(BIG ? BS + HID : a.b2, R0, false);
-  if constexpr (W3LDS) {  // from the copy of W3 staged in the dZ image at the start (no global load)
-#pragma unroll
-    for (int ks = 0; ks < KS2; ++ks) w3f[ks] = lds8(RZ + ks * 512 + lane * 8);
-  } else if constexpr (ONE) {  // after the epilogue: the 32 registers would push past the 168 budget
+  if constexpr (ONE) {  // after the epilogue: the 32 registers would push past the 168 budget
 #pragma unroll
     for (int ks = 0; ks < KS2; ++ks) w3f[ks] = f_w3(0, ks, KS2);
   }
@@ -687,13 +665,12 @@ __global__ __launch_bounds__(rows_nwv<BM>() * 64, BM == 256 ? 1 : 2) void mlp_ro
 #pragma unroll
     for (int sp = 0; sp < SPW; ++sp)
       z3[sp] = mfma16(lds8(R0 + ((sp * NWV + wave) * 16 + lr) * HS_LD + 8 * lg + ks * 32), w3f[ks], z3[sp]);
-  if constexpr (W3LDS) bar();  // every wave holds W3 in registers: dZ may overwrite its staging copy
 #pragma unroll
   for (int sp = 0; sp < SPW; ++sp) {
     const int rb = (sp * NWV + wave) * 16;  // this pass's 16 rows
     const floatx4_t z = z3[sp];
     const int c = lr;
-    const float bias3 = c < NC ? (B3LDS ? BS[2 * HID + c] : a.b3[c]) : 0.f;
+    const float bias3 = c < NC ? a.b3[c] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = rb + 4 * lg + r;
@@ -1459,7 +1436,6 @@ struct SgdArgs {
   float xa, xb;
   int mode;  // 0: refresh bf16 shadows from w; 1: reduce only (grad_out); 2: reduce/read + update
   uint16_t *w1h, *w2h, *w2th, *w3h, *w3th;
-  uint16_t* w1f;  // optional fp16 copy of W1 in the same fragment order (mlp_fwd1.hip's operand)
   int* cursor;
   // xGMI hand-off (mode 1 only): grad_out / grad_out_alt are this rank's exchange slots 0 / 1,
   // picked by the parity of the step in flight (xgmi.h)
@@ -1472,7 +1448,6 @@ __device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) 
   if (p < P_B1) {
     const int o = (int)(p / D_IN), i = (int)(p - (long)o * D_IN);
     a.w1h[frag_off(o, i, KS1)] = h;                     // layer 1: B[k=i][n=o]
-    if (a.w1f) a.w1f[frag_off(o, i, KS1)] = __builtin_bit_cast(uint16_t, (_Float16)w);
   } else if (p >= P_W2 && p < P_B2) {
     const int q = (int)(p - P_W2), o = q >> 8, i = q & 255;
     a.w2h[frag_off(o, i, KS2)] = h;                     // layer 2: B[k=i][n=o]
@@ -1680,7 +1655,7 @@ int sl_mlp_set_stagger(int n) {
   g_stagger = n;
   return 0;
 }
-static int g_rows_bm = 0;  // 0: auto; 64 / 256 force a tile height (benchmarks, tests)
+static int g_rows_bm = 0;  // 0: auto; 64 / 128 force a tile height (benchmarks, tests)
 int sl_mlp_set_rows_bm(int bm) {
   g_rows_bm = bm;
   return 0;
@@ -1690,23 +1665,23 @@ int sl_mlp_set_rows_bm(int bm) {
 // CU: each weight fragment streamed from L2 feeds 8 MFMAs, half the weight stream of the
 // 64-row tile, and the two co-resident workgroups overlap each other's epilogues).  In-process
 // interleaved A/B at B = 65,536 (scripts/ab_mlp_inproc.py, profiles/r04_e): 114.0 us/step vs
-// 122.7 for the 64-row tile and 123.2 for the 8-wave 256-row tile.  64 for batches that are not
-// a multiple of 128; SL_MLP_ROWS_BM=64 / 256 force the others.
+// 122.7 for the 64-row tile and 123.2 for an 8-wave 256-row tile (removed).  64 for batches that
+// are not a multiple of 128; SL_MLP_ROWS_BM=64 forces it.
 int sl_mlp_rows_bm(int batch) {
-  if ((g_rows_bm == 64 || g_rows_bm == 128 || g_rows_bm == 256) && batch % g_rows_bm == 0) return g_rows_bm;
+  if ((g_rows_bm == 64 || g_rows_bm == 128) && batch % g_rows_bm == 0) return g_rows_bm;
   return batch % 128 == 0 ? 128 : 64;
 }
 
 int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_batches, int batch,
                 const uint16_t* w1h, const uint16_t* w2h, const uint16_t* w3h, const uint16_t* w2th,
-                const uint16_t* w3th, const uint16_t* w1f, const float* params, float xa, float xb,
+                const uint16_t* w3th, const float* params, float xa, float xb,
                 float grad_scale, float dh1_scale,
                 uint16_t* h1, float* w3p, uint16_t* dh2, uint16_t* dh1,
                 float* loss, float* correct, float* logits, int train, hipStream_t stream) {
   if (batch <= 0 || batch % BM != 0) return -1;
   MlpRowArgs a;
   a.x = x; a.y = y; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
-  a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th; a.w1f = w1f;
+  a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th;
   a.b1 = params + P_B1; a.b2 = params + P_B2; a.b3 = params + P_B3;
   a.xa = xa; a.xb = xb; a.grad_scale = grad_scale; a.dh1_scale = dh1_scale;
   a.h1 = h1; a.w3p = w3p; a.dh2 = dh2; a.dh1 = dh1;
@@ -1714,18 +1689,13 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.stamps = g_stamps;
   a.stagger = g_stagger;
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
-  // train == 2: H1 already holds relu(Xn W1^T + b1) from sl_mlp_fwd1 (same batch rows)
   const int bm = sl_mlp_rows_bm(batch);
-  if (bm == 128 && train != 2) {
-    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128, 1>), dim3(batch / 128), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128, 1>), dim3(batch / 128), dim3(256), 0, stream, a);
-  } else if (bm == 256 && train != 2) {
-    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 256, 2>), dim3(batch / 256), dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<false, 256, 2>), dim3(batch / 256), dim3(512), 0, stream, a);
+  if (bm == 128) {
+    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 128>), dim3(batch / 128), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 128>), dim3(batch / 128), dim3(256), 0, stream, a);
   } else {
-    if (train == 2) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1, false>), dim3(batch / 64), dim3(256), 0, stream, a);
-    else if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<false, 64, 1>), dim3(batch / 64), dim3(256), 0, stream, a);
+    if (train) hipLaunchKernelGGL((mlp_rows_kernel<true, 64>), dim3(batch / 64), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<false, 64>), dim3(batch / 64), dim3(256), 0, stream, a);
   }
   SL_CHECK_LAUNCH();
   return 0;
@@ -1788,9 +1758,8 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
 int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, int slices2, long slab_stride, const float* grad_in,
                float* grad_out, float lr, float mu, float wd, float xa, float xb, int mode, uint16_t* w1h,
                uint16_t* w2h,
-               uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, uint16_t* w1f, int* cursor, hipStream_t stream) {
+               uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, hipStream_t stream) {
   SgdArgs a = {};
-  a.w1f = w1f;
   a.w = w; a.mom = mom; a.slab = slab; a.slices = slices; a.slices2 = slices2; a.slab_stride = slab_stride;
   a.grad_in = grad_in; a.grad_out = grad_out; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = mode;
   a.xa = xa; a.xb = xb;
@@ -1822,7 +1791,7 @@ int sl_mlp_reduce_xgmi(const float* slab, int slices, int slices2, long slab_str
 }
 
 int sl_mlp_sgd_xgmi(float* w, float* mom, float lr, float mu, float wd, uint16_t* w1h, uint16_t* w2h,
-                    uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, uint16_t* w1f, int* cursor, char* const* bases,
+                    uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, char* const* bases,
                     unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, hipStream_t stream) {
   if (!w || !bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return -1;
   if (slot_bytes < ((P_N + 3) / 4) * 16 || (slot_bytes & 255)) return -1;
@@ -1830,7 +1799,7 @@ int sl_mlp_sgd_xgmi(float* w, float* mom, float lr, float mu, float wd, uint16_t
   if (((uintptr_t)w | (uintptr_t)(mom ? mom : w)) & 15) return -2;
   SgdArgs a = {};
   a.w = w; a.mom = mom; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = 2;
-  a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.w1f = w1f; a.cursor = cursor;
+  a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
   XgArgs x;
   x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world; x.chunk4 = chunk4;
   const long groups = (P_N + 3) / 4;

@@ -5,10 +5,10 @@ Separate bench processes on one box spread by +-2-3 %, more than the effects bei
 measured.  Here one trainer on one batch re-captures its step graph for each arm and the
 arms alternate over R rounds of K timed steps; medians and per-round ratios are printed.
 
-Arms: rows-kernel tile heights ("--bm 64,256"), or layer-1 kernels ("--l1 fwd1,none": the
-256 x 256-tile mlp_fwd1 GEMM vs layer 1 inside the rows kernel).  Kernel libraries cannot be
-loaded side by side in one process: use scripts/ab_env.sh for those.
-Usage: python scripts/ab_mlp_inproc.py [--bm 64,256 | --l1 fwd1,none] [--rounds 8] [--steps 50] [--batch 65536]
+Arms: rows-kernel tile heights ("--bm 64,128"), rows-kernel start staggers ("--stagger 0,3"), or
+weight-gradient split-K slice counts ("--split 32:32,31:35", one trainer per arm).  Kernel libraries
+cannot be loaded side by side in one process: use scripts/ab_env.sh for those.
+Usage: python scripts/ab_mlp_inproc.py [--bm 64,128 | --stagger 0,3 | --split s1:s2,...] [--rounds 8] [--steps 50]
 """
 import argparse
 import json
@@ -24,8 +24,7 @@ from serverless_learn_amd.models.mlp import FusedMLPTrainer
 from serverless_learn_amd.ops import _native
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--bm", default="64,256")
-ap.add_argument("--l1", default=None, help="comma list of layer-1 kernels: fwd1, l1, none")
+ap.add_argument("--bm", default="64,128")
 ap.add_argument("--stagger", default=None, help="comma list of rows-kernel stagger counts (s_sleep(127) rounds)")
 ap.add_argument("--split", default=None,
                 help="comma list of s1:s2 weight-gradient splits (dW1 tiles : dW2 tiles slices), one trainer each")
@@ -35,8 +34,6 @@ ap.add_argument("--batch", type=int, default=65536)
 a = ap.parse_args()
 if a.split:
     arms = a.split.split(",")
-elif a.l1:
-    arms = a.l1.split(",")
 else:
     arms = [int(v) for v in a.stagger.split(",")] if a.stagger else [int(v) for v in a.bm.split(",")]
 B = a.batch
@@ -59,8 +56,6 @@ for r in range(a.rounds):
     for bm in arms:
         if a.split:
             tr = trs[bm]
-        elif a.l1:
-            tr.l1_kernel = None if bm == "none" else bm
         elif a.stagger:
             _native.call("sl_mlp_set_stagger", bm)
         else:

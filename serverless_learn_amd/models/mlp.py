@@ -118,24 +118,18 @@ def reference_grads(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor,
     return losses.detach().sum(), correct.detach(), w.grad.detach()
 
 
-def reference_grads_bf16(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor, grad_scale: float,
-                         l1: str = "bf16"):
+def reference_grads_bf16(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor, grad_scale: float):
     """fp32 math with bf16 rounding at exactly the points the fused kernels round.
 
     A tight check of csrc/kernels/mlp_fused.hip: any indexing/layout bug shows
     up as an O(1) error, while legitimate differences are fp32 summation order.
-    ``l1="fp16"`` rounds layer 1 the way mlp_fwd1.hip does (exact normalised pixels,
-    fp16 W1) instead of bf16 Xn and bf16 W1.  Returns (loss_sum, correct, grad_flat).
+    Returns (loss_sum, correct, grad_flat).
     """
     r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
     v = {k: t.detach().float() for k, t in views(flat).items()}
     a, b = norm_coeffs()
-    if l1 == "fp16":
-        xn = x_u8.reshape(-1, D_IN).float() * a + b
-        w1 = v["fc1.weight"].to(torch.float16).float()
-    else:
-        xn = r(x_u8.reshape(-1, D_IN).float() * a + b)
-        w1 = r(v["fc1.weight"])
+    xn = r(x_u8.reshape(-1, D_IN).float() * a + b)
+    w1 = r(v["fc1.weight"])
     w2, w3 = r(v["fc2.weight"]), r(v["fc3.weight"])
     p1 = xn @ w1.t() + v["fc1.bias"]
     h1 = r(torch.relu(p1))
@@ -274,7 +268,7 @@ class FusedMLPTrainer:
             raise ValueError(f"batch must be a multiple of {BLOCK_ROWS}")
         self._n = _native
         _native.lib()  # fail loudly if the HIP library cannot be loaded
-        if os.environ.get("SL_MLP_ROWS_BM"):  # force the rows kernel's tile height (64 / 128 / 256)
+        if os.environ.get("SL_MLP_ROWS_BM"):  # force the rows kernel's tile height (64 / 128)
             _native.call("sl_mlp_set_rows_bm", int(os.environ["SL_MLP_ROWS_BM"]))
         dev = torch.device(device)
         self.device = dev
@@ -321,14 +315,6 @@ class FusedMLPTrainer:
         self.slab = torch.empty(max(self.slices, self.slices2), self.slab_stride, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
-        # fp16 copy of W1 in the same fragment order, written with the bf16 shadows (k >= 784 stays 0)
-        self.w1f = torch.zeros(HIDDEN, D_IN_PAD, dtype=torch.float16, device=dev)
-        # Layer 1 of the train step: with SL_MLP_FWD1=1 (batch % 256 == 0) its own 256 x 256-tile
-        # GEMM, mlp_fwd1_kernel (csrc/kernels/mlp_fwd1.hip: exact fp16 (1024 + u) pixels, LDS-DMA
-        # ring), after which the rows kernel starts at layer 2 from H1; otherwise layer 1 runs
-        # inside the rows kernel.
-        fwd1 = os.environ.get("SL_MLP_FWD1", "0") == "1" and batch % 256 == 0
-        self.l1_kernel = "fwd1" if fwd1 else None
         self.allreduce = None  # callable(grad_tensor) -> None, sums in place (RCCL)
         self.xgmi = None       # parallel.xgmi.XgmiExchange: all-reduce fused into the update (no RCCL)
         self.x = self.y = None
@@ -338,18 +324,6 @@ class FusedMLPTrainer:
 
     n_params = N_PARAMS
     model_name = "mlp-784-256-256-10"
-
-    @property
-    def l1_gemm(self) -> bool:
-        """Layer 1 runs as its own launch (mlp_fwd1) and the rows kernel starts at H1."""
-        return self.l1_kernel is not None
-
-    @property
-    def l1_numerics(self) -> str:
-        """Where layer 1 rounds: "fp16" (mlp_fwd1: exact pixels, fp16 W1) or "bf16" (the rows
-        kernel's own layer 1: bf16 Xn and W1).  An fp16 layer 1 inside the 128-row tile measured
-        3.5 % slower (the in-loop S sums), profiles/r04_rows128."""
-        return "fp16" if self.l1_kernel == "fwd1" else "bf16"
 
     def layout(self):
         return [[n, list(s), o] for n, s, o, _ in param_layout()]
@@ -376,7 +350,7 @@ class FusedMLPTrainer:
         n = self._n
         n.call("sl_mlp_sgd", n.ptr(self.params), None, None, 0, 0, 0, None, None, 0.0, 0.0, 0.0, self.xa, self.xb, 0,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
-               n.ptr(self.w1f), None, n.stream_ptr())
+               None, n.stream_ptr())
 
     @property
     def dh1_scale(self) -> float:
@@ -390,24 +364,21 @@ class FusedMLPTrainer:
         """Cached launches for the current buffers/hyper-parameters (rebuilt on change)."""
         key = (self.x.data_ptr() if self.x is not None else 0, self.n_batches, self.grad_scale, self.lr,
                self.momentum, self.weight_decay, id(self.xgmi), bool(self.xgmi and self.xgmi.two_shot),
-               self.l1_kernel)
+               )
         if getattr(self, "_lkey", None) == key:
             return self._lc
         n, p = self._n, self._n.ptr
-        ws = (p(self.w1h), p(self.w2h), p(self.w2th), p(self.w3h), p(self.w3th), p(self.w1f))
+        ws = (p(self.w1h), p(self.w2h), p(self.w2th), p(self.w3h), p(self.w3th))
         lc = {
             "rows": n.Launch("sl_mlp_rows", p(self.x), p(self.y), p(self.cursor), self.n_batches, self.batch,
-                             p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th), p(self.w1f),
+                             p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
                              p(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                              p(self.h1t), p(self.w3p), p(self.dh2t), p(self.dh1t),
-                             p(self.loss), p(self.correct), None, 2 if self.l1_gemm else 1),
+                             p(self.loss), p(self.correct), None, 1),
             "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
                               self.slices, self.slices2, self.slab_stride),
         }
-        if self.l1_kernel == "fwd1":
-            lc["l1"] = n.Launch("sl_mlp_fwd1", p(self.x), p(self.cursor), self.n_batches, self.batch, p(self.w1f),
-                                p(self.params[N_PARAMS_B1:]), self.xa, self.xb, p(self.h1t))
         for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
                                                         "reduce": (1, False, True, False),
                                                         "update": (2, True, False, True)}.items():
@@ -428,14 +399,11 @@ class FusedMLPTrainer:
 
     def _rows(self, train: bool = True):
         if train:
-            lc = self._launches()
-            if self.l1_gemm:
-                lc["l1"]()
-            return lc["rows"]()
+            return self._launches()["rows"]()
         n = self._n
         n.call("sl_mlp_rows", n.ptr(self.x), n.ptr(self.y), n.ptr(self.cursor), self.n_batches, self.batch,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.w1f), n.ptr(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
+               n.ptr(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                n.ptr(self.h1t), n.ptr(self.w3p), n.ptr(self.dh2t), n.ptr(self.dh1t),
                n.ptr(self.loss), n.ptr(self.correct), None, 0, n.stream_ptr())
 
@@ -561,7 +529,7 @@ class FusedMLPTrainer:
         corr = torch.zeros(rows, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.w1f), n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
                n.ptr(loss), n.ptr(corr), None, 0, n.stream_ptr())
         return StepStats(float(loss.mean()), float(corr.mean()), rows)
 
@@ -574,7 +542,7 @@ class FusedMLPTrainer:
         out = torch.empty(rows, CLASSES, device=self.device)
         n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
-               n.ptr(self.w1f), n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
+               n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
                None, None, n.ptr(out), 0, n.stream_ptr())
         return out
 

@@ -31,7 +31,7 @@ F = ctypes.c_float
 _SIGS: dict[str, list] = {
     "sl_mlp_param_count": [],
     "sl_mlp_slab_stride": [],
-    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P],
+    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P],
     "sl_mlp_wgrad": [I, P, P, I, P, P, P, P, I, P, I, I, L, P],
     "sl_mlp_wgrad_slices": [I, I],
     "sl_mlp_wgrad_slices2": [I, I, I],
@@ -41,10 +41,9 @@ _SIGS: dict[str, list] = {
     "sl_conv_set_phase": [I],
     "sl_mlp_rows_bm": [I],
     "sl_mlp_set_stamps": [P],
-    "sl_mlp_sgd": [P, P, P, I, I, L, P, P, F, F, F, F, F, I, P, P, P, P, P, P, P, P],
+    "sl_mlp_sgd": [P, P, P, I, I, L, P, P, F, F, F, F, F, I, P, P, P, P, P, P, P],
     "sl_mlp_reduce_xgmi": [P, I, I, L, F, F, P, P, P, P],
-    "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, P, L, I, I, L, P],
-    "sl_mlp_fwd1": [P, P, I, I, P, P, F, F, P, P],
+    "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, L, P],
     "sl_clock_probe": [P, P, I, P],
 }
 _RESTYPE = {"sl_mlp_param_count": ctypes.c_long, "sl_mlp_slab_stride": ctypes.c_long}

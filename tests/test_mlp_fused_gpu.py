@@ -17,7 +17,7 @@ def _rel(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
 
-@pytest.mark.parametrize("bm", [64, 128, 256])
+@pytest.mark.parametrize("bm", [64, 128])
 def test_logits_match_reference(bm, rows_bm):
     rows_bm(bm)
     x, y = _data(256)
@@ -37,9 +37,8 @@ def rows_bm():
     _native.call("sl_mlp_set_rows_bm", 0)
 
 
-@pytest.mark.parametrize("batch,bm,l1", [(64, 64, None), (512, 64, "fwd1"), (2048, 64, "fwd1"), (2048, 64, None),
-                                         (512, 128, None), (2048, 128, None), (512, 256, None), (2048, 256, None)])
-def test_gradients_match_reference(batch, bm, l1, rows_bm):
+@pytest.mark.parametrize("batch,bm", [(64, 64), (512, 64), (2048, 64), (512, 128), (2048, 128), (4096, 128)])
+def test_gradients_match_reference(batch, bm, rows_bm):
     from serverless_learn_amd.ops import _native
 
     rows_bm(bm)
@@ -47,12 +46,11 @@ def test_gradients_match_reference(batch, bm, l1, rows_bm):
     x, y = _data(batch, seed=3)
     flat = M.init_params(2)
     tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
-    tr.l1_kernel = l1  # layer 1 as mlp_fwd1, or inside the rows kernel (None)
     tr.load_shard(x, y)
     g = tr.compute_grads().cpu()
     torch.cuda.synchronize()
     loss, correct, gref = M.reference_grads(flat, x, y, 1.0 / batch)
-    _, _, gemu = M.reference_grads_bf16(flat, x, y, 1.0 / batch, l1=tr.l1_numerics)
+    _, _, gemu = M.reference_grads_bf16(flat, x, y, 1.0 / batch)
     for name, shape, off, n in M.param_layout():
         a, b, e = g[off:off + n], gref[off:off + n], gemu[off:off + n]
         # vs the true fp32 gradient: bf16 operand rounding only
@@ -87,33 +85,6 @@ def test_gradients_with_per_problem_split_k(batch, s1, s2):
         a, b = g[off:off + n], g0[off:off + n]
         # the same products, summed in another order
         assert float((a - b).norm() / b.norm()) < 1e-5, (name, float((a - b).norm() / b.norm()))
-
-
-def test_fwd1_layer1_matches_fp32_reference():
-    """mlp_fwd1_kernel (exact fp16 (1024 + u) pixels against fp16 W1, S-corrected) gives
-    H1 = relu(Xn W1^T + b1) to fp16-weight precision, on a batch whose rows come from the
-    second batch of the shard (device cursor), including the padded K chunk."""
-    batch = 1024
-    x, y = _data(batch * 2, seed=17)
-    flat = M.init_params(8)
-    tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
-    tr.l1_kernel = "fwd1"
-    tr.load_shard(x, y)
-    tr.cursor.fill_(1)
-    tr._launches()["l1"]()
-    torch.cuda.synchronize()
-    h = tr.h1t.float().cpu()
-    v = M.views(flat)
-    a, b = M.norm_coeffs()
-    xn = x[batch:].float() * a + b
-    w16 = v["fc1.weight"].to(torch.float16).float()
-    ref = torch.relu(xn.double() @ w16.double().t() + v["fc1.bias"].double()).float()
-    ref_bf = ref.to(torch.bfloat16).float()
-    # bf16 output rounding (2^-9 relative) plus fp32 accumulation of the 1024-offset products
-    err = (h - ref).abs()
-    assert float(err.max()) < 1e-2 * float(ref.abs().max()), float(err.max())
-    assert float((h - ref_bf).abs().max()) <= 2 * float((ref - ref_bf).abs().max()) + 1e-4
-    assert (h > 0).eq(ref > 1e-3).float().mean() > 0.999
 
 
 def test_sgd_step_matches_reference():
@@ -202,7 +173,7 @@ def test_allreduce_hook_path_matches_single_rank():
     assert torch.allclose(a.get_flat(), b.get_flat(), rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("bm", [64, 128, 256])
+@pytest.mark.parametrize("bm", [64, 128])
 def test_training_is_deterministic_at_full_batch(bm, rows_bm):
     """Two 30-step runs from the same start give bit-identical, finite parameters at the
     bench batch (B = 65,536) for every rows-kernel tile height.  A one-step gradient check
@@ -246,7 +217,7 @@ def test_gradients_match_reference_at_headline_config():
     torch.cuda.synchronize()
     xd, yd, fd = x.cuda(), y.cuda(), flat.cuda()
     loss, correct, gref = M.reference_grads(fd, xd, yd, 1.0 / B)
-    _, _, gemu = M.reference_grads_bf16(fd, xd, yd, 1.0 / B, l1=tr.l1_numerics)
+    _, _, gemu = M.reference_grads_bf16(fd, xd, yd, 1.0 / B)
     gref, gemu = gref.double().cpu(), gemu.double().cpu()
     for name, shape, off, n in M.param_layout():
         a, b, e = g[off:off + n], gref[off:off + n], gemu[off:off + n]
