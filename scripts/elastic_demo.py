@@ -181,6 +181,11 @@ def main(argv=None) -> int:
         summary["phases"]["rejoined"] = {n: worker_state(n)[:2] for n in group}
         summary["resumed_from_checkpoint"] = {n: last(read_events(logs[n]), "checkpoint_loaded") for n in fresh}
         summary["resume_pulled"] = {n: last(read_events(logs[n]), "resume_pulled") for n in fresh}
+        # the fresh workers may have logged the step that met the wait a few ms before the
+        # survivors logged it (each writes its own log after the chunk): give them a moment
+        t_rep = time.time()
+        while replicas_agree(group) is None and time.time() - t_rep < 10.0:
+            time.sleep(0.2)
         summary["replicas_after"] = replicas_agree(group)
         summary["xgmi"] = {n: [(e.get("event"), e.get("epoch")) for e in read_events(logs[n])
                                if e.get("event") in ("xgmi_enabled", "xgmi_closed")] for n in group}

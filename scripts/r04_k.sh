@@ -6,9 +6,9 @@ export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r04_k
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu \
-  > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
-tail -2 $O/pytest_gpu.log
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_mlp_fused_gpu.py \
+  > $O/pytest_mlp.log 2>&1 || { tail -30 $O/pytest_mlp.log; exit 1; }
+tail -1 $O/pytest_mlp.log
 OLD=$GRAFT_REPO_ROOT/serverless_learn_amd/_native/ab/libslkernels_7tile.so
 rm -f gpurun_out/abenv/summary.txt
 bash scripts/ab_env.sh 3 "SL_KERNELS_SO=$OLD" "SL_KERNELS_SO=$OLD SL_MLP_WG_S2=30" "SL_AB_ARM=tail32" "SL_MLP_WG_S1=31 SL_MLP_WG_S2=35" \
@@ -32,4 +32,6 @@ import json
 d = json.load(open('gpurun_out/r04_k/ab_stagger.json'))
 print("stagger", {k: round(v['median_us'], 2) for k, v in d.items() if 'median_us' in v})
 PY
+timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread tests -m gpu \
+  > $O/pytest_gpu.log 2>&1; echo "gpu suite rc=$?"; tail -4 $O/pytest_gpu.log
 echo r04_k done
