@@ -105,7 +105,6 @@ struct MlpRowArgs {
   uint16_t *dh2, *dh1;                 // row-major [batch][256]: dH2 bf16, dH1 fp16 (scaled)
   float *loss, *correct, *logits;
   unsigned long long* stamps;  // diagnostics: per-workgroup phase timestamps (nullptr in production)
-  int stagger;                 // experiment: s_sleep(127) rounds before the second half of the grid starts
 };
 
 // Fully unrolled K loop with a D-deep register ring for the per-wave B operand
@@ -309,10 +308,6 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   auto stamp = [&](int i) {
     if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
   };
-  // Stagger experiment: the grid's second half (the second workgroup of each CU when the first
-  // half fills the chip) starts later, so the two co-resident workgroups are out of phase.
-  if (a.stagger > 0 && blockIdx.x >= gridDim.x / 2)
-    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   stamp(0);
   // Workgroup barrier.  The 128-row tile waits only for LDS
   // traffic: __syncthreads() also drains every outstanding global store (vmcnt(0)), and
@@ -907,13 +902,14 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
 // per 65,536-row step.  The u8 image is read with ds_read_b64_tr_b8 (probed
 // lane map, scripts/probes/tr8_probe.hip: per 16-lane group, lane 2q+p
 // addresses row q bytes 8p..8p+7; lane i receives column i of the 8 rows).
-// dW1 has 784 columns = 6 tiles of 128 + 16: the 6th tile's workgroups also
-// compute the 16 tail columns (their slab tile is the 7th).  dW1's 6 tiles and dW2's 2 tiles may be split into
-// different slice counts (WgProblem::slices; slab regions of slices a problem
-// does not have are never read).
+// dW1 has 784 columns: its 7th tile holds 16 real ones, and the waves past
+// them skip their MFMAs (the tile count per slice stays 9).  Computing the 16
+// columns inside the 6th tile instead (+12.5 % MFMAs there, 256 workgroups of
+// 32 stages) and splitting dW1 / dW2 into different slice counts both measured
+// 0.2-2 % slower (profiles/r04_wgrad).
 //
 // The rows kernel writes per-64-row partial rows: [dW3 | db3] and the column
-// sums of dH1 / dH2 (db1 / db2).  After its main loop each dW1 workgroup sums a
+// sums of dH1 / dH2 (db1 / db2).  After its main loop each workgroup sums a
 // band of those columns over its slice's stages into the slice's slab, so the
 // slab carries every gradient and mlp_sgd_kernel needs no special case.
 // ---------------------------------------------------------------------------
@@ -923,7 +919,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
 // partial-row sums in their own layout [dW3 | db3 | pad | db1 | db2].  The row-major form wrote
 // 16 rows x 64 B per store instruction; that tail took ~16 us (knockout, profiles/r03_wgrad).
 constexpr long TL_TILE = 256L * 128;            // floats per 256 x 128 tile
-constexpr long TL_W2 = 7L * TL_TILE;            // dW2 tiles (dW1: tiles 0..6; tile 6 = the 16 tail columns, written by tile 5's workgroups)
+constexpr long TL_W2 = 7L * TL_TILE;            // dW2 tiles (dW1: tiles 0..6, tile 6 = 16 real columns)
 constexpr long TL_SMALL = 9L * TL_TILE;         // [dW3 | db3 | pad | db1 | db2]
 constexpr long TL_STRIDE = (TL_SMALL + W3P_LD + 63) / 64 * 64;
 
@@ -934,15 +930,11 @@ struct WgProblem {
   int n_real, tiles_n, tile_base;
   long w_off, b_off;  // flat destinations of dW ([256][n_real]) and db
   int bias_part;      // this problem's db partial inside the rows kernel's partial rows
-  // Split-K per problem: a dW2 stage moves 48 KB into LDS, a dW1 stage 40 KB (u8 X), so the
-  // two problems may cut the batch into different slice counts.  The problem's workgroups are
-  // logical ids [wg_base, wg_base + slices * tiles_n), slice-major (a slice's tiles are
-  // consecutive: the same XCD, sharing the A rows in its L2).
-  int slices, steps_per_slice, wg_base;
 };
 struct WgArgs {
   WgProblem p[2];  // dW1 (u8 X), dW2 (H1); dW3 comes from the rows kernel's partials
-  int total_steps;  // 64-row stages
+  int total_tiles;
+  int steps_per_slice, total_steps;  // 64-row stages
   float* slab;
   long slab_stride;
   const int* cursor;  // X is the resident shard: rows start at batch_base(cursor)
@@ -955,8 +947,6 @@ constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages
 constexpr int WG_IMG = 64 * 128;          // one [64 k][128] bf16 image, unpadded (swizzled)
 constexpr int WG_SLOT = 3 * WG_IMG;       // A half 0, A half 1, B = 48 KB
 constexpr int WG_LDS = WG_NSLOT * WG_SLOT;
-// u8 slots use 8 KB of the 16 KB B image; the dW1 tail columns (768..783) go in the rest
-constexpr int WG_TAIL = 8192;  // bytes from the B image
 
 // 16-B chunk position inside a 256-B image row.  XOR on chunk-pair bits with
 // f(r) = (r & 3) | ((r >> 3) & 1) << 2 makes every ds_read_b64_tr_b16 of the
@@ -1056,45 +1046,41 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int wm = wave & 1, wn = wave >> 1;
   const int lr = lane & 15, lg = lane >> 4;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int pi = logical >= A.p[1].wg_base ? 1 : 0;
+  const int s = logical / A.total_tiles;
+  const int t = logical - s * A.total_tiles;
+  const int pi = t >= A.p[1].tile_base ? 1 : 0;
   const WgProblem& P = A.p[pi];
-  const int s = (logical - P.wg_base) / P.tiles_n;
-  const int tn = logical - P.wg_base - s * P.tiles_n;
+  const int tn = t - P.tile_base;
   const int n0 = tn * 128;
-  const int st0 = s * P.steps_per_slice;
-  const int nst = min(P.steps_per_slice, A.total_steps - st0);
+  const int st0 = s * A.steps_per_slice;
+  const int nst = min(A.steps_per_slice, A.total_steps - st0);
   const bool u8b = pi == 0;
-  // dW1's last tile (columns 640..767) also computes the 16 columns 768..783 ("tail"): each
-  // wave takes them for two of its eight m-fragments (m-fragments 2 wn, 2 wn + 1), +12.5 % MFMAs,
-  // instead of a tile of its own that streamed all of dH1 for 16 columns (28 of 252 workgroups).
-  const bool tail = u8b && tn == P.tiles_n - 1;
+  // n-blocks of this wave that hold real columns (dW1's last tile: 16 columns)
+  const int nvalid = __builtin_amdgcn_readfirstlane(min(WG_NJ, max(0, (P.n_real - n0 - wn * 16 * WG_NJ + 15) / 16)));
 
   // LDS-DMA map: bf16 [64][128] images -- wave w, piece j (0..1) covers rows 4 (2w + j) .. +3,
   // lane -> row 4 (2w + j) + lane / 16, LDS chunk lane % 16 <- global chunk swz(lane % 16, row);
   // A is two such images (m 0..127, 128..255).  u8 image: wave w covers rows 8w .. 8w+7,
-  // lane -> row + lane / 8, LDS chunk lane % 8 <- global chunk swz8(lane % 8, row).  The tail
-  // image sits in the u8 slot's free second 8 KB: wave w's 1 KB holds 8 copies of rows
-  // 8w .. 8w+7 x 16 B (lane -> row 8w + lane % 8), so a tr read group can take its own copy.
-  // (wave-uniform 64-bit bases + 32-bit per-lane byte offsets: four fewer VGPRs than per-lane pointers)
+  // lane -> row + lane / 8, LDS chunk lane % 8 <- global chunk swz8(lane % 8, row).
   const int prow = lane >> 4;
+  const uint16_t* asrc[2];
+  const uint16_t* bsrc[2];
   const long xrow0 = batch_base(A.cursor, A.n_batches, A.batch);
-  const char* abase = static_cast<const char*>(P.a) + (long)st0 * 64 * HID * 2;
-  const char* bbase = static_cast<const char*>(P.b) + (u8b ? (xrow0 + st0 * 64) * P.ldb : (long)st0 * 64 * P.ldb * 2);
-  uint32_t aoff[2], boff[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int row = 4 * (2 * wave + j) + prow;
     const int c = wg_swz(lane & 15, row);
-    aoff[j] = (uint32_t)((row * HID + c * 8) * 2);
-    boff[j] = (uint32_t)((row * P.ldb + n0 + c * 8) * 2);
+    asrc[j] = static_cast<const uint16_t*>(P.a) + (long)(st0 * 64 + row) * HID + c * 8;
+    bsrc[j] = static_cast<const uint16_t*>(P.b) + (long)(st0 * 64 + row) * P.ldb + n0 + c * 8;
   }
-  uint32_t boff8, toff8;
+  const uint8_t* bsrc8;
   {
     const int row = 8 * wave + (lane >> 3);
-    boff8 = (uint32_t)(row * P.ldb + n0 + wg_swz8(lane & 7, row) * 16);
-    toff8 = (uint32_t)((8 * wave + (lane & 7)) * P.ldb + (D_IN - 16));
+    const int c = wg_swz8(lane & 7, row);
+    const int col = min(n0 + c * 16, P.ldb - 16);  // columns >= 784 are don't-care columns of dW1
+    bsrc8 = static_cast<const uint8_t*>(P.b) + (xrow0 + st0 * 64 + row) * P.ldb + col;
   }
-  auto issue = [&](int st, auto u8_c, auto tail_c) {  // stage st (relative to the slice) -> ring slot st % NS
+  auto issue = [&](int st, auto u8_c) {  // stage st (relative to the slice) -> ring slot st % NS
     constexpr bool U8 = decltype(u8_c)::value;
     uint16_t* Ai = smem + (st % WG_NSLOT) * WG_SLOT;
     uint16_t* Bi = Ai + 2 * WG_IMG;
@@ -1103,29 +1089,24 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(abase + aoff[j] + (st * 64 * HID + h * 128) * 2),
+            (const __attribute__((address_space(1))) void*)(asrc[j] + (long)st * 64 * HID + h * 128),
             (SL_LDS void*)(Ai + h * WG_IMG + 4 * (2 * wave + j) * 128), 16, 0, 0);
     if constexpr (U8) {
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bbase + boff8 + st * 64 * P.ldb),
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc8 + (long)st * 64 * P.ldb),
                                        (SL_LDS void*)(reinterpret_cast<uint8_t*>(Bi) + 8 * wave * 128), 16, 0, 0);
-      if constexpr (decltype(tail_c)::value)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bbase + toff8 + st * 64 * P.ldb),
-                                         (SL_LDS void*)(reinterpret_cast<uint8_t*>(Bi) + WG_TAIL + wave * 1024), 16, 0, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bbase + boff[j] + st * 64 * P.ldb * 2),
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[j] + (long)st * 64 * P.ldb),
                                          (SL_LDS void*)(Bi + 4 * (2 * wave + j) * 128), 16, 0, 0);
     }
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if (tail) {
-    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, T_{}, T_{});
-  } else if (u8b) {
-    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, T_{}, F_{});
+  if (u8b) {
+    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, T_{});
   } else {
-    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, F_{}, F_{});
+    for (int st = 0; st < WG_NSLOT - 1 && st < nst; ++st) issue(st, F_{});
   }
 
   floatx4_t acc[WG_MI][WG_NJ];
@@ -1133,7 +1114,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   for (int i = 0; i < WG_MI; ++i)
 #pragma unroll
     for (int j = 0; j < WG_NJ; ++j) acc[i][j] = zero4();
-  floatx4_t tacc[2] = {zero4(), zero4()};  // tail columns of m-fragments 2 wn, 2 wn + 1
 
   // per-lane tr-read byte addresses within a slot; k-step 1 is a constant offset
   const uint32_t lds_base = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
@@ -1148,11 +1128,8 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     const int c = wn * 16 * WG_NJ + j * 16;
     b_addr[j] = 2 * WG_IMG * 2 + (u8b ? wg_tr8_addr(c, lane) : wg_tr_addr(c, lane));
   }
-  // tail tr_b8 read: 16-lane group g takes rows 8g .. 8g+7 (wave block g, copy g: distinct banks),
-  // lane 2q + p row 8g + q bytes 8p..; k-step 1 (rows 32..63) is +4 KB
-  const uint32_t t_addr = 2 * WG_IMG * 2 + WG_TAIL + (lane >> 4) * (1024 + 128) + ((lane & 15) >> 1) * 16 + 8 * (lane & 1);
 
-  // Instantiated per (u8, tail wave) and selected by a scalar branch OUTSIDE the loop
+  // Instantiated per (u8, live n-blocks) and selected by a scalar branch OUTSIDE the loop
   // (conditions inside made hipcc copy every accumulator AGPR<->VGPR).
   // Software-pipelined: the fragment reads of stage st+1 are issued right
   // after the barrier that publishes it and run under stage st's MFMAs (two
@@ -1161,44 +1138,36 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // per stage back to back (knockout "reads + MFMAs only": 45.7 us).
   // The slot of stage st is refilled (stage st+3) after the barrier of step st,
   // when every wave has waited for its own reads of stage st.
-  auto mainloop_pipe = [&](auto u8_c, auto tl_c) {
+  auto mainloop_pipe = [&](auto u8_c, auto nb_c) {
     constexpr bool U8 = decltype(u8_c)::value;
-    constexpr int TL = decltype(tl_c)::value;  // this wave's wn in the tail tile, else -1
-    constexpr bool TAIL = TL >= 0;
-    using TailC = std::integral_constant<bool, TAIL>;
-    constexpr int PPS = U8 ? (TAIL ? 6 : 5) : 6;
+    constexpr int NB = decltype(nb_c)::value;
+    constexpr int NBR = NB > 0 ? NB : 1;
+    constexpr int PPS = U8 ? 5 : 6;
     constexpr int KB = U8 ? 4096 : 8192;
     constexpr int NS = WG_NSLOT, SLOT = WG_SLOT;  // ring depth / slot stride (uint16)
     short8_t fa[2][2][WG_MI]; // [set][k-step][m-block]
-    short8_t fb[2][2][WG_NJ]; // bf16 B fragments
-    uint2v_t fr[2][2][WG_NJ]; // raw u8 B fragments (converted next to their MFMAs)
-    short8_t fc[2][2][WG_NJ]; // converted u8 B fragments (1 schedule)
-    // raw tail fragments: one set, read for the next stage after this stage's tail MFMAs took theirs
-    uint2v_t ft[2];
-    auto read_tail = [&](uint32_t sb) {
-      if constexpr (TAIL) {
-        ft[0] = ds_tr8_off<0>(sb + t_addr);
-        ft[1] = ds_tr8_off<4096>(sb + t_addr);
-      }
-    };
+    short8_t fb[2][2][NBR];   // bf16 B fragments
+    uint2v_t fr[2][2][NBR];   // raw u8 B fragments (converted next to their MFMAs)
+    short8_t fc[2][2][NBR];   // converted u8 B fragments (1 schedule)
     auto read_stage = [&](int st, auto set_c) {
       constexpr int S = decltype(set_c)::value;
-      const uint32_t sb = lds_base + (uint32_t)((st % NS) * SLOT * 2);
+      if constexpr (NB > 0) {
+        const uint32_t sb = lds_base + (uint32_t)((st % NS) * SLOT * 2);
 #pragma unroll
-      for (int i = 0; i < WG_MI; ++i) fa[S][0][i] = wg_tr8<0>(sb + a_addr[i]);
+        for (int i = 0; i < WG_MI; ++i) fa[S][0][i] = wg_tr8<0>(sb + a_addr[i]);
 #pragma unroll
-      for (int j = 0; j < WG_NJ; ++j) {
-        if constexpr (U8) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
-        else fb[S][0][j] = wg_tr8<0>(sb + b_addr[j]);
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (U8) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
+          else fb[S][0][j] = wg_tr8<0>(sb + b_addr[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < WG_MI; ++i) fa[S][1][i] = wg_tr8<8192>(sb + a_addr[i]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (U8) fr[S][1][j] = ds_tr8_off<KB>(sb + b_addr[j]);
+          else fb[S][1][j] = wg_tr8<KB>(sb + b_addr[j]);
+        }
       }
-#pragma unroll
-      for (int i = 0; i < WG_MI; ++i) fa[S][1][i] = wg_tr8<8192>(sb + a_addr[i]);
-#pragma unroll
-      for (int j = 0; j < WG_NJ; ++j) {
-        if constexpr (U8) fr[S][1][j] = ds_tr8_off<KB>(sb + b_addr[j]);
-        else fb[S][1][j] = wg_tr8<KB>(sb + b_addr[j]);
-      }
-      read_tail(sb);
     };
     // one fragment of the next stage (f: A k0 i0..MI-1, B k0, A k1, B k1), for the interleave
     auto read_frag = [&](uint32_t sb, int f, auto set_c) {
@@ -1207,7 +1176,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       if (w < WG_MI) {
         if (k == 0) fa[S][0][w] = wg_tr8<0>(sb + a_addr[w]);
         else fa[S][1][w] = wg_tr8<8192>(sb + a_addr[w]);
-      } else {
+      } else if (w - WG_MI < NB) {
         const int j = w - WG_MI;
         if constexpr (U8) {
           if (k == 0) fr[S][0][j] = ds_tr8_off<0>(sb + b_addr[j]);
@@ -1227,18 +1196,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    // the tail's 2 MFMAs per k-step (current set)
-    auto tail_mfmas = [&](auto cur_c) {
-      constexpr int C = decltype(cur_c)::value;
-      if constexpr (TAIL) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const short8_t bt = u8x8_f16_biased(ft[k]);
-          tacc[0] = wg_mma<true>(bt, fa[C][k][2 * TL], tacc[0]);
-          tacc[1] = wg_mma<true>(bt, fa[C][k][2 * TL + 1], tacc[1]);
-        }
-      }
-    };
     // The next stage's fragment reads are interleaved one per ~two MFMAs: issued
     // as one burst after the barrier, the 8 waves' reads queued behind each other
     // and the MFMAs waited for the queue (reads and MFMAs did not overlap).  The
@@ -1248,13 +1205,11 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       if (st + 1 < nst) {
         wg_vmcnt<PPS>(min(NS - 2, nst - 2 - st));  // stage st+1 has landed (st+2 .. st+NS-1 may be in flight)
         __builtin_amdgcn_s_barrier();          // ... for everyone; every wave is done reading stage st
-        if (st + NS < nst) issue(st + NS, u8_c, TailC{});  // into stage st's slot
+        if (st + NS < nst) issue(st + NS, u8_c);  // into stage st's slot
       }
-      // the tail MFMAs first: the next stage's fragments (set N) are not live yet
-      tail_mfmas(cur_c);
       const uint32_t sbn = lds_base + (uint32_t)((min(st + 1, nst - 1) % NS) * SLOT * 2);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (U8) {
+      if constexpr (U8 && NB > 0) {
         // u8 -> bf16 conversions off the MFMA critical path: k-step 1's fragments
         // (landed at the end of the previous step) are converted under k-step 0's
         // MFMAs, the next stage's k-step-0 fragments under k-step 1's second half.
@@ -1265,8 +1220,8 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int j = q / WG_MI, i = q % WG_MI;
-            acc[i][j] = wg_mma<U8>(fc[C][k][j], fa[C][k][i], acc[i][j]);
-            if (k == 0 && q % WG_MI == 1) {
+            if (j < NB) acc[i][j] = wg_mma<U8>(fc[C][k][j], fa[C][k][i], acc[i][j]);
+            if (k == 0 && q % WG_MI == 1 && j < NB) {
               fc[C][1][j] = u8x8_f16_biased(fr[C][1][j]);
               asm volatile("" : "+v"(fc[C][1][j]));
             }
@@ -1276,7 +1231,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
               asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * (8 * WG_NF / 16)) : "memory");
               __builtin_amdgcn_sched_barrier(0);
             }
-            if (k == 1 && q >= 8 && (q & 1) == 0 && ((q - 8) >> 1) < WG_NJ) {
+            if (k == 1 && q >= 8 && (q & 1) == 0 && ((q - 8) >> 1) < NB) {
               short8_t& d = fc[N][0][(q - 8) >> 1];
               d = u8x8_f16_biased(fr[N][0][(q - 8) >> 1]);
               asm volatile("" : "+v"(d));  // keep it here (LLVM sinks it past the back edge otherwise)
@@ -1284,18 +1239,24 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
             reads_after(sbn, k, q, nxt_c);
           }
         }
-      } else {
+      } else
+      if constexpr (NB > 0) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
+          short8_t b[NBR];
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            if constexpr (U8) b[j] = u8x8_f16_biased(fr[C][k][j]);
+            else b[j] = fb[C][k][j];
+          }
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int i = q / WG_NJ, j = q % WG_NJ;
-            acc[i][j] = wg_mma<U8>(fb[C][k][j], fa[C][k][i], acc[i][j]);
+            if (j < NB) acc[i][j] = wg_mma<U8>(b[j], fa[C][k][i], acc[i][j]);
             reads_after(sbn, k, q, nxt_c);
           }
         }
       }
-      read_tail(sbn);
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -1304,35 +1265,33 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     using S1 = std::integral_constant<int, 1>;
     wg_vmcnt<PPS>(min(NS - 2, nst - 1));  // stage 0 has landed (stages 1 .. NS-2 may be in flight)
     __builtin_amdgcn_s_barrier();
-    if (NS - 1 < nst) issue(NS - 1, u8_c, TailC{});  // the last slot: free once the prologue sums are done
+    if (NS - 1 < nst) issue(NS - 1, u8_c);  // the last slot: free once the prologue sums are done
     read_stage(0, S0{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (U8) {
 #pragma unroll
-      for (int j = 0; j < WG_NJ; ++j) fc[0][0][j] = u8x8_f16_biased(fr[0][0][j]);
+      for (int j = 0; j < NB; ++j) fc[0][0][j] = u8x8_f16_biased(fr[0][0][j]);
     }
     for (int st = 0; st < nst; st += 2) {
       step(st, S0{}, S1{});
       if (st + 1 < nst) step(st + 1, S1{}, S0{});
     }
   };
-  using IN = std::integral_constant<int, -1>;
-  if (tail) {
-    if (wn == 0) mainloop_pipe(T_{}, std::integral_constant<int, 0>{});
-    else if (wn == 1) mainloop_pipe(T_{}, std::integral_constant<int, 1>{});
-    else if (wn == 2) mainloop_pipe(T_{}, std::integral_constant<int, 2>{});
-    else mainloop_pipe(T_{}, std::integral_constant<int, 3>{});
-  } else if (u8b) {
-    mainloop_pipe(T_{}, IN{});
+  using I4 = std::integral_constant<int, WG_NJ>;  // all n-blocks live
+  using I1 = std::integral_constant<int, 1>;
+  using I0 = std::integral_constant<int, 0>;
+  if (u8b) {
+    if (nvalid >= WG_NJ) mainloop_pipe(T_{}, I4{});
+    else if (nvalid >= 1) mainloop_pipe(T_{}, I1{});
+    else mainloop_pipe(T_{}, I0{});
   } else {
-    mainloop_pipe(F_{}, IN{});
+    mainloop_pipe(F_{}, I4{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
-  // 64 rows), by the dW1 workgroups only (their slices own the slab's partial-row region):
-  // dW1 tile tn of the slice takes a band of float4 columns, G row groups per column,
+  // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
   // a fixed-order sum through LDS (deterministic).  Done HERE, around the slab stores: the
   // loads are issued first (every row of the band at once, clamped indices so no branch
   // splits them), the accumulator stores go out while they are in flight, and the sum
@@ -1340,11 +1299,11 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // main loop; the store tail is issue-bound (~16 us, profiles/r03_wgrad) and hides it. ----
   constexpr int NC4 = W3P_LD / 4;
   constexpr int PR_MAX = 12;  // partial rows per thread held in registers (else a plain loop)
-  const int per = (NC4 + A.p[0].tiles_n - 1) / A.p[0].tiles_n;
-  const int c0 = tn * per, nc = pi == 0 ? min(NC4, c0 + per) - c0 : 1;
-  const int G = pi == 0 ? WG_NT / nc : 0, col = tid % nc, g = tid / nc;
+  const int per = (NC4 + A.total_tiles - 1) / A.total_tiles;
+  const int c0 = t * per, nc = min(NC4, c0 + per) - c0;
+  const int G = WG_NT / nc, col = tid % nc, g = tid / nc;
   const float4* psrc = reinterpret_cast<const float4*>(A.w3p + (long)st0 * W3P_LD) + c0 + col;
-  const bool pr_regs = G > 0 && (nst + G - 1) / G <= PR_MAX;
+  const bool pr_regs = (nst + G - 1) / G <= PR_MAX;
   float4 pv[PR_MAX];
   if (g < G && pr_regs) {
 #pragma unroll
@@ -1355,6 +1314,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   // 4 consecutive n of one m row: float4 stores straight from registers into slab slice
   // s (no LDS staging, no barriers) ----
   static_assert(WG_MI == 8 && WG_NJ == 2, "tiled slab assumes 2 x 4 waves of 128 x 32");
+  float* out = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096 + lane * 4;
   // buffer stores of this wave's 16 KB of the tile (a wave-uniform base): lane offset + constant per store
   float* out_base = A.slab + (long)s * A.slab_stride + (pi ? TL_W2 : 0) + (long)tn * TL_TILE + wave * 4096;
   const auto out_rs = __builtin_amdgcn_make_buffer_rsrc(out_base, 0, WG_MI * WG_NJ * 1024, 0x00020000);
@@ -1370,18 +1330,6 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
                                                (i * WG_NJ + j) * 1024, 0);
       }
     }
-
-  if (tail) {
-    // the tail columns go to slab tile 6 where a 16-column tile's wn = 0 waves put them
-    // (wave wm, store i * WG_NJ), the layout mlp_sgd_kernel decodes
-    float* t_base = A.slab + (long)s * A.slab_stride + 6L * TL_TILE + wm * 4096;
-    const auto t_rs = __builtin_amdgcn_make_buffer_rsrc(t_base, 0, WG_MI * WG_NJ * 1024, 0x00020000);
-    typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4w, tacc[t]), t_rs, out_voff,
-                                             (2 * wn + t) * WG_NJ * 1024, 0);
-  }
 
   float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
   if (g < G) {
@@ -1402,7 +1350,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __syncthreads();  // every wave is done with the ring
   if (g < G) red[g * nc + col] = sum;
   __syncthreads();
-  if (g == 0 && G > 0) {
+  if (g == 0) {
     float4 tot = red[col];
     for (int i = 1; i < G; ++i) {
       const float4 v = red[i * nc + col];
@@ -1425,7 +1373,7 @@ struct SgdArgs {
   float* w;
   float* mom;
   const float* slab;
-  int slices, slices2;   // slab slices of the dW1 tiles + partial-row region / of the dW2 tiles
+  int slices;
   long slab_stride;
   const float* grad_in;  // used when slab == nullptr
   float* grad_out;       // reduced gradient written here (all-reduce hand-off)
@@ -1532,7 +1480,7 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
   float db = 0.f;
   const float* src = a.slab + off;
   const float* dbs = a.slab + TL_SMALL + W3P_DB1 + (w1row >= 0 ? w1row : 0);
-  const int ns = off >= TL_W2 && off < TL_SMALL ? a.slices2 : a.slices;
+  const int ns = a.slices;
   constexpr int U = 8;
   for (int s0 = part; s0 < ns; s0 += SGD_TPG * U) {
     float4 v[U];
@@ -1650,11 +1598,6 @@ int sl_mlp_set_stamps(unsigned long long* p) {
   g_stamps = p;
   return 0;
 }
-static int g_stagger = 0;
-int sl_mlp_set_stagger(int n) {
-  g_stagger = n;
-  return 0;
-}
 static int g_rows_bm = 0;  // 0: auto; 64 / 128 force a tile height (benchmarks, tests)
 int sl_mlp_set_rows_bm(int bm) {
   g_rows_bm = bm;
@@ -1687,7 +1630,6 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.h1 = h1; a.w3p = w3p; a.dh2 = dh2; a.dh1 = dh1;
   a.loss = loss; a.correct = correct; a.logits = logits;
   a.stamps = g_stamps;
-  a.stagger = g_stagger;
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
   const int bm = sl_mlp_rows_bm(batch);
   if (bm == 128) {
@@ -1706,61 +1648,49 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
 int sl_mlp_wgrad_slices(int batch, int requested) {
   if (batch <= 0 || batch % 64 != 0) return -1;
   const int total = batch / 64;
-  int req = requested > 0 ? requested : 32;  // (6 + 2 tiles) x 32 = 256 workgroups: one per CU (144 KB LDS each)
+  int req = requested > 0 ? requested : 28;  // one GEMM WG per CU (128 KB LDS each)
   if (req > total) req = total;
   const int spp = (total + req - 1) / req;
   return (total + spp - 1) / spp;
-}
-
-// Slices of the dW2 tiles for dW1 slices `slices` (requested <= 0: the default split).  A dW2
-// stage moves 48 KB into LDS against 40 KB for dW1, so a finer dW2 split balances the two
-// problems' workgroups; 7 s1 + 2 s2 <= 256 keeps the grid within one workgroup per CU.
-int sl_mlp_wgrad_slices2(int batch, int slices, int requested) {
-  if (sl_mlp_wgrad_slices(batch, slices) != slices) return -1;
-  return sl_mlp_wgrad_slices(batch, requested > 0 ? requested : slices);
 }
 
 // x: the resident u8 shard [n_batches * batch][784]; the batch rows are the
 // ones the rows kernel used (cursor not yet bumped: mlp_sgd_kernel bumps it).
 int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, const uint16_t* h1,
                  const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
-                 int slices2, long slab_stride, hipStream_t stream) {
+                 long slab_stride, hipStream_t stream) {
   if (!w3p || n_w3p != batch / 64) return -1;
   if (slab_stride < TL_STRIDE) return -1;
   const int s_eff = sl_mlp_wgrad_slices(batch, slices);
-  if (s_eff <= 0 || s_eff != slices || sl_mlp_wgrad_slices(batch, slices2) != slices2) return -1;
+  if (s_eff <= 0 || s_eff != slices) return -1;
   WgArgs a;
   // dW1, db1 = dH1^T [256 x B] . X (raw u8; normalised in mlp_sgd_kernel)
-  // (6 tiles of 128 columns; the last one also computes the 16 columns 768..783)
-  a.p[0] = WgProblem{dh1, x, D_IN, D_IN, D_IN / 128, 0, P_W1, P_B1, W3P_DB1};
+  a.p[0] = WgProblem{dh1, x, D_IN, D_IN, (D_IN + 127) / 128, 0, P_W1, P_B1, W3P_DB1};
   // dW2, db2 = dH2^T . H1
   a.p[1] = WgProblem{dh2, h1, HID, HID, HID / 128, 0, P_W2, P_B2, W3P_DB2};
-  a.total_steps = batch / 64;
-  int base = 0, wgs = 0;
+  int base = 0;
   for (int i = 0; i < 2; ++i) {
-    WgProblem& q = a.p[i];
-    q.tile_base = base;
-    q.slices = i ? slices2 : slices;
-    q.steps_per_slice = (a.total_steps + q.slices - 1) / q.slices;
-    q.wg_base = wgs;
-    base += q.tiles_n;
-    wgs += q.tiles_n * q.slices;
+    a.p[i].tile_base = base;
+    base += a.p[i].tiles_n;
   }
+  a.total_tiles = base;
+  a.total_steps = batch / 64;
+  a.steps_per_slice = (a.total_steps + slices - 1) / slices;
   a.slab = slab; a.slab_stride = slab_stride;
   a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
   a.w3p = w3p; a.n_w3p = n_w3p;
   if (((uintptr_t)x & 15) != 0 || ((uintptr_t)w3p & 15) != 0) return -2;  // 16-B pieces / float4 reads
-  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(wgs), dim3(WG_NT), 0, stream, a);
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(WG_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
 
-int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, int slices2, long slab_stride, const float* grad_in,
+int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_stride, const float* grad_in,
                float* grad_out, float lr, float mu, float wd, float xa, float xb, int mode, uint16_t* w1h,
                uint16_t* w2h,
                uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, hipStream_t stream) {
   SgdArgs a = {};
-  a.w = w; a.mom = mom; a.slab = slab; a.slices = slices; a.slices2 = slices2; a.slab_stride = slab_stride;
+  a.w = w; a.mom = mom; a.slab = slab; a.slices = slices; a.slab_stride = slab_stride;
   a.grad_in = grad_in; a.grad_out = grad_out; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = mode;
   a.xa = xa; a.xb = xb;
   a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
@@ -1776,12 +1706,11 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, int slices2,
 }
 
 // Slab reduction straight into this rank's xGMI exchange slot for the step in flight.
-int sl_mlp_reduce_xgmi(const float* slab, int slices, int slices2, long slab_stride, float xa, float xb, float* slot0,
+int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa, float xb, float* slot0,
                        float* slot1, const unsigned* ctl, hipStream_t stream) {
   if (!slab || !slot0 || !slot1 || !ctl || (slab_stride & 3)) return -1;
   SgdArgs a = {};
-  a.slab = slab; a.slices = slices; a.slices2 = slices2; a.slab_stride = slab_stride; a.grad_out = slot0;
-  a.grad_out_alt = slot1;
+  a.slab = slab; a.slices = slices; a.slab_stride = slab_stride; a.grad_out = slot0; a.grad_out_alt = slot1;
   a.ar_ctl = ctl; a.n = P_N; a.xa = xa; a.xb = xb; a.mode = 1;
   if (slab_stride < TL_STRIDE) return -1;
   const long groups = sgd_units(true);

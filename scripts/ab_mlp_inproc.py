@@ -5,10 +5,10 @@ Separate bench processes on one box spread by +-2-3 %, more than the effects bei
 measured.  Here one trainer on one batch re-captures its step graph for each arm and the
 arms alternate over R rounds of K timed steps; medians and per-round ratios are printed.
 
-Arms: rows-kernel tile heights ("--bm 64,128"), rows-kernel start staggers ("--stagger 0,3"), or
-weight-gradient split-K slice counts ("--split 32:32,31:35", one trainer per arm).  Kernel libraries
-cannot be loaded side by side in one process: use scripts/ab_env.sh for those.
-Usage: python scripts/ab_mlp_inproc.py [--bm 64,128 | --stagger 0,3 | --split s1:s2,...] [--rounds 8] [--steps 50]
+Arms: rows-kernel tile heights ("--bm 64,128") or weight-gradient split-K slice counts
+("--slices 28,24", one trainer per arm).  Kernel libraries cannot be loaded side by side in one
+process: use scripts/ab_env.sh for those.
+Usage: python scripts/ab_mlp_inproc.py [--bm 64,128 | --slices 28,24] [--rounds 8] [--steps 50]
 """
 import argparse
 import json
@@ -25,28 +25,22 @@ from serverless_learn_amd.ops import _native
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--bm", default="64,128")
-ap.add_argument("--stagger", default=None, help="comma list of rows-kernel stagger counts (s_sleep(127) rounds)")
-ap.add_argument("--split", default=None,
-                help="comma list of s1:s2 weight-gradient splits (dW1 tiles : dW2 tiles slices), one trainer each")
+ap.add_argument("--slices", default=None, help="comma list of weight-gradient split-K slice counts, one trainer each")
 ap.add_argument("--rounds", type=int, default=8)
 ap.add_argument("--steps", type=int, default=50)
 ap.add_argument("--batch", type=int, default=65536)
 a = ap.parse_args()
-if a.split:
-    arms = a.split.split(",")
-else:
-    arms = [int(v) for v in a.stagger.split(",")] if a.stagger else [int(v) for v in a.bm.split(",")]
+arms = [int(v) for v in (a.slices or a.bm).split(",")]
 B = a.batch
 ap_nb = int(os.environ.get("SL_AB_BATCHES", "4"))  # shard size in batches (4: X streams from HBM, as in bench.py)
 x, y = make_mnist_like(B * ap_nb, seed=0)
 xs, ys = torch.from_numpy(x), torch.from_numpy(y)
-if a.split:
+if a.slices:
     trs = {}
     for arm in arms:
-        s1, s2 = (int(v) for v in arm.split(":"))
-        trs[arm] = FusedMLPTrainer(batch=B, device="cuda:0", slices=s1, slices2=s2)
+        trs[arm] = FusedMLPTrainer(batch=B, device="cuda:0", slices=arm)
         trs[arm].load_shard(xs, ys)
-        print(arm, "->", trs[arm].slices, trs[arm].slices2, file=sys.stderr)
+        print(arm, "->", trs[arm].slices, file=sys.stderr)
 else:
     tr = FusedMLPTrainer(batch=B, device="cuda:0")
     tr.load_shard(xs, ys)
@@ -54,10 +48,8 @@ t = {bm: [] for bm in arms}
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for r in range(a.rounds):
     for bm in arms:
-        if a.split:
+        if a.slices:
             tr = trs[bm]
-        elif a.stagger:
-            _native.call("sl_mlp_set_stagger", bm)
         else:
             _native.call("sl_mlp_set_rows_bm", bm)
         tr.graph = None

@@ -261,7 +261,7 @@ class FusedMLPTrainer:
 
     def __init__(self, batch: int, device="cuda", lr: float = 0.05, momentum: float = 0.9,
                  weight_decay: float = 0.0, seed: int = 0, world_size: int = 1,
-                 slices: int | None = None, flat: torch.Tensor | None = None, slices2: int | None = None):
+                 slices: int | None = None, flat: torch.Tensor | None = None):
         from ..ops import _native
 
         if batch % BLOCK_ROWS != 0:
@@ -276,16 +276,10 @@ class FusedMLPTrainer:
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
         self.world_size = world_size
         self.grad_scale = 1.0 / (batch * world_size)
-        s1 = slices or int(os.environ.get("SL_MLP_WG_S1", "0") or 0)  # dW1 split-K slices (0: library default)
+        s1 = slices or int(os.environ.get("SL_MLP_WG_SLICES", "0") or 0)  # split-K slices (0: library default)
         self.slices = int(_native.lib().sl_mlp_wgrad_slices(batch, s1))
         if self.slices <= 0:
             raise ValueError(f"batch {batch} not supported by the weight-gradient kernel")
-        # dW2's own split-K slice count (its stages move 48 KB into LDS, dW1's 40 KB); SL_MLP_WG_S2
-        # overrides the kernel library's default
-        s2 = slices2 or int(os.environ.get("SL_MLP_WG_S2", "0") or 0)
-        self.slices2 = int(_native.lib().sl_mlp_wgrad_slices2(batch, self.slices, s2))
-        if self.slices2 <= 0:
-            raise ValueError(f"dW2 slice count {s2} not supported for batch {batch}")
         self.xa, self.xb = norm_coeffs()
         n = N_PARAMS
         self.n_pad = (n + 3) // 4 * 4
@@ -312,7 +306,7 @@ class FusedMLPTrainer:
         lib = _native.lib()
         # (older kernel builds, kept for A/B runs, have no tiled layout and no stride query)
         self.slab_stride = int(lib.sl_mlp_slab_stride()) if hasattr(lib, "sl_mlp_slab_stride") else self.n_pad
-        self.slab = torch.empty(max(self.slices, self.slices2), self.slab_stride, dtype=torch.float32, device=dev)
+        self.slab = torch.empty(self.slices, self.slab_stride, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.allreduce = None  # callable(grad_tensor) -> None, sums in place (RCCL)
@@ -348,7 +342,7 @@ class FusedMLPTrainer:
     # ---- kernels ----
     def refresh_shadows(self) -> None:
         n = self._n
-        n.call("sl_mlp_sgd", n.ptr(self.params), None, None, 0, 0, 0, None, None, 0.0, 0.0, 0.0, self.xa, self.xb, 0,
+        n.call("sl_mlp_sgd", n.ptr(self.params), None, None, 0, 0, None, None, 0.0, 0.0, 0.0, self.xa, self.xb, 0,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
                None, n.stream_ptr())
 
@@ -377,19 +371,19 @@ class FusedMLPTrainer:
                              p(self.loss), p(self.correct), None, 1),
             "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
-                              self.slices, self.slices2, self.slab_stride),
+                              self.slices, self.slab_stride),
         }
         for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
                                                         "reduce": (1, False, True, False),
                                                         "update": (2, True, False, True)}.items():
             lc[name] = n.Launch("sl_mlp_sgd", p(self.params), p(self.mom),
-                                None if from_grad else p(self.slab), self.slices, self.slices2, self.slab_stride,
+                                None if from_grad else p(self.slab), self.slices, self.slab_stride,
                                 p(self.grad) if from_grad else None, p(self.grad) if grad_out else None,
                                 self.lr, self.momentum, self.weight_decay, *self.dw1_coeffs, mode, *ws,
                                 p(self.cursor) if bump else None)
         if self.xgmi is not None:
             xg = self.xgmi
-            lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.slices2, self.slab_stride, *self.dw1_coeffs,
+            lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.slab_stride, *self.dw1_coeffs,
                                      xg.slot_ptr(0), xg.slot_ptr(1), xg.ctl.data_ptr())
             lc["xbarrier"] = [n.Launch(fn, *xg.args(), *extra) for fn, extra in xg.exchange_launches(self.n_pad)]
             lc["xupdate"] = n.Launch("sl_mlp_sgd_xgmi", p(self.params), p(self.mom), self.lr, self.momentum,

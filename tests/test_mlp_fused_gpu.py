@@ -65,28 +65,6 @@ def test_gradients_match_reference(batch, bm, rows_bm):
     assert abs(st.accuracy - float(correct) / batch) < 0.05
 
 
-@pytest.mark.parametrize("batch,s1,s2", [(4096, 4, 16), (4096, 16, 3), (4096, 28, 37), (65536, 26, 37)])
-def test_gradients_with_per_problem_split_k(batch, s1, s2):
-    """dW1 and dW2 cut into different split-K slice counts (WgProblem::slices): the slab regions
-    a problem does not have are never written nor read (the slab is filled with NaN first)."""
-    x, y = _data(batch, seed=7)
-    flat = M.init_params(3)
-    ref = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0)
-    tr = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.0, slices=s1, slices2=s2)
-    assert tr.slices2 != tr.slices
-    tr.slab.fill_(float("nan"))
-    for t in (ref, tr):
-        t.load_shard(x, y)
-    g0 = ref.compute_grads().double().cpu()
-    g = tr.compute_grads().double().cpu()
-    torch.cuda.synchronize()
-    assert bool(torch.isfinite(g).all())
-    for name, shape, off, n in M.param_layout():
-        a, b = g[off:off + n], g0[off:off + n]
-        # the same products, summed in another order
-        assert float((a - b).norm() / b.norm()) < 1e-5, (name, float((a - b).norm() / b.norm()))
-
-
 def test_sgd_step_matches_reference():
     batch = 512
     x, y = _data(batch, seed=5)
