@@ -78,6 +78,8 @@ def parse(argv=None):
                     help="train through the runtime roles instead of the bare engine: an in-process file "
                          "server, master and worker (gRPC control + data plane, the worker's hipGraph "
                          "chunks, its logging and feedback); 1 GPU")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="--runtime: steps per worker graph chunk (0: the runtime's default, config.py)")
     ap.add_argument("--settle", type=float, default=0.3,
                     help="after the timed region (1 GPU, graph mode): replay the same K-step graph back-to-back "
                          "for this many seconds and report the last replay as settled_* fields (informative; the "
@@ -212,10 +214,12 @@ def runtime_bench(args, dev) -> tuple[float, dict, object]:
     once its device work has drained: hold at W, release to W + K, and the K steps between
     are timed.  Returns (seconds, runtime info, the worker's trainer)."""
     from serverless_learn_amd.proto import messages as pb
+    from serverless_learn_amd.config import Config
     from serverless_learn_amd.runtime.local_cluster import LocalCluster, fast_config
 
     cfg = fast_config(device=str(dev), model=args.model, batch=args.batch,
-                      shard_records=args.batch * args.shard_batches, log_every=64, graph_steps=16,
+                      shard_records=args.batch * args.shard_batches, log_every=64,
+                      graph_steps=args.graph_steps or Config().graph_steps,
                       lr=args.lr, momentum=args.momentum, rpc_timeout_s=30.0, checkup_interval_ms=500,
                       dataset="synthetic-mnist" if args.model == "mlp" else "synthetic-cifar")
     c = LocalCluster(cfg)
