@@ -315,6 +315,9 @@ class FusedMLPTrainer:
         self.n_batches = 1
         self.graph = None
         self.refresh_shadows()
+        # torch loads its reduction kernel's code object on first use (~27 ms): take that here,
+        # at construction, not in the first logged chunk of a training worker (profiles/r04_runtime)
+        self.stats()
 
     n_params = N_PARAMS
     model_name = "mlp-784-256-256-10"

@@ -191,6 +191,7 @@ class FusedResNetTrainer:
         items.append((self.fc_w, self.fc_wt, classes, 1, 512, LOGIT_LD))
         self.wt = K.WeightTransposer(items, dev)
         self.refresh_shadows()
+        self.stats()  # load torch's reduction kernel now, not inside the first logged chunk (as mlp.py)
 
     def _shortcut_even(self, blk) -> bool:
         """A 1x1 / stride-2 shortcut beside a 3x3 / stride-2 conv1 (every ResNet-18 downsample
