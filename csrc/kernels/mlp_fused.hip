@@ -923,156 +923,6 @@ constexpr long TL_W2 = 7L * TL_TILE;            // dW2 tiles (dW1: tiles 0..6, t
 constexpr long TL_SMALL = 9L * TL_TILE;         // [dW3 | db3 | pad | db1 | db2]
 constexpr long TL_STRIDE = (TL_SMALL + W3P_LD + 63) / 64 * 64;
 
-// ---------------------------------------------------------------------------
-// Slab reduction + momentum SGD + bf16 shadow refresh.
-// ---------------------------------------------------------------------------
-struct SgdArgs {
-  float* w;
-  float* mom;
-  const float* slab;
-  int slices;
-  long slab_stride;
-  const float* grad_in;  // used when slab == nullptr
-  float* grad_out;       // reduced gradient written here (all-reduce hand-off)
-  long n;
-  float lr, mu, wd;
-  // dW1 = xa * (slab dW1 rows) + xb * db1: the slabs hold s dH1^T (X + 1024) for raw u8 X (fp16 GEMM,
-  // see mlp_wgrad_kernel), so the host passes xa = xa_norm / s, xb = xb_norm - 1024 xa_norm
-  float xa, xb;
-  int mode;  // 0: refresh bf16 shadows from w; 1: reduce only (grad_out); 2: reduce/read + update
-  uint16_t *w1h, *w2h, *w2th, *w3h, *w3th;
-  int* cursor;
-  // xGMI hand-off (mode 1 only): grad_out / grad_out_alt are this rank's exchange slots 0 / 1,
-  // picked by the parity of the step in flight (xgmi.h)
-  float* grad_out_alt;
-  const unsigned* ar_ctl;
-};
-
-__device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) {
-  const uint16_t h = f2bf(w);
-  if (p < P_B1) {
-    const int o = (int)(p / D_IN), i = (int)(p - (long)o * D_IN);
-    a.w1h[frag_off(o, i, KS1)] = h;                     // layer 1: B[k=i][n=o]
-  } else if (p >= P_W2 && p < P_B2) {
-    const int q = (int)(p - P_W2), o = q >> 8, i = q & 255;
-    a.w2h[frag_off(o, i, KS2)] = h;                     // layer 2: B[k=i][n=o]
-    a.w2th[frag_off(i, o, KS2)] = h;                    // dH1 = dH2 W2: B[k=o][n=i]
-  } else if (p >= P_W3 && p < P_B3) {
-    const int q = (int)(p - P_W3), c = q >> 8, i = q & 255;
-    a.w3h[frag_off(c, i, KS2)] = h;                     // layer 3: B[k=i][n=c]
-    a.w3th[frag_off(i, c, 1)] = h;                      // dH2 = dZ W3: B[k=c][n=i]
-  }
-}
-
-// Four threads per float4 group of parameters: each sums every fourth slab
-// slice and the quad combines by DPP; thread `part` then updates element
-// p0 + part.  (One thread per group gave ~4 waves per CU for a chain of 24
-// dependent-latency slab loads: latency-bound at ~9 us.)
-__device__ __forceinline__ float quad_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
-}
-
-// w0 / m0: the parameter and momentum, loaded by the caller ahead of the slab sums
-__device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p, float gme, float w0, float m0) {
-  if (gout) gout[p] = gme;
-  if (a.mode == 1) return;
-  float w = w0;
-  float d = gme + a.wd * w;
-  if (a.mom) {
-    d = a.mu * m0 + d;
-    a.mom[p] = d;
-  }
-  w -= a.lr * d;
-  a.w[p] = w;
-  write_shadow(a, p, w);
-}
-
-// SGD_TPG threads per float4 group of parameters: each sums every SGD_TPG-th
-// slab slice, the group combines by DPP (quad perms, then row_half_mirror for 8).
-constexpr int SGD_TPG = 4;
-constexpr int SGD_NT = 1024;
-static_assert(SGD_TPG == 4 || SGD_TPG == 8, "4 or 8 threads per group");
-__device__ __forceinline__ float group_sum(float v) {
-  v = quad_sum(v);
-  if constexpr (SGD_TPG == 8) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
-  return v;
-}
-
-// Slab reduction + update over a tiled slab (1): the threads walk the slab in its
-// own order (float4 unit u of every slice: coalesced 1 KB per wave and slice), each unit's 4
-// floats map back to 4 consecutive parameters of one weight row (or, in the small region, to
-// single parameters).  w / mom / the shadows are then touched in a scattered order, but they
-// are 1 MB arrays that stay in L2.
-__device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
-  const long off = u * 4;
-  if (off >= TL_SMALL + W3P_LD) return;
-  long pe = -1;       // this thread's parameter (part < 4)
-  int w1row = -1;     // dW1 row (output feature) of the unit, for the db1 term
-  if (off < TL_SMALL) {
-    const int tile = (int)(off / TL_TILE), within = (int)(off % TL_TILE);
-    const int wave = within >> 12, rem = within & 4095;
-    const int ins = rem >> 8, lane = (rem & 255) >> 2;
-    const int m = (wave & 1) * 128 + (ins >> 1) * 16 + (lane & 15);
-    const int nn = (wave >> 1) * 32 + (ins & 1) * 16 + (lane >> 4) * 4;
-    if (tile < 7) {
-      const int n = tile * 128 + nn;
-      if (n >= D_IN) return;  // dW1's last tile: 16 real columns (whole group exits together)
-      pe = P_W1 + (long)m * D_IN + n + part;
-      w1row = m;
-    } else {
-      pe = P_W2 + (long)m * HID + (tile - 7) * 128 + nn + part;
-    }
-  } else {
-    const int q = (int)(off - TL_SMALL) + part;
-    if (q < W3P_N) pe = P_W3 + q;
-    else if (q >= W3P_DB1 && q < W3P_DB2) pe = P_B1 + q - W3P_DB1;
-    else if (q >= W3P_DB2 && q < W3P_LD) pe = P_B2 + q - W3P_DB2;
-  }
-  const bool mine = part < 4 && pe >= 0;
-  const bool upd = mine && a.mode != 1;
-  const float w0 = upd ? a.w[pe] : 0.f;
-  const float m0 = upd && a.mom ? a.mom[pe] : 0.f;
-  float g[4] = {0.f, 0.f, 0.f, 0.f};
-  float db = 0.f;
-  const float* src = a.slab + off;
-  const float* dbs = a.slab + TL_SMALL + W3P_DB1 + (w1row >= 0 ? w1row : 0);
-  const int ns = a.slices;
-  constexpr int U = 8;
-  for (int s0 = part; s0 < ns; s0 += SGD_TPG * U) {
-    float4 v[U];
-    float d[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int sidx = s0 + k * SGD_TPG;
-      v[k] = sidx < ns ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-      d[k] = (w1row >= 0 && sidx < ns) ? dbs[(long)sidx * a.slab_stride] : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      g[0] += v[k].x; g[1] += v[k].y; g[2] += v[k].z; g[3] += v[k].w;
-      db += d[k];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) g[j] = group_sum(g[j]);
-  float gme = g[part & 3];
-  if (w1row >= 0) {
-    db = group_sum(db);
-    gme = a.xa * gme + a.xb * db;
-  }
-  if (!mine) return;
-  float* gout = a.grad_out;
-  if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
-  sgd_apply(a, gout, pe, gme, w0, m0);
-}
-
-// float4 units a launch of mlp_sgd_kernel walks: the slab's (tiled) or the parameters'
-__host__ __device__ constexpr long sgd_units(bool slab) {
-  return slab ? TL_STRIDE / 4 : (P_N + 3) / 4;
-}
-
 struct WgProblem {
   const void* a;  // [batch][256] bf16: dH1 / dH2
   const void* b;  // [batch][ldb]: u8 X (problem 0) / bf16 H1
@@ -1091,10 +941,6 @@ struct WgArgs {
   int n_batches, batch;
   const float* w3p;      // [n_w3p][W3P_LD] partial rows of the rows kernel
   int n_w3p;
-  // FUSE: the slab reduction + SGD of mlp_sgd_kernel run at the end of this kernel, after a
-  // grid barrier (bar: [0] arrivals, [1] generation, [2] timeout flag)
-  SgdArgs sgd;
-  unsigned* bar;
 };
 
 constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages in flight
@@ -1193,7 +1039,6 @@ constexpr int WG_MI = 8;  // 16-row A (dZ) fragments per wave
 constexpr int WG_NJ = 2;  // 16-column B fragments per wave
 constexpr int WG_NF = WG_MI + WG_NJ;       // fragments per wave per k-step
 
-template <bool FUSE>
 __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1519,42 +1364,156 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       if (q < W3P_N || q >= W3P_DB1) srow[TL_SMALL + q] = tv[j];
     }
   }
-  if constexpr (FUSE) {
-    // Grid barrier, then this workgroup's share of mlp_sgd_kernel's units.  Every workgroup is
-    // resident (the host launches this form only when the grid fits one workgroup per CU), so
-    // the spin cannot wait on an unscheduled workgroup; it is still bounded (XG_TIMEOUT_TICKS):
-    // a timeout sets bar[2] and leaves the update undone rather than hanging the GPU.
-    // __syncthreads() drains every thread's slab stores (workgroup release: vmcnt(0)); the
-    // agent-scope fences write back / invalidate this XCD's L2 so the other XCDs' slab tiles are
-    // read from memory (the kernel boundary did this before).
-    __syncthreads();
-    if (tid == 0) {
-      __threadfence();
-      const unsigned gen = __hip_atomic_load(A.bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned prev = __hip_atomic_fetch_add(A.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == gridDim.x - 1) {
-        __hip_atomic_store(A.bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(A.bar + 1, gen + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(A.bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-          __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > XG_TIMEOUT_TICKS) {
-            __hip_atomic_store(A.bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-      }
-      __threadfence();
-    }
-    __syncthreads();
-    if (__hip_atomic_load(A.bar + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
-    constexpr int GPW = WG_NT / SGD_TPG;  // unit groups per workgroup
-    const long units = sgd_units(true);
-    for (long u = (long)blockIdx.x * GPW + tid / SGD_TPG; u < units; u += (long)gridDim.x * GPW)
-      sgd_tiled(A.sgd, u, tid % SGD_TPG);
-    if (blockIdx.x == 0 && tid == 0 && A.sgd.cursor) atomicAdd(A.sgd.cursor, 1);
+}
+
+// ---------------------------------------------------------------------------
+// Slab reduction + momentum SGD + bf16 shadow refresh.
+// ---------------------------------------------------------------------------
+struct SgdArgs {
+  float* w;
+  float* mom;
+  const float* slab;
+  int slices;
+  long slab_stride;
+  const float* grad_in;  // used when slab == nullptr
+  float* grad_out;       // reduced gradient written here (all-reduce hand-off)
+  long n;
+  float lr, mu, wd;
+  // dW1 = xa * (slab dW1 rows) + xb * db1: the slabs hold s dH1^T (X + 1024) for raw u8 X (fp16 GEMM,
+  // see mlp_wgrad_kernel), so the host passes xa = xa_norm / s, xb = xb_norm - 1024 xa_norm
+  float xa, xb;
+  int mode;  // 0: refresh bf16 shadows from w; 1: reduce only (grad_out); 2: reduce/read + update
+  uint16_t *w1h, *w2h, *w2th, *w3h, *w3th;
+  int* cursor;
+  // xGMI hand-off (mode 1 only): grad_out / grad_out_alt are this rank's exchange slots 0 / 1,
+  // picked by the parity of the step in flight (xgmi.h)
+  float* grad_out_alt;
+  const unsigned* ar_ctl;
+};
+
+__device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) {
+  const uint16_t h = f2bf(w);
+  if (p < P_B1) {
+    const int o = (int)(p / D_IN), i = (int)(p - (long)o * D_IN);
+    a.w1h[frag_off(o, i, KS1)] = h;                     // layer 1: B[k=i][n=o]
+  } else if (p >= P_W2 && p < P_B2) {
+    const int q = (int)(p - P_W2), o = q >> 8, i = q & 255;
+    a.w2h[frag_off(o, i, KS2)] = h;                     // layer 2: B[k=i][n=o]
+    a.w2th[frag_off(i, o, KS2)] = h;                    // dH1 = dH2 W2: B[k=o][n=i]
+  } else if (p >= P_W3 && p < P_B3) {
+    const int q = (int)(p - P_W3), c = q >> 8, i = q & 255;
+    a.w3h[frag_off(c, i, KS2)] = h;                     // layer 3: B[k=i][n=c]
+    a.w3th[frag_off(i, c, 1)] = h;                      // dH2 = dZ W3: B[k=c][n=i]
   }
+}
+
+// Four threads per float4 group of parameters: each sums every fourth slab
+// slice and the quad combines by DPP; thread `part` then updates element
+// p0 + part.  (One thread per group gave ~4 waves per CU for a chain of 24
+// dependent-latency slab loads: latency-bound at ~9 us.)
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+
+// w0 / m0: the parameter and momentum, loaded by the caller ahead of the slab sums
+__device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p, float gme, float w0, float m0) {
+  if (gout) gout[p] = gme;
+  if (a.mode == 1) return;
+  float w = w0;
+  float d = gme + a.wd * w;
+  if (a.mom) {
+    d = a.mu * m0 + d;
+    a.mom[p] = d;
+  }
+  w -= a.lr * d;
+  a.w[p] = w;
+  write_shadow(a, p, w);
+}
+
+// SGD_TPG threads per float4 group of parameters: each sums every SGD_TPG-th
+// slab slice, the group combines by DPP (quad perms, then row_half_mirror for 8).
+constexpr int SGD_TPG = 4;
+constexpr int SGD_NT = 1024;
+static_assert(SGD_TPG == 4 || SGD_TPG == 8, "4 or 8 threads per group");
+__device__ __forceinline__ float group_sum(float v) {
+  v = quad_sum(v);
+  if constexpr (SGD_TPG == 8) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  return v;
+}
+
+// Slab reduction + update over a tiled slab (1): the threads walk the slab in its
+// own order (float4 unit u of every slice: coalesced 1 KB per wave and slice), each unit's 4
+// floats map back to 4 consecutive parameters of one weight row (or, in the small region, to
+// single parameters).  w / mom / the shadows are then touched in a scattered order, but they
+// are 1 MB arrays that stay in L2.
+__device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
+  const long off = u * 4;
+  if (off >= TL_SMALL + W3P_LD) return;
+  long pe = -1;       // this thread's parameter (part < 4)
+  int w1row = -1;     // dW1 row (output feature) of the unit, for the db1 term
+  if (off < TL_SMALL) {
+    const int tile = (int)(off / TL_TILE), within = (int)(off % TL_TILE);
+    const int wave = within >> 12, rem = within & 4095;
+    const int ins = rem >> 8, lane = (rem & 255) >> 2;
+    const int m = (wave & 1) * 128 + (ins >> 1) * 16 + (lane & 15);
+    const int nn = (wave >> 1) * 32 + (ins & 1) * 16 + (lane >> 4) * 4;
+    if (tile < 7) {
+      const int n = tile * 128 + nn;
+      if (n >= D_IN) return;  // dW1's last tile: 16 real columns (whole group exits together)
+      pe = P_W1 + (long)m * D_IN + n + part;
+      w1row = m;
+    } else {
+      pe = P_W2 + (long)m * HID + (tile - 7) * 128 + nn + part;
+    }
+  } else {
+    const int q = (int)(off - TL_SMALL) + part;
+    if (q < W3P_N) pe = P_W3 + q;
+    else if (q >= W3P_DB1 && q < W3P_DB2) pe = P_B1 + q - W3P_DB1;
+    else if (q >= W3P_DB2 && q < W3P_LD) pe = P_B2 + q - W3P_DB2;
+  }
+  const bool mine = part < 4 && pe >= 0;
+  const bool upd = mine && a.mode != 1;
+  const float w0 = upd ? a.w[pe] : 0.f;
+  const float m0 = upd && a.mom ? a.mom[pe] : 0.f;
+  float g[4] = {0.f, 0.f, 0.f, 0.f};
+  float db = 0.f;
+  const float* src = a.slab + off;
+  const float* dbs = a.slab + TL_SMALL + W3P_DB1 + (w1row >= 0 ? w1row : 0);
+  const int ns = a.slices;
+  constexpr int U = 8;
+  for (int s0 = part; s0 < ns; s0 += SGD_TPG * U) {
+    float4 v[U];
+    float d[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int sidx = s0 + k * SGD_TPG;
+      v[k] = sidx < ns ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      d[k] = (w1row >= 0 && sidx < ns) ? dbs[(long)sidx * a.slab_stride] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      g[0] += v[k].x; g[1] += v[k].y; g[2] += v[k].z; g[3] += v[k].w;
+      db += d[k];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) g[j] = group_sum(g[j]);
+  float gme = g[part & 3];
+  if (w1row >= 0) {
+    db = group_sum(db);
+    gme = a.xa * gme + a.xb * db;
+  }
+  if (!mine) return;
+  float* gout = a.grad_out;
+  if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
+  sgd_apply(a, gout, pe, gme, w0, m0);
+}
+
+// float4 units a launch of mlp_sgd_kernel walks: the slab's (tiled) or the parameters'
+__host__ __device__ constexpr long sgd_units(bool slab) {
+  return slab ? TL_STRIDE / 4 : (P_N + 3) / 4;
 }
 
 __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
@@ -1695,14 +1654,16 @@ int sl_mlp_wgrad_slices(int batch, int requested) {
   return (total + spp - 1) / spp;
 }
 
-static int wgrad_args(WgArgs& a, int batch, const uint8_t* x, const int* cursor, int n_batches, const uint16_t* h1,
-                      const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
-                      long slab_stride) {
+// x: the resident u8 shard [n_batches * batch][784]; the batch rows are the
+// ones the rows kernel used (cursor not yet bumped: mlp_sgd_kernel bumps it).
+int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, const uint16_t* h1,
+                 const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
+                 long slab_stride, hipStream_t stream) {
   if (!w3p || n_w3p != batch / 64) return -1;
   if (slab_stride < TL_STRIDE) return -1;
   const int s_eff = sl_mlp_wgrad_slices(batch, slices);
   if (s_eff <= 0 || s_eff != slices) return -1;
-  a = WgArgs{};
+  WgArgs a;
   // dW1, db1 = dH1^T [256 x B] . X (raw u8; normalised in mlp_sgd_kernel)
   a.p[0] = WgProblem{dh1, x, D_IN, D_IN, (D_IN + 127) / 128, 0, P_W1, P_B1, W3P_DB1};
   // dW2, db2 = dH2^T . H1
@@ -1719,50 +1680,7 @@ static int wgrad_args(WgArgs& a, int batch, const uint8_t* x, const int* cursor,
   a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
   a.w3p = w3p; a.n_w3p = n_w3p;
   if (((uintptr_t)x & 15) != 0 || ((uintptr_t)w3p & 15) != 0) return -2;  // 16-B pieces / float4 reads
-  return 0;
-}
-
-// x: the resident u8 shard [n_batches * batch][784]; the batch rows are the
-// ones the rows kernel used (cursor not yet bumped: mlp_sgd_kernel bumps it).
-int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, const uint16_t* h1,
-                 const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
-                 long slab_stride, hipStream_t stream) {
-  WgArgs a;
-  if (int rc = wgrad_args(a, batch, x, cursor, n_batches, h1, dh2, dh1, w3p, n_w3p, slab, slices, slab_stride)) return rc;
-  hipLaunchKernelGGL(mlp_wgrad_kernel<false>, dim3(a.total_tiles * slices), dim3(WG_NT), 0, stream, a);
-  SL_CHECK_LAUNCH();
-  return 0;
-}
-
-// Weight gradient + slab reduction + momentum SGD in ONE launch (world 1): the update that
-// mlp_sgd_kernel (mode 2) would run follows a grid barrier at the end of the weight-gradient
-// kernel, which saves that kernel's launch and boundary.  bar: 3 zeroed words owned by the
-// caller.  Returns 3 (nothing launched) when the grid does not fit one workgroup per CU of this
-// device, where a barrier could wait on a workgroup that is never scheduled: use
-// sl_mlp_wgrad + sl_mlp_sgd then.
-int sl_mlp_wgrad_sgd(int batch, const uint8_t* x, int* cursor, int n_batches, const uint16_t* h1,
-                     const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
-                     long slab_stride, float* w, float* mom, float lr, float mu, float wd, float xa, float xb,
-                     uint16_t* w1h, uint16_t* w2h, uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, unsigned* bar,
-                     hipStream_t stream) {
-  WgArgs a;
-  if (int rc = wgrad_args(a, batch, x, cursor, n_batches, h1, dh2, dh1, w3p, n_w3p, slab, slices, slab_stride)) return rc;
-  if (!w || !bar || !w1h || !w2h || !w2th || !w3h || !w3th) return -1;
-  static int n_cu = -1;
-  if (n_cu < 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n_cu = 0;
-  }
-  const int grid = a.total_tiles * slices;
-  if (grid > n_cu) return 3;
-  SgdArgs& g = a.sgd;
-  g = SgdArgs{};
-  g.w = w; g.mom = mom; g.slab = slab; g.slices = slices; g.slab_stride = slab_stride; g.n = P_N;
-  g.lr = lr; g.mu = mu; g.wd = wd; g.xa = xa; g.xb = xb; g.mode = 2;
-  g.w1h = w1h; g.w2h = w2h; g.w2th = w2th; g.w3h = w3h; g.w3th = w3th; g.cursor = cursor;
-  a.bar = bar;
-  hipLaunchKernelGGL(mlp_wgrad_kernel<true>, dim3(grid), dim3(WG_NT), 0, stream, a);
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(WG_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -25,13 +25,12 @@ from serverless_learn_amd.ops import _native
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--bm", default="64,128")
-ap.add_argument("--fuse", default=None, help="comma list of 1/0: SGD fused into the weight-gradient launch or not")
 ap.add_argument("--slices", default=None, help="comma list of weight-gradient split-K slice counts, one trainer each")
 ap.add_argument("--rounds", type=int, default=8)
 ap.add_argument("--steps", type=int, default=50)
 ap.add_argument("--batch", type=int, default=65536)
 a = ap.parse_args()
-arms = [int(v) for v in (a.fuse or a.slices or a.bm).split(",")]
+arms = [int(v) for v in (a.slices or a.bm).split(",")]
 B = a.batch
 ap_nb = int(os.environ.get("SL_AB_BATCHES", "4"))  # shard size in batches (4: X streams from HBM, as in bench.py)
 x, y = make_mnist_like(B * ap_nb, seed=0)
@@ -49,9 +48,7 @@ t = {bm: [] for bm in arms}
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for r in range(a.rounds):
     for bm in arms:
-        if a.fuse:
-            tr.fuse_sgd = bool(bm)
-        elif a.slices:
+        if a.slices:
             tr = trs[bm]
         else:
             _native.call("sl_mlp_set_rows_bm", bm)

@@ -309,12 +309,6 @@ class FusedMLPTrainer:
         self.slab = torch.empty(self.slices, self.slab_stride, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
-        # world-1 step as 2 launches: the SGD after a grid barrier at the end of the weight
-        # gradient (sl_mlp_wgrad_sgd) when its grid fits one workgroup per CU; SL_MLP_FUSE_SGD=0
-        # keeps the separate mlp_sgd_kernel.  bar: arrivals, generation, timeout flag
-        self.sgd_bar = torch.zeros(4, dtype=torch.int32, device=dev)
-        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
-        self.fuse_sgd = os.environ.get("SL_MLP_FUSE_SGD", "1") != "0" and 9 * self.slices <= n_cu
         self.allreduce = None  # callable(grad_tensor) -> None, sums in place (RCCL)
         self.xgmi = None       # parallel.xgmi.XgmiExchange: all-reduce fused into the update (no RCCL)
         self.x = self.y = None
@@ -382,11 +376,6 @@ class FusedMLPTrainer:
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
                               self.slices, self.slab_stride),
         }
-        lc["wgrad_sgd"] = n.Launch("sl_mlp_wgrad_sgd", self.batch, p(self.x), p(self.cursor), self.n_batches,
-                                   p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0],
-                                   p(self.slab), self.slices, self.slab_stride, p(self.params), p(self.mom),
-                                   self.lr, self.momentum, self.weight_decay, *self.dw1_coeffs, *ws,
-                                   p(self.sgd_bar))
         for name, (mode, from_grad, grad_out, bump) in {"sgd": (2, False, False, True),
                                                         "reduce": (1, False, True, False),
                                                         "update": (2, True, False, True)}.items():
@@ -487,9 +476,6 @@ class FusedMLPTrainer:
         if getattr(self, "probe", None) is not None:
             self.probe()
         self._rows(True)
-        if self.xgmi is None and self.allreduce is None and self.fuse_sgd:
-            self._launches()["wgrad_sgd"]()
-            return
         self._wgrad()
         if self.xgmi is not None:
             lc = self._launches()
@@ -503,11 +489,6 @@ class FusedMLPTrainer:
             self._sgd(1, from_grad=False, grad_out=True, bump=False)
             self.allreduce(self.grad)
             self._sgd(2, from_grad=True, grad_out=False)
-
-    def fused_sgd_timed_out(self) -> bool:
-        """The fused weight-gradient + SGD launch's grid barrier gave up (never expected: every
-        workgroup is resident); its updates since are void."""
-        return bool(int(self.sgd_bar[2].item()))
 
     def capture(self, warmup: int = 2, unroll: int = 1) -> None:
         """Capture one step into a hipGraph (kernels only, or kernels + RCCL);

@@ -34,7 +34,6 @@ _SIGS: dict[str, list] = {
     "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P],
     "sl_mlp_wgrad": [I, P, P, I, P, P, P, P, I, P, I, L, P],
     "sl_mlp_wgrad_slices": [I, I],
-    "sl_mlp_wgrad_sgd": [I, P, P, I, P, P, P, P, I, P, I, L, P, P, F, F, F, F, F, P, P, P, P, P, P],
     "sl_mlp_set_rows_bm": [I],
     "sl_conv_set_halo": [I],
     "sl_conv_set_phase": [I],

@@ -65,34 +65,6 @@ def test_gradients_match_reference(batch, bm, rows_bm):
     assert abs(st.accuracy - float(correct) / batch) < 0.05
 
 
-@pytest.mark.parametrize("batch", [4096, 65536])
-def test_fused_wgrad_sgd_matches_separate_launches(batch):
-    """World-1 steps with the SGD fused behind a grid barrier at the end of the weight-gradient
-    kernel (sl_mlp_wgrad_sgd) are bit-identical to the wgrad + mlp_sgd_kernel launches, eager
-    and graph-replayed, and the barrier never times out."""
-    x, y = _data(batch * 2, seed=23)
-    flat = M.init_params(12)
-    a = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.9, weight_decay=1e-4)
-    b = M.FusedMLPTrainer(batch=batch, flat=flat, momentum=0.9, weight_decay=1e-4)
-    assert a.fuse_sgd
-    b.fuse_sgd = False
-    for t in (a, b):
-        t.load_shard(x, y)
-    for _ in range(3):
-        a.step()
-        b.step()
-    a.capture(warmup=0, unroll=4)
-    b.capture(warmup=0, unroll=4)
-    a.steps(9)
-    b.steps(9)
-    torch.cuda.synchronize()
-    assert not a.fused_sgd_timed_out()
-    assert int(a.cursor.item()) == int(b.cursor.item()) == 12
-    assert torch.equal(a.params, b.params)
-    assert torch.equal(a.mom, b.mom)
-    assert torch.equal(a.w1h, b.w1h) and torch.equal(a.w2th, b.w2th) and torch.equal(a.w3th, b.w3th)
-
-
 def test_sgd_step_matches_reference():
     batch = 512
     x, y = _data(batch, seed=5)
