@@ -1434,7 +1434,7 @@ __device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p,
 // SGD_TPG threads per float4 group of parameters: each sums every SGD_TPG-th
 // slab slice, the group combines by DPP (quad perms, then row_half_mirror for 8).
 constexpr int SGD_TPG = 4;
-constexpr int SGD_NT = 1024;
+constexpr int SGD_NT = 512;  // 512: 10.2 vs 11.4 us for 1024 on the tiled slab (profiles/r04_sgd)
 static_assert(SGD_TPG == 4 || SGD_TPG == 8, "4 or 8 threads per group");
 __device__ __forceinline__ float group_sum(float v) {
   v = quad_sum(v);
