@@ -36,6 +36,8 @@ CONV_CASES = [
     (1024, 16, 128, 256, 3, 2, 1),  # forward + phase-mode dgrad (parity classes of 65,536 rows)
     (256, 8, 256, 512, 3, 1, 1),    # stage-4 shape forward; large-tile weight gradient (cout 512)
     (64, 16, 128, 256, 3, 1, 1),    # large-tile weight gradient, cout 256, K 1152
+    (1024, 32, 64, 128, 3, 2, 1),   # phase-mode dgrad into 64 channels: 256 x 64 large tiles
+    (1024, 32, 64, 128, 1, 2, 0),   # 1x1 / stride-2 shortcut dgrad into 64 channels (256 x 64 tiles)
 ]
 
 
@@ -99,6 +101,7 @@ BNB_CASES = [
     (4, 32, 64, 64, 3, 1),
     (256, 16, 128, 128, 3, 1),
     (1024, 16, 128, 256, 3, 2),
+    (1024, 32, 64, 128, 3, 2),      # 256 x 64 large tiles with the fused BN-backward epilogue
     (2, 16, 64, 128, 3, 2),
     (3, 7, 128, 256, 3, 1),
 ]
@@ -153,7 +156,7 @@ def test_dgrad_fused_bn_backward_matches_separate_reduce(case, mode):
         assert rel(f2, r2) < 1e-4
 
 
-@pytest.mark.parametrize("n,h,c,cout", [(8, 32, 64, 128), (4, 16, 128, 256), (2, 8, 256, 512)])
+@pytest.mark.parametrize("n,h,c,cout", [(8, 32, 64, 128), (1024, 32, 64, 128), (4, 16, 128, 256), (2, 8, 256, 512)])
 @pytest.mark.parametrize("fused_bn", [False, True])
 def test_shortcut_gradient_into_even_positions(n, h, c, cout, fused_bn):
     """Downsample block input gradient: the 1x1/s2 shortcut data gradient written straight into
