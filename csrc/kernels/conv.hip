@@ -492,14 +492,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #define SL_GEMM_BIG 1  // use conv_gemm_big_kernel where it applies
 #endif
 
-// BN = 128, or 64 for the data gradients into 64-channel tensors (stage 2's stride-2 conv1 in
-// four parity classes and its 1x1 shortcut), which otherwise ran 128 x 64 tiles at 6 % MFMA-busy.
-template <bool TRANSPOSED, int BN>
+template <bool TRANSPOSED>
 __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
-  static_assert(BN == 128 || BN == 64, "128- or 64-column tiles");
-  constexpr int BM = 256, NSLOT = 3;
-  constexpr int MT = 4, NT = BN / 32;  // 16 x 16 MFMA tiles per wave (64 x BN / 2)
-  constexpr int PA = 4, PB = BN / 64;  // DMA pieces (8 rows x 64 k, 1 KB) per wave per stage
+  constexpr int BM = 256, BN = 128, NSLOT = 3;
+  constexpr int MT = 4, NT = 4;     // 16 x 16 MFMA tiles per wave (64 x 64)
+  constexpr int PA = 4, PB = 2;     // DMA pieces (8 rows x 64 k, 1 KB) per wave per stage
   constexpr int PS = PA + PB;
   constexpr int SLOT = (BM + BN) * BK;  // elements: 48 KB
   constexpr int CS_LD = BN + 8;
@@ -584,7 +581,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
   }
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    const int r = wn * (BN / 2) + j * 16 + lr;
+    const int r = wn * 64 + j * 16 + lr;
 #pragma unroll
     for (int h = 0; h < 2; ++h) boff[j][h] = (uint32_t)(((BM + r) * BK + swz64(h * 4 + lg, r) * 8) * 2);
   }
@@ -646,7 +643,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
       s += __shfl_xor(s, 32);
       q += __shfl_xor(q, 16);
       q += __shfl_xor(q, 32);
-      const int col = n0 + wn * (BN / 2) + j * 16 + lr;
+      const int col = n0 + wn * 64 + j * 16 + lr;
       if (lg == 0 && col < e.ncols) {
         rsum_add(rep, col, s);
         rsum_add(rep, e.ncols + col, q);
@@ -658,7 +655,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const int col = n0 + wn * (BN / 2) + j * 16 + lr;
+        const int col = n0 + wn * 64 + j * 16 + lr;
         if (col >= e.ncols) continue;
         const float b = e.bias ? e.bias[col] : 0.f;
 #pragma unroll
@@ -674,7 +671,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int cl = wn * (BN / 2) + j * 16 + lr;
+      const int cl = wn * 64 + j * 16 + lr;
       const float b = (e.bias && n0 + cl < e.ncols) ? e.bias[n0 + cl] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) Cs[(wm * 64 + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[i][j][r] + b);
@@ -1247,13 +1244,10 @@ static GemmPlan plan_gemm(const ConvGeom& g, const ConvEpi& e) {
   GemmPlan p{};
   // 256 x 128 tiles: uniform taps (64-channel stages), whole 128-column tiles, and enough
   // tiles for every CU; transposed gathers only in phase mode or at stride 1
-  // (64-column tiles when the whole output is 64 channels wide)
-  const int bbn = (e.ncols & 127) == 0 ? 128 : (e.ncols == 64 ? 64 : 0);
-  const long big_tiles = bbn ? (long)((g.M + 255) / 256) * (e.ncols / bbn) : 0;
-  if (gemm_big_enabled() && bbn && (g.SC & 63) == 0 && (g.K & 63) == 0 && big_tiles >= 256 &&
-      (!T || g.ph >= 0 || g.stride == 1) && (g.wld & 7) == 0 && (!e.y || (e.ldy & 7) == 0) &&
-      (bbn == 128 || gemm_big_enabled() != 2)) {
-    p.big = 1; p.BM = 256; p.BN = bbn; p.tiles_n = e.ncols / bbn; p.grid = big_tiles;
+  const long big_tiles = (long)((g.M + 255) / 256) * (e.ncols / 128);
+  if (gemm_big_enabled() && (g.SC & 63) == 0 && (g.K & 63) == 0 && (e.ncols & 127) == 0 && big_tiles >= 256 &&
+      (!T || g.ph >= 0 || g.stride == 1) && (g.wld & 7) == 0 && (!e.y || (e.ldy & 7) == 0)) {
+    p.big = 1; p.BM = 256; p.BN = 128; p.tiles_n = e.ncols / 128; p.grid = big_tiles;
     return p;
   }
   const bool small_n = e.ncols <= 64;
@@ -1273,8 +1267,7 @@ static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) 
   const GemmPlan p = plan_gemm<T>(g, e);
   dim3 grid((unsigned)p.grid);
   if (p.big) {
-    if (p.BN == 128) hipLaunchKernelGGL((conv_gemm_big_kernel<T, 128>), grid, dim3(512), 0, stream, g, e, p.tiles_n);
-    else hipLaunchKernelGGL((conv_gemm_big_kernel<T, 64>), grid, dim3(512), 0, stream, g, e, p.tiles_n);
+    hipLaunchKernelGGL((conv_gemm_big_kernel<T>), grid, dim3(512), 0, stream, g, e, p.tiles_n);
     SL_CHECK_LAUNCH();
     return 0;
   }

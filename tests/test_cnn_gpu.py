@@ -36,8 +36,8 @@ CONV_CASES = [
     (1024, 16, 128, 256, 3, 2, 1),  # forward + phase-mode dgrad (parity classes of 65,536 rows)
     (256, 8, 256, 512, 3, 1, 1),    # stage-4 shape forward; large-tile weight gradient (cout 512)
     (64, 16, 128, 256, 3, 1, 1),    # large-tile weight gradient, cout 256, K 1152
-    (1024, 32, 64, 128, 3, 2, 1),   # phase-mode dgrad into 64 channels: 256 x 64 large tiles
-    (1024, 32, 64, 128, 1, 2, 0),   # 1x1 / stride-2 shortcut dgrad into 64 channels (256 x 64 tiles)
+    (1024, 32, 64, 128, 3, 2, 1),   # ResNet-18 stage 2 at B = 1024: phase-mode dgrad into 64 channels
+    (1024, 32, 64, 128, 1, 2, 0),   # ... and its 1x1 / stride-2 shortcut
 ]
 
 
@@ -101,7 +101,7 @@ BNB_CASES = [
     (4, 32, 64, 64, 3, 1),
     (256, 16, 128, 128, 3, 1),
     (1024, 16, 128, 256, 3, 2),
-    (1024, 32, 64, 128, 3, 2),      # 256 x 64 large tiles with the fused BN-backward epilogue
+    (1024, 32, 64, 128, 3, 2),      # stage-2 shape with the fused BN-backward epilogue
     (2, 16, 64, 128, 3, 2),
     (3, 7, 128, 256, 3, 1),
 ]
