@@ -292,10 +292,6 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   uint16_t* R1 = ONE ? smem : smem + REGB;      // H1 image -> dH1 image
   uint16_t* RZ = smem + (ONE ? REGB : 2 * REGB);  // dZ image
   uint8_t* M1 = reinterpret_cast<uint8_t*>(smem + REGB + BM * DZL);  // ONE: [BM][64] H1 mask nibbles
-  // Byte offset of mask dword d (features 16 d .. 16 d + 15) of row r: the dword index is XORed
-  // with (r / 4) % 16.  Unswizzled, the 16 rows of a fragment (64-B row stride) fell on 4 of the
-  // 64 banks; the rows kernel spent 48 % of its LDS-active cycles in bank conflicts (r04_s).
-  auto m1_off = [](int r, int d) { return r * 64 + 4 * (d ^ ((r >> 2) & 15)); };
   // ReLU masks are NOT kept in registers: H1/H2 stay in LDS until the masked
   // backward products overwrite them in place (hipcc held 64 compare masks per
   // layer in SGPR pairs and spilled ~200 SGPRs).
@@ -407,7 +403,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
         v.y = pack2(fmaxf(fmaf(sc, acc[m][n][2], bias.z), 0.f), fmaxf(fmaf(sc, acc[m][n][3], bias.w), 0.f));
         *reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col) = v;
         if (ONE && with_mask)
-          M1[m1_off(rw + m * 16 + lr, col >> 4) + lg] =
+          M1[(rw + m * 16 + lr) * 64 + (col >> 2)] =
               (uint8_t)(((v.x & 0xffffu) != 0) | (((v.x >> 16) != 0) << 1) | (((v.y & 0xffffu) != 0) << 2) |
                         (((v.y >> 16) != 0) << 3));
       }
@@ -418,7 +414,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   // alive across the whole kernel (it spilled them, and each spill reload's vmcnt(0)
   // drained the dH2 stores in flight).
   auto masked_bits_out = [&](uint16_t* img) {
-    int mbo = (rw + lr) * 64 + lg;
+    int mbo = (rw + lr) * 64 + (cw >> 2) + lg;
     asm volatile("" : "+v"(mbo));
     const uint8_t* M1b = M1 + mbo;
 #pragma unroll
@@ -426,7 +422,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       const int col = cw + n * 16 + 4 * lg;
 #pragma unroll
       for (int m = 0; m < MF; ++m) {
-        const uint32_t b = M1b[m1_off(rw + lr + m * 16, (cw >> 4) + n) - (rw + lr) * 64];
+        const uint32_t b = M1b[(m * 16) * 64 + n * 4];
         uint2 v;
         v.x = pack2((b & 1u) ? acc[m][n][0] : 0.f, (b & 2u) ? acc[m][n][1] : 0.f);
         v.y = pack2((b & 4u) ? acc[m][n][2] : 0.f, (b & 8u) ? acc[m][n][3] : 0.f);
@@ -797,7 +793,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
     // HBM (8 B per fragment row), and the db1 partial as fp32 column sums (DPP over the
     // 16 rows of a fragment).  The LDS image + barrier + re-read of the other tiles cost
     // ~16k cycles here with every CU in this phase at once (profiles/r03_big).
-    int mbo = (rw + lr) * 64 + lg;
+    int mbo = (rw + lr) * 64 + (cw >> 2) + lg;
     asm volatile("" : "+v"(mbo));
     const uint8_t* M1b = M1 + mbo;
     const auto dst = __builtin_amdgcn_make_buffer_rsrc(a.dh1 + (long)row0 * HID, 0, BM * HID * 2, 0x00020000);
@@ -817,7 +813,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
     for (int m = 0; m < MF; ++m) {
 #pragma unroll
       for (int n = 0; n < NF; ++n) {
-        const int b = M1b[m1_off(rw + lr + m * 16, (cw >> 4) + n) - (rw + lr) * 64];
+        const int b = M1b[(m * 16) * 64 + n * 4];
         floatx4_t v;
 #pragma unroll
         for (int r = 0; r < 4; ++r)  // bit r sign-extended to an all-ones / zero mask
