@@ -1117,53 +1117,34 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = zero4();
 
-  // Software-pipelined as conv_gemm_big_kernel: stage st + 1's transposed fragment reads run
-  // under stage st's MFMAs (two register sets); stage st's slot takes stage st + 3.
-  short8_t af[2][2][MT], bf[2][2][NT];  // [register set][k half][fragment]
-  auto read_frags = [&](int st, auto set_c) {
-    constexpr int S = decltype(set_c)::value;
-    const uint32_t sb = lds0 + (uint32_t)((st % NSLOT) * SLOT * 2);
-#pragma unroll
-    for (int i = 0; i < MT; ++i) af[S][0][i] = tr8<WA, 0>(sb + aoff[i]);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) bf[S][0][j] = tr8<WB, 0>(sb + boff[j]);
-#pragma unroll
-    for (int i = 0; i < MT; ++i) af[S][1][i] = tr8<WA, 32 * WA * 16>(sb + aoff[i]);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) bf[S][1][j] = tr8<WB, 32 * WB * 16>(sb + boff[j]);
-  };
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
   for (int st = 0; st < NSLOT - 1 && st < nst; ++st) issue(st);
-  if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (NSLOT - 1 < nst) issue(NSLOT - 1);
-  read_frags(0, S0{});
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  auto step = [&](int st, auto cur_c, auto nxt_c) {
-    constexpr int C = decltype(cur_c)::value;
-    if (st + 1 < nst) {
-      if (st + 2 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // everyone's pieces of stage st + 1; slot st % 3 is free
-      if (st + NSLOT < nst) issue(st + NSLOT);
-      read_frags(st + 1, nxt_c);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + NSLOT - 1 < nst) issue(st + NSLOT - 1);
+    const uint32_t sb = lds0 + (uint32_t)((st % NSLOT) * SLOT * 2);
+    short8_t af[2][MT], bf[2][NT];
+    auto reads = [&](auto kk) {
+      constexpr int H = decltype(kk)::value;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+      for (int i = 0; i < MT; ++i) af[H][i] = tr8<WA, H * 32 * WA * 16>(sb + aoff[i]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[H][j] = tr8<WB, H * 32 * WB * 16>(sb + boff[j]);
+    };
+    reads(std::integral_constant<int, 0>{});
+    reads(std::integral_constant<int, 1>{});
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (h == 0) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");  // h0 landed (counter max 15 < 16 h1 reads)
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[C][h][i], bf[C][h][j], acc[i][j]);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  for (int st = 0; st < nst; st += 2) {
-    step(st, S0{}, S1{});
-    if (st + 1 < nst) step(st + 1, S1{}, S0{});
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[h][i], bf[h][j], acc[i][j]);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

@@ -1,4 +1,4 @@
-# Round-4 GPU pass v: software-pipelined fragment reads in the 256 x 128 conv GEMM and weight-gradient kernels (ResNet-18).
+# Round-4 GPU pass v: software-pipelined fragment reads in the 256 x 128 conv GEMM (ResNet-18).
 set -u
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
@@ -15,7 +15,7 @@ for v in new old; do
   if [ $v = new ]; then unset SL_KERNELS_SO; else export SL_KERNELS_SO=$OLD; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$v -o run -- python3 bench.py --model resnet18 --ingest device --steps 10 --warmup 3 > $O/prof_$v.log 2>&1 || exit 1
   python scripts/rocprof_summary.py $O/prof_$v/run_results.db > $O/kernels_$v.csv
-  echo "== $v"; grep -E "conv_gemm_big|conv_wgrad_big" $O/kernels_$v.csv | cut -c1-120 || true
+  echo "== $v"; grep -E "conv_gemm_big" $O/kernels_$v.csv | cut -c1-120 || true
   rm -rf $O/prof_$v
 done
 unset SL_KERNELS_SO
