@@ -595,55 +595,32 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 
   const int nk = g.K / BK;  // uniform taps: K is a multiple of 64
   for (int kt = 0; kt < NSLOT - 1 && kt < nk; ++kt) issue(kt);
-  // Software-pipelined: stage kt + 1's fragments are read under stage kt's MFMAs (two register
-  // sets), so no step waits for its own LDS reads; stage kt's slot is refilled with stage kt + 3
-  // right after step kt's barrier (every wave holds stage kt in registers by then).  Two stages
-  // stay in flight from HBM, as before.
-  short8_t af[2][2][MT], bf[2][2][NT];  // [register set][k half][fragment]
-  auto read_frags = [&](int kt, auto set_c) {
-    constexpr int S = decltype(set_c)::value;
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's pieces of stage kt have landed once only stage kt + 1's (if issued) remain
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's have; every wave is done reading slot (kt - 1) % 3
+    if (kt + NSLOT - 1 < nk) issue(kt + NSLOT - 1);
     const uint32_t sb = lds0 + (uint32_t)((kt % NSLOT) * SLOT * 2);
+    short8_t af[2][MT], bf[2][NT];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
-      for (int i = 0; i < MT; ++i) af[S][h][i] = ds_b128(sb + aoff[i][h]);
+      for (int i = 0; i < MT; ++i) af[h][i] = ds_b128(sb + aoff[i][h]);
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bf[S][h][j] = ds_b128(sb + boff[j][h]);
+      for (int j = 0; j < NT; ++j) bf[h][j] = ds_b128(sb + boff[j][h]);
     }
-  };
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  // stage 0 has landed once only stage 1's pieces (if issued) remain; then stage 2 into slot 2
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (NSLOT - 1 < nk) issue(NSLOT - 1);
-  read_frags(0, S0{});
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  auto step = [&](int kt, auto cur_c, auto nxt_c) {
-    constexpr int C = decltype(cur_c)::value;
-    if (kt + 1 < nk) {
-      // stage kt + 1 has landed once only stage kt + 2's pieces (if issued) remain
-      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // everyone's pieces; every wave is done reading slot kt % 3
-      if (kt + NSLOT < nk) issue(kt + NSLOT);
-      read_frags(kt + 1, nxt_c);
-    }
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (h == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[C][h][i], bf[C][h][j], acc[i][j]);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(kt, S0{}, S1{});
-    if (kt + 1 < nk) step(kt + 1, S1{}, S0{});
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[h][i], bf[h][j], acc[i][j]);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
