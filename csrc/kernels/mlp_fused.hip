@@ -1447,10 +1447,7 @@ __device__ __forceinline__ float group_sum(float v) {
 // floats map back to 4 consecutive parameters of one weight row (or, in the small region, to
 // single parameters).  w / mom / the shadows are then touched in a scattered order, but they
 // are 1 MB arrays that stay in L2.
-// db_tot: the db1 totals of dW1 rows row0 .. row0 + 15 (LDS, summed once per workgroup by
-// mlp_sgd_kernel), or null to sum them per unit from the slab.
-__device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part, const float* db_tot = nullptr,
-                                          int row0 = 0) {
+__device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
   const long off = u * 4;
   if (off >= TL_SMALL + W3P_LD) return;
   long pe = -1;       // this thread's parameter (part < 4)
@@ -1493,7 +1490,7 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part, co
       const int sidx = s0 + k * SGD_TPG;
       v[k] = sidx < ns ? *reinterpret_cast<const float4*>(src + (long)sidx * a.slab_stride)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
-      d[k] = (w1row >= 0 && !db_tot && sidx < ns) ? dbs[(long)sidx * a.slab_stride] : 0.f;
+      d[k] = (w1row >= 0 && sidx < ns) ? dbs[(long)sidx * a.slab_stride] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
@@ -1505,7 +1502,7 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part, co
   for (int j = 0; j < 4; ++j) g[j] = group_sum(g[j]);
   float gme = g[part & 3];
   if (w1row >= 0) {
-    db = db_tot ? db_tot[w1row - row0] : group_sum(db);
+    db = group_sum(db);
     gme = a.xa * gme + a.xb * db;
   }
   if (!mine) return;
@@ -1524,42 +1521,7 @@ __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int part = (int)(t % SGD_TPG);
   if (a.slab && a.mode != 0) {
-    // This workgroup's SGD_NT / 4 units are one 512-float block of a slab tile, so its dW1 units
-    // share 16 rows m0 .. m0 + 15: their db1 totals (28 slab loads each) are summed once here,
-    // in the per-unit order ((p0 + p1) + (p2 + p3), bit-identical), instead of by every unit
-    // (the db loads were most of the kernel's load instructions).
-    static_assert(SGD_TPG == 4 && SGD_NT / SGD_TPG * 4 == 512 && TL_TILE % 512 == 0, "one 512-float block per workgroup");
-    __shared__ float s_dbp[SGD_TPG][16];
-    __shared__ float s_db[16];
-    const long off0 = (long)blockIdx.x * (SGD_NT / SGD_TPG) * 4;
-    const bool w1 = off0 < TL_W2;
-    int m0 = 0;
-    if (w1) {
-      const int within = (int)(off0 % TL_TILE);
-      m0 = ((within >> 12) & 1) * 128 + ((within & 4095) >> 9) * 16;
-      const int tid = threadIdx.x;
-      if (tid < 16 * SGD_TPG) {
-        const int r = tid & 15, p = tid >> 4;
-        const float* dbs = a.slab + TL_SMALL + W3P_DB1 + m0 + r;
-        float db = 0.f;
-        constexpr int U = 8;
-        for (int s0 = p; s0 < a.slices; s0 += SGD_TPG * U) {
-          float d[U];
-#pragma unroll
-          for (int k = 0; k < U; ++k) {
-            const int sidx = s0 + k * SGD_TPG;
-            d[k] = sidx < a.slices ? dbs[(long)sidx * a.slab_stride] : 0.f;
-          }
-#pragma unroll
-          for (int k = 0; k < U; ++k) db += d[k];
-        }
-        s_dbp[p][r] = db;
-      }
-      __syncthreads();
-      if (tid < 16) s_db[tid] = (s_dbp[0][tid] + s_dbp[1][tid]) + (s_dbp[2][tid] + s_dbp[3][tid]);
-      __syncthreads();
-    }
-    sgd_tiled(a, t / SGD_TPG, part, w1 ? s_db : nullptr, m0);
+    sgd_tiled(a, t / SGD_TPG, part);
     return;
   }
   const long p0 = (t / SGD_TPG) * 4;
