@@ -103,7 +103,9 @@ struct HaloArgs {
 constexpr int DEFER_BYTES = TPIX * HC * 2;
 __device__ __forceinline__ int cs_swz(int p, int chunk) { return p * (HC * 2) + ((chunk ^ ((p >> 1) & 7)) << 4); }
 
-template <int CIN, bool DEFER>
+// BNB: the data gradient with the fused BN-backward epilogue (a.bn); else a forward, which may
+// apply BN-on-load (a.bin).  Separate instances, so neither carries the other's registers.
+template <int CIN, bool DEFER, bool BNB>
 __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   using L = Lay<CIN>;
   constexpr int HL = (L::HALO_CHUNKS + NTF - 1) / NTF;  // halo chunks per thread
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   }
 
   // BN-on-load: a thread's halo chunks are all channel chunk (tid & 7) (NTF % 8 == 0)
-  const bool bni = CIN == 64 && a.bin.stats != nullptr;
+  const bool bni = CIN == 64 && !BNB && a.bin.stats != nullptr;
   float isc[8], ish[8];
   if (bni) {
     bn_coef8(a.bin, HC, (tid & 7) * 8, a.bin_count, a.bin_eps, isc, ish);
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
 
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
   // fused BN backward: the epilogue's 8-channel chunk of a thread is (tid & 7) in every tile
-  const bool bnb = a.bn.x != nullptr;
+  const bool bnb = BNB && a.bn.x != nullptr;
   BnbAcc bacc;
   float msc[8], msh[8];
   if (bnb) bnb_init(a.bn, HC, (tid & 7) * 8, bacc, msc, msh);
@@ -423,10 +425,19 @@ static int conv3x3_launch(const uint16_t* src, const uint16_t* w, int cin, int f
     a.bin = *bin;
   }
   const int grid = a.tiles < g_num_cus ? a.tiles : g_num_cus;  // persistent: one workgroup per CU (130 KB LDS)
+  // the plain forward defers its output stores into the next tile's k-loop; deferring the data
+  // gradient's epilogue (residual add + fused BN backward) too measured 152.8 vs 138 us per call
+  // and the stem's needs its 3-step k-loop re-planned (profiles/r04_haloepi)
   const bool defer = SL_HALO_DEFER && cin == 64 && !flip && !add && !bn;
-  if (defer) hipLaunchKernelGGL((conv3x3_kernel<64, true>), dim3(grid), dim3(NTF), 0, stream, a);
-  else if (cin == 64) hipLaunchKernelGGL((conv3x3_kernel<64, false>), dim3(grid), dim3(NTF), 0, stream, a);
-  else hipLaunchKernelGGL((conv3x3_kernel<8, false>), dim3(grid), dim3(NTF), 0, stream, a);
+  if (cin == 8) {
+    if (bn) return -2;
+    hipLaunchKernelGGL((conv3x3_kernel<8, false, false>), dim3(grid), dim3(NTF), 0, stream, a);
+  } else if (bn) {
+    hipLaunchKernelGGL((conv3x3_kernel<64, false, true>), dim3(grid), dim3(NTF), 0, stream, a);
+  } else {
+    if (defer) hipLaunchKernelGGL((conv3x3_kernel<64, true, false>), dim3(grid), dim3(NTF), 0, stream, a);
+    else hipLaunchKernelGGL((conv3x3_kernel<64, false, false>), dim3(grid), dim3(NTF), 0, stream, a);
+  }
   SL_CHECK_LAUNCH();
   return 0;
 }
