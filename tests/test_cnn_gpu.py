@@ -99,6 +99,7 @@ def test_conv_fwd_dgrad_wgrad(case):
 # tile parity classes, 64/128-tile parity classes, 128-tile stride 1
 BNB_CASES = [
     (4, 32, 64, 64, 3, 1),
+    (160, 32, 64, 64, 3, 1),        # direct kernel, several tiles per persistent workgroup
     (256, 16, 128, 128, 3, 1),
     (1024, 16, 128, 256, 3, 2),
     (1024, 32, 64, 128, 3, 2),      # stage-2 shape with the fused BN-backward epilogue
@@ -668,7 +669,9 @@ def test_resnet_bucketed_allreduce_hooks_cover_gradient_before_update():
     assert torch.allclose(b.params, expect, rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("n,h,cin", [(3, 32, 64), (5, 8, 64), (3, 32, 8), (2, 16, 8)])
+# (160, 32, *): 640 tiles, several per persistent workgroup -- the deferred-store k-loop path and
+# the stats kept across tiles (the smaller cases run one tile per workgroup)
+@pytest.mark.parametrize("n,h,cin", [(3, 32, 64), (5, 8, 64), (3, 32, 8), (2, 16, 8), (160, 32, 64), (160, 32, 8)])
 def test_direct_3x3_c64_matches_reference_and_gemm_path(n, h, cin):
     """conv3x3_halo.hip (3x3/s1/p1 -> 64 channels, width 32; 64 input channels fwd + dgrad,
     8 = the padded CIFAR stem fwd) vs fp32 torch and vs the implicit GEMM."""
