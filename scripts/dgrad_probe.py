@@ -3,7 +3,7 @@
 the four parity-class launches of ``conv_dgrad``) in its variants, to split its cost between the
 GEMM and the fused epilogue work: plain, + residual add, + fused BN backward (mask + sums), + both.
 
-    python scripts/dgrad_probe.py [--batch 1024] [--reps 30]
+    python scripts/dgrad_probe.py [--batch 1024] [--reps 30] [--h 32 --cin 64 | --h 16 --cin 128 | --h 8 --cin 256]
 
 Prints one JSON line of microseconds per call (CUDA events around ``reps`` back-to-back calls).
 """
@@ -24,11 +24,14 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--h", type=int, default=32, help="input (dx) height = width: 32 / 16 / 8 = stage 2 / 3 / 4")
+    ap.add_argument("--cin", type=int, default=64)
     args = ap.parse_args()
     from serverless_learn_amd.ops import cnn as K
 
     dev = "cuda"
-    n, h, c, cout = args.batch, 32, 64, 128
+    n, h, c = args.batch, args.h, args.cin
+    cout = 2 * c
     oh = h // 2
     g = torch.Generator(device="cpu").manual_seed(0)
     dy = torch.randn(n, oh, oh, cout, generator=g).to(dev, torch.bfloat16)
