@@ -387,10 +387,18 @@ def main(argv=None) -> int:
         tr.step()
     run = getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
     if use_graph:
-        if mlp:
-            tr.capture(warmup=0, unroll=args.unroll)
-        else:
-            tr.capture(warmup=0)
+        try:
+            if mlp:
+                tr.capture(warmup=0, unroll=args.unroll)
+            else:
+                tr.capture(warmup=0)
+        except RuntimeError as e:
+            if not (graph_pg and world > 1 and xg is None):
+                raise
+            # a multi-rank RCCL capture the runtime refuses: the timed steps run eagerly
+            print(f"RCCL step capture failed, stepping eagerly: {e}", file=sys.stderr)
+            tr.drop_graphs()
+            graph_pg = use_graph = False
 
     def upload_graph():
         # upload the K-step executable graph before the clock starts, as any graph about to be
@@ -425,12 +433,18 @@ def main(argv=None) -> int:
         upload_graph()
 
     def pg_mode():
+        nonlocal graph_pg
         tr.enable_xgmi(None)
         tr.allreduce = lambda g: dist.all_reduce(g)
         tr.step()  # eager first: anything lazily set up by the collective happens outside capture
         if use_graph and graph_pg:
-            tr.capture(warmup=0, unroll=args.unroll)
-            return getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
+            try:
+                tr.capture(warmup=0, unroll=args.unroll)
+                return getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
+            except RuntimeError as e:  # a multi-rank RCCL capture the runtime refuses: eager steps
+                print(f"RCCL step capture failed, stepping eagerly: {e}", file=sys.stderr)
+                tr.drop_graphs()
+                graph_pg = False
         return lambda n: [tr.step() for _ in range(n)]
 
     autotune = None

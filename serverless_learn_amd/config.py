@@ -62,6 +62,7 @@ class Config:
     log_every: int = 50
     graph: bool = True                 # capture the fused step in a hipGraph when possible
     graph_steps: int = 16              # steps per graph replay chunk (error / metrics checks between chunks)
+    graph_collectives: bool = False    # also capture a multi-rank RCCL group's collectives into the step graph
     dp_backend: str = "auto"           # auto (nccl = RCCL on GPU, gloo on CPU) | nccl | gloo
     dp_timeout_s: float = 30.0         # collective / rendezvous timeout of the data-parallel group
     xgmi: bool = True                  # MLP on a GPU group: all-reduce through IPC-mapped buffers over xGMI

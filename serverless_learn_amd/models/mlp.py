@@ -490,6 +490,16 @@ class FusedMLPTrainer:
             self.allreduce(self.grad)
             self._sgd(2, from_grad=True, grad_out=False)
 
+    def drop_graphs(self) -> None:
+        """Release every captured step graph after the device has finished with them.  A
+        graph may hold a communicator's kernels: the runtime calls this before it re-forms or
+        tears down the group, so no replay is in flight when the old
+        communicator goes away and the k-step graph is not left alive holding it."""
+        if self.graph is not None or getattr(self, "graph_unrolled", None) is not None:
+            torch.cuda.synchronize(self.device)
+        self.graph = None
+        self.graph_unrolled = None
+
     def capture(self, warmup: int = 2, unroll: int = 1) -> None:
         """Capture one step into a hipGraph (kernels only, or kernels + RCCL);
         ``unroll > 1`` also captures a k-step graph used by :meth:`steps`."""

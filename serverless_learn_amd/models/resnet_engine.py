@@ -418,6 +418,13 @@ class FusedResNetTrainer:
             return
         self._step_eager()
 
+    def drop_graphs(self) -> None:
+        """Release the captured step graph once the device is done with it (called by the
+        runtime before it re-forms or tears down a group whose collectives the graph holds)."""
+        if self.graph is not None:
+            torch.cuda.synchronize(self.device)
+        self.graph = None
+
     def capture(self, warmup: int = 2) -> None:
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))

@@ -64,6 +64,14 @@ def resolve_device(spec: str) -> torch.device:
     return torch.device(spec)
 
 
+class ChunkBroken(GroupBroken):
+    """A collective failed part-way through a step chunk: ``done`` steps completed first."""
+
+    def __init__(self, done: int, cause: BaseException):
+        super().__init__(str(cause))
+        self.done, self.cause = done, cause
+
+
 class Worker:
     def __init__(self, addr: str, config: Config | None = None):
         self.cfg = config or Config.from_env()
@@ -416,8 +424,7 @@ class Worker:
         self._drop_xgmi(healthy=not self.group.broken)
         self._ensure_resumed(v.get("resume_file", 0))
         with trace.span("regroup", epoch=v["epoch"], world=v["world"]):
-            if self.trainer is not None:
-                self.trainer.graph = None  # a captured step may embed the old communicator
+            self._drop_graphs()  # a captured step may embed the old communicator
             ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"])
             if not ok:
                 self._stop.wait(0.2)
@@ -527,6 +534,19 @@ class Worker:
                 t.graph = None  # the captured step must be re-captured with (or without) the collective
             self._set_world(max(1, self.group.world) if self.group.active and self.group.world > 1 else 1)
 
+    def _drop_graphs(self) -> None:
+        """Free the trainer's captured step graphs (the one-step and the k-step graph) after
+        the device has drained them: they may hold the current communicator's kernels, so
+        this runs before every re-form and teardown of the group."""
+        t = self.trainer
+        if t is None:
+            return
+        with self.train_lock:
+            if hasattr(t, "drop_graphs"):
+                t.drop_graphs()
+            elif hasattr(t, "graph"):
+                t.graph = None
+
     def _bucket_hook(self, view: torch.Tensor):
         return self.group.allreduce_async(view)
 
@@ -547,13 +567,18 @@ class Worker:
         (the MLP hook, the ResNet bucket all-reduces and their stream waits) is device work
         ordered on the stream and is captured into the step graph with the kernels
         (tests/test_rccl_gpu.py).  A gloo group's collectives run on the host: eager steps.
+        Capturing a multi-rank RCCL group's collectives is opt-in (``graph_collectives`` /
+        ``SL_GRAPH_COLLECTIVES=1``): a peer failing inside a replayed graph does not reach
+        ``_bucket_wait``'s GroupBroken path, so the elastic runtime steps eagerly by default.
         The captured graph embeds the communicator, so every re-form drops it
-        (``_maybe_regroup``)."""
+        (``_maybe_regroup`` -> ``_drop_graphs``)."""
         t = self.trainer
         if not (self.cfg.graph and self.device.type == "cuda" and hasattr(t, "capture")):
             return False
         host_hooks = t.allreduce is not None or getattr(t, "bucket_hook", None) is not None
-        return not host_hooks or (self.group.active and self.group.backend == "nccl")
+        if not host_hooks:
+            return True
+        return self.group.active and self.group.backend == "nccl" and self.cfg.graph_collectives
 
     def _run_chunk(self, n: int) -> int:
         """Run exactly ``min(n, graph_steps)`` steps and return that count.
@@ -564,31 +589,50 @@ class Worker:
         lock-step group must cut their chunks at the same steps even when a shard landing
         on one of them mid-run dropped only its graph.  Graph mode replays a
         captured k-step graph; a chunk that finds no graph runs one eager step (sizes the
-        lazily-grown workspaces), captures, and replays the rest of the chunk."""
+        lazily-grown workspaces), captures, and replays the rest of the chunk.
+
+        Eager steps take ``train_lock`` one step at a time, so ReceiveFile / ExchangeUpdates /
+        gossip wait for at most one step, not a whole chunk.  A collective failing
+        at step j of a chunk raises :class:`ChunkBroken` carrying the j steps that did complete,
+        so the step counter stays equal to the trainer's real state."""
         t = self.trainer
         k = max(1, self.cfg.graph_steps)
         n = max(1, min(n, k))
-        if not self._use_graph():
-            for _ in range(n):
-                t.step()
-            return n
         done = 0
-        if t.graph is None:
-            t.step()
-            done = 1
-            if hasattr(t, "steps"):
-                t.capture(warmup=0, unroll=k)
-            else:
-                t.capture(warmup=0)
-            self.log.info("graph_captured", steps=k, step=self.step + 1)
-        if n > done:
-            if hasattr(t, "steps"):
-                t.steps(n - done)
-            else:
-                for _ in range(n - done):
+        try:
+            if not self._use_graph():
+                while done < n:
+                    with self.train_lock:
+                        t.step()
+                    done += 1
+                return n
+            with self.train_lock:
+                if t.graph is None:
                     t.step()
-        self.graph_chunks += 1
-        return n
+                    done = 1
+                    if hasattr(t, "steps"):
+                        t.capture(warmup=0, unroll=k)
+                    else:
+                        t.capture(warmup=0)
+                    self.log.info("graph_captured", steps=k, step=self.step + 1)
+                if n > done:
+                    if hasattr(t, "steps"):
+                        t.steps(n - done)
+                    else:
+                        while done < n:
+                            t.step()
+                            done += 1
+                    done = n
+            self.graph_chunks += 1
+            return n
+        except GroupBroken as e:
+            raise ChunkBroken(done, e) from e
+
+    def _account_steps(self, prev: int, ran: int) -> None:
+        self.step = prev + ran
+        self.samples += ran * self.trainer.batch
+        for s_i in range(prev + 1, self.step + 1):
+            self.fault.on_step(s_i)
 
     def _group_metrics_update(self, dt: float, samples: int, st) -> None:
         """N3: all-reduce [loss_sum, correct_sum, samples] (SUM) and the interval (MAX) over
@@ -682,16 +726,14 @@ class Worker:
                     want = min(want, every - self.step % every)
             prev = self.step
             try:
-                with self.train_lock, trace.span("steps", step=self.step):
+                with trace.span("steps", step=self.step):
                     ran = self._run_chunk(want)
-            except GroupBroken as e:
-                self.log.warn("collective_failed", error=str(e), epoch=self.group.epoch)
+            except ChunkBroken as e:
+                self._account_steps(prev, e.done)
+                self.log.warn("collective_failed", error=str(e.cause), epoch=self.group.epoch, steps_done=e.done)
                 continue
-            self.step += ran
-            self.samples += ran * self.trainer.batch
+            self._account_steps(prev, ran)
             self.state = "training"
-            for s_i in range(prev + 1, self.step + 1):
-                self.fault.on_step(s_i)
             lockstep = self.cfg.sync == "allreduce" and self.group.active and self.group.world > 1
             agreement = None
             if lockstep:
@@ -831,6 +873,7 @@ class Worker:
         for t in self._threads:
             t.join(timeout=10)
         self._drop_xgmi(healthy=False)
+        self._drop_graphs()
         self.group.teardown()
         if self.server:
             self.server.stop()

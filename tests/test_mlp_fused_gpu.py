@@ -177,19 +177,23 @@ def test_training_is_deterministic_at_full_batch(bm, rows_bm):
     assert s1.loss < 1.5, s1.loss
 
 
-def test_gradients_match_reference_at_headline_config():
+def test_gradients_match_reference_at_headline_config(monkeypatch):
     """The bench configuration itself (B = 65,536, the default rows tile and the default split-K
     slice count of the weight gradient) against the fp32 autograd reference and the
     bf16-rounding emulation, with the bounds of test_gradients_match_reference.  The
     references run in fp32 on the GPU (torch matmul, no reduced-precision path on gfx950)."""
     from serverless_learn_amd.ops import _native
 
+    # the shipped defaults, whatever the environment or an earlier test forced
+    monkeypatch.delenv("SL_MLP_ROWS_BM", raising=False)
+    monkeypatch.delenv("SL_MLP_WG_SLICES", raising=False)
+    _native.call("sl_mlp_set_rows_bm", 0)
     B = 65536
     x, y = _data(B, seed=13)
     flat = M.init_params(6)
     tr = M.FusedMLPTrainer(batch=B, flat=flat, momentum=0.0)
-    assert tr.slices == M.default_slices(B)
-    assert _native.lib().sl_mlp_rows_bm(B) in (64, 128, 256)
+    assert tr.slices == M.default_slices(B) == 28
+    assert _native.lib().sl_mlp_rows_bm(B) == 128
     tr.load_shard(x, y)
     g = tr.compute_grads().double().cpu()
     torch.cuda.synchronize()

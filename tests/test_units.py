@@ -475,6 +475,98 @@ def test_worker_chunk_length_does_not_depend_on_graph_state(monkeypatch):
     assert w._run_chunk(40) == 16 and w._run_chunk(3) == 3
 
 
+def test_worker_chunk_failure_counts_completed_steps_and_releases_lock(monkeypatch):
+    """an eager chunk takes train_lock per step (so RPC handlers wait at
+    most one step), and a collective failing at step k of a chunk raises ChunkBroken carrying
+    the k steps that completed, which the loop adds to the step / sample counters."""
+    from serverless_learn_amd.parallel.dp import GroupBroken
+    from serverless_learn_amd.runtime.local_cluster import fast_config
+    from serverless_learn_amd.runtime.worker import ChunkBroken, Worker
+
+    import threading
+
+    w = Worker("127.0.0.1:0", fast_config(graph_steps=16))
+
+    def lock_free() -> bool:  # train_lock is an RLock: probe it from another thread
+        out = []
+
+        def probe():
+            got = w.train_lock.acquire(blocking=False)
+            if got:
+                w.train_lock.release()
+            out.append(got)
+        th = threading.Thread(target=probe)
+        th.start()
+        th.join()
+        return out[0]
+
+    class Failing(_FakeGraphTrainer):
+        batch = 8
+
+        def __init__(self, fail_at):
+            super().__init__()
+            self.fail_at = fail_at
+
+        def step(self):
+            assert not lock_free()  # the worker holds train_lock during a step
+            if self.ran == self.fail_at:
+                raise GroupBroken("peer died")
+            self.ran += 1
+
+    w.trainer = Failing(fail_at=5)
+    monkeypatch.setattr(w, "_use_graph", lambda: False)
+    with pytest.raises(ChunkBroken) as ei:
+        w._run_chunk(10)
+    assert ei.value.done == 5 and isinstance(ei.value, GroupBroken)
+    assert lock_free()  # released after the failure
+    w.step, w.samples = 100, 0
+    w._account_steps(100, ei.value.done)
+    assert (w.step, w.samples) == (105, 5 * 8)
+    # graph mode: a failure in the capture step reports 0 completed steps
+    t = Failing(fail_at=0)
+    w.trainer = t
+    monkeypatch.setattr(w, "_use_graph", lambda: True)
+    with pytest.raises(ChunkBroken) as ei:
+        w._run_chunk(10)
+    assert ei.value.done == 0
+
+
+def test_worker_drops_graphs_before_regroup_and_multirank_rccl_capture_is_opt_in():
+    """a re-form frees BOTH captured graphs through drop_graphs (which
+    syncs the device first); capturing a multi-rank RCCL group's collectives is opt-in."""
+    from serverless_learn_amd.runtime.local_cluster import fast_config
+    from serverless_learn_amd.runtime.worker import Worker
+
+    w = Worker("127.0.0.1:0", fast_config())
+
+    class T(_FakeGraphTrainer):
+        dropped = 0
+
+        def drop_graphs(self):
+            T.dropped += 1
+            self.graph = None
+            self.graph_unrolled = None
+
+    t = T()
+    t.graph, t.graph_unrolled = object(), object()
+    w.trainer = t
+    w._drop_graphs()
+    assert T.dropped == 1 and t.graph is None and t.graph_unrolled is None
+
+    class G:
+        active, backend, world = True, "nccl", 2
+
+    w.group = G()
+    w.device = torch.device("cuda", 0)
+    t.allreduce = lambda g: None
+    assert w._use_graph() is False
+    w.cfg.graph_collectives = True
+    assert w._use_graph() is True
+    t.allreduce = None
+    w.cfg.graph_collectives = False
+    assert w._use_graph() is True  # no host-side collective in the step: always captured
+
+
 def test_allreduce_async_enqueue_failure_is_group_broken():
     """an enqueue that fails on an aborted communicator must surface as
     GroupBroken (which the training loop handles by re-forming) on both the sum path and
