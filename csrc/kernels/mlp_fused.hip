@@ -941,6 +941,7 @@ struct WgArgs {
   int n_batches, batch;
   const float* w3p;      // [n_w3p][W3P_LD] partial rows of the rows kernel
   int n_w3p;
+  unsigned long long* stamps;  // diagnostics: [logical workgroup][4] start / main loop done / end / XCC (nullptr in production)
 };
 
 constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages in flight
@@ -1055,6 +1056,10 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int st0 = s * A.steps_per_slice;
   const int nst = min(A.steps_per_slice, A.total_steps - st0);
   const bool u8b = pi == 0;
+  if (A.stamps && tid == 0) {
+    A.stamps[logical * 4 + 0] = __builtin_amdgcn_s_memtime();
+    A.stamps[logical * 4 + 3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
   // n-blocks of this wave that hold real columns (dW1's last tile: 16 columns)
   const int nvalid = __builtin_amdgcn_readfirstlane(min(WG_NJ, max(0, (P.n_real - n0 - wn * 16 * WG_NJ + 15) / 16)));
 
@@ -1289,6 +1294,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     mainloop_pipe(F_{}, I4{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (A.stamps && tid == 0) A.stamps[logical * 4 + 1] = __builtin_amdgcn_s_memtime();
 
   // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
   // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
@@ -1364,6 +1370,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       if (q < W3P_N || q >= W3P_DB1) srow[TL_SMALL + q] = tv[j];
     }
   }
+  if (A.stamps && tid == 0) A.stamps[logical * 4 + 2] = __builtin_amdgcn_s_memtime();
 }
 
 // ---------------------------------------------------------------------------
@@ -1598,6 +1605,11 @@ int sl_mlp_set_stamps(unsigned long long* p) {
   g_stamps = p;
   return 0;
 }
+static unsigned long long* g_wg_stamps = nullptr;
+int sl_mlp_set_wg_stamps(unsigned long long* p) {  // weight-gradient stamps (diagnostics)
+  g_wg_stamps = p;
+  return 0;
+}
 static int g_rows_bm = 0;  // 0: auto; 64 / 128 force a tile height (benchmarks, tests)
 int sl_mlp_set_rows_bm(int bm) {
   g_rows_bm = bm;
@@ -1679,6 +1691,7 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
   a.slab = slab; a.slab_stride = slab_stride;
   a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
   a.w3p = w3p; a.n_w3p = n_w3p;
+  a.stamps = g_wg_stamps;
   if (((uintptr_t)x & 15) != 0 || ((uintptr_t)w3p & 15) != 0) return -2;  // 16-B pieces / float4 reads
   hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(base * slices), dim3(WG_NT), 0, stream, a);
   SL_CHECK_LAUNCH();

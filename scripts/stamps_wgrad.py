@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-stage s_memtime stamps of the MLP weight gradient's dW2 loop (slice 0, first
-dW2 tile, wave 0).  Prints the median cycles of each phase over the steady-state stages."""
+"""Diagnostic: per-workgroup s_memtime stamps of the MLP weight gradient (mlp_wgrad_kernel):
+main-loop and total cycles per tile kind (dW1 tiles 0-6, dW2 tiles 7-8) for a steady-state step."""
 import os
 import sys
 
@@ -17,19 +17,19 @@ tr = FusedMLPTrainer(batch=B, device="cuda:0")
 tr.load_shard(torch.from_numpy(x), torch.from_numpy(y))
 for _ in range(5):
     tr.step()
-st = torch.zeros(64 * 8, dtype=torch.int64, device="cuda:0")
+nwg = 9 * tr.slices
+st = torch.zeros(nwg * 4, dtype=torch.int64, device="cuda:0")
 _native.call("sl_mlp_set_wg_stamps", st.data_ptr())
 tr._lc = None; tr._lkey = None
 for _ in range(3):
     tr.step()
 torch.cuda.synchronize()
 _native.call("sl_mlp_set_wg_stamps", None)
-s = st.view(64, 8)[:, :6].cpu().double()
-n = int((s[:, 0] != 0).sum())
-s = s[:n]
-names = ["wait+barrier+issue", "k0 MFMAs+reads", "mid lgkm wait", "k1 MFMAs+recompute", "finish+end wait"]
-d = s[:, 1:] - s[:, :-1]
-step = s[1:, 0] - s[:-1, 0]
-print(f"stages {n}  median cycles per stage {float(step[2:-2].median()):.0f}")
-for i, nm in enumerate(names):
-    print(f"  {nm:22s} median {float(d[2:-2, i].median()):7.0f}  mean {float(d[2:-2, i].mean()):7.0f}")
+s = st.view(nwg, 4).cpu().double()
+t0 = s[:, 0].min()
+tile = torch.arange(nwg) % 9
+for name, sel in (("dW1 tiles 0-5", tile < 6), ("dW1 tile 6 (16 cols)", tile == 6), ("dW2 tiles", tile >= 7)):
+    v = s[sel]
+    print(f"{name:22s} n={int(sel.sum()):3d}  main loop median {float((v[:, 1] - v[:, 0]).median()):8.0f}  "
+          f"max {float((v[:, 1] - v[:, 0]).max()):8.0f}  total median {float((v[:, 2] - v[:, 0]).median()):8.0f}  "
+          f"start spread {float((v[:, 0] - t0).max()):6.0f}  end max {float((v[:, 2] - t0).max()):8.0f}")
