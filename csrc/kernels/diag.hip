@@ -28,3 +28,23 @@ extern "C" int sl_clock_probe(unsigned long long* buf, unsigned* cnt, int cap, h
   SL_CHECK_LAUNCH();
   return 0;
 }
+
+// A stand-in for a collective's footprint on one GPU (profiles/r05_overlap): nwg workgroups
+// stream a read-modify-write over a bucket-sized scratch buffer (a = (a + b) / 2), as a ring
+// all-reduce's few channel workgroups stream their bucket through LDS-free copies.  Launched
+// from a gradient-bucket hook on a side stream, its kernel-trace start / end times show
+// whether anything runs beside the backward's one-workgroup-per-CU convolution kernels.
+__global__ __launch_bounds__(256) void comm_proxy_kernel(float4* a, const float4* b, long n4) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 x = a[i], y = b[i];
+    a[i] = make_float4(0.5f * (x.x + y.x), 0.5f * (x.y + y.y), 0.5f * (x.z + y.z), 0.5f * (x.w + y.w));
+  }
+}
+
+extern "C" int sl_comm_proxy(float* a, const float* b, long n, int nwg, hipStream_t stream) {
+  if (!a || !b || n <= 0 || (n & 3) || nwg <= 0 || (((uintptr_t)a | (uintptr_t)b) & 15)) return -1;
+  hipLaunchKernelGGL(comm_proxy_kernel, dim3(nwg), dim3(256), 0, stream, reinterpret_cast<float4*>(a),
+                     reinterpret_cast<const float4*>(b), n / 4);
+  SL_CHECK_LAUNCH();
+  return 0;
+}

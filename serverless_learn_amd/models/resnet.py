@@ -343,3 +343,59 @@ class CPUResNetTrainer:
             loss = F.cross_entropy(logits, y, reduction="mean")
             acc = (logits.argmax(1) == y).float().mean()
         return StepStats(float(loss), float(acc), int(y.numel()))
+
+
+def block_backward_errors(tr, g: torch.Tensor) -> list:
+    """Per residual block of a FusedResNetTrainer that just ran ``compute_grads`` (returned
+    ``g``): the block's backward (BN x2-3, conv data / weight gradients, ReLU masks, skip)
+    against fp32 autograd of that block run on the engine's OWN stored input, bf16 weights and
+    incoming gradient.  Returns [(conv name, "dx" | "dW", relative L2 error)].  Used by the GPU
+    numerics tests at B = 32 (tests/test_cnn_gpu.py) and at the bench batch
+    (scripts/resnet_block_check.py)."""
+    spec = tr.spec
+    w32 = tr.shadow.float()
+    f32 = lambda t: t.float().permute(0, 3, 1, 2).detach()  # noqa: E731
+    nhwc = lambda t: t.permute(0, 2, 3, 1)  # noqa: E731
+
+    def rel(a, b):
+        a, b = a.detach().float(), b.detach().float()
+        return float((a - b).norm() / (b.norm() + 1e-12))
+
+    def bn(xx, b):
+        return F.batch_norm(xx, None, None, tr.params[b.g_off:b.g_off + b.c], tr.params[b.b_off:b.b_off + b.c],
+                            training=True)
+
+    if tr.stem_onload:  # block 0's input a0 is rebuilt on load from c0, never stored: materialise it
+        tr.K.bn_apply(tr.c0, tr.bn[spec.stem_bn.name].coef, tr.a0, relu=True)
+        torch.cuda.synchronize()
+    nb = len(tr.blocks)
+    if tr.fuse_bn_bwd:
+        # the data gradient of block i+1 lands in block i's dz, already ReLU-masked by block
+        # i's output (the block input of i+1); block 0's in its own dx, masked by the stem's ReLU
+        dys = [tr.blocks[i]["dz"] for i in range(nb - 1)] + [tr.dfeat_in]
+        dxs = [tr.blocks[0]["dx"]] + [tr.blocks[i - 1]["dz"] for i in range(1, nb)]
+    else:
+        dys = [tr.blocks[i + 1]["dx"] for i in range(nb - 1)] + [tr.dfeat_in]
+        dxs = [st["dx"] for st in tr.blocks]
+    errs = []
+    for st, blk, dy, dx in zip(tr.blocks, spec.blocks, dys, dxs):
+        ws = {c.name: conv_weight_nchw(w32, c).clone().requires_grad_(True)
+              for c in (blk.conv1, blk.conv2, blk.down) if c is not None}
+        xin = f32(st["x"]).requires_grad_(True)
+        conv = lambda t, c: F.conv2d(t, ws[c.name], stride=c.stride, padding=c.pad)  # noqa: E731
+        o = F.relu(bn(conv(xin, blk.conv1), blk.bn1))
+        o = bn(conv(o, blk.conv2), blk.bn2)
+        sc = bn(conv(xin, blk.down), blk.dbn) if blk.down is not None else xin
+        out = F.relu(o + sc)
+        out.backward(f32(dy))
+        # compared where the block input is positive: the fused path stores the input
+        # gradient masked by the ReLU that produced the input
+        keep = (st["x"] > 0).float()
+        errs.append((blk.conv1.name, "dx", rel(dx.float() * keep, nhwc(xin.grad) * keep)))
+        for c in (blk.conv1, blk.conv2, blk.down):
+            if c is None:
+                continue
+            mine = g[c.off:c.off + c.numel].view(c.cout, c.k, c.k, c.cin).permute(0, 3, 1, 2)
+            errs.append((c.name, "dW", rel(mine, ws[c.name].grad)))
+        del ws, xin, o, sc, out, keep
+    return errs

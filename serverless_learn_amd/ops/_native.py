@@ -44,6 +44,7 @@ _SIGS: dict[str, list] = {
     "sl_mlp_reduce_xgmi": [P, I, L, F, F, P, P, P, P],
     "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, L, P],
     "sl_clock_probe": [P, P, I, P],
+    "sl_comm_proxy": [P, P, L, I, P],
 }
 _RESTYPE = {"sl_mlp_param_count": ctypes.c_long, "sl_mlp_slab_stride": ctypes.c_long}
 
