@@ -40,6 +40,17 @@
 using namespace sl;
 
 namespace {
+// Cache policy of the stores that hand a kernel's outputs to the next launch (H1/dH2/dH1 rows,
+// w3p partials, weight-gradient slabs): 16 = sc1 (write-through), 0 = default write-back.
+#ifndef SL_STORE_AUX
+#define SL_STORE_AUX 0
+#endif
+constexpr int OUT_AUX = SL_STORE_AUX;
+__device__ __forceinline__ void st_out(float* p, float v) {
+  if constexpr (OUT_AUX & 16) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 constexpr int D_IN = 784;   // input features (28x28)
 constexpr int D_INP = 832;  // layer-1 K padded to 13 chunks of 64 (w1h row stride)
 constexpr int NCHUNK = D_INP / 64;
@@ -68,7 +79,28 @@ constexpr int W3P_N = NC * HID + NC;
 constexpr int W3P_DB1 = 2576;
 constexpr int W3P_DB2 = W3P_DB1 + HID;
 constexpr int W3P_LD = W3P_DB2 + HID;  // 3088
+// Layer 1 runs on the EXACT pixels as fp16 1024 + u (one v_perm per two pixels; the
+// normalise-and-round-to-bf16 of every pixel was ~1,100 VALU per wave, a fifth of the rows
+// kernel's) against fp16 W1.  Then acc = sum_k W1[f][k] (1024 + u_k) = 1024 R[f] + W1 u, and
+//   Z1 = W1 (xa u + xb) + b1 = xa acc + (xb - 1024 xa) R[f] + b1,
+// R[f] = sum_k fp16(W1[f][k]).  R is kept exactly, as 64-bit fixed point (fp16 values are
+// multiples of 2^-24 below 2^16): per row, R1_BLK partial sums of 32 columns, written by the
+// SGD launch that writes the fp16 shadow (or by mlp_w1_rowsum_kernel after the flat update
+// paths) and summed by every rows workgroup in its prologue into its layer-1 bias.
+constexpr int R1_BLK = (D_IN + 31) / 32;  // 25 column blocks per W1 row
+constexpr double R1_FIX = 16777216.0;     // 2^24
 }  // namespace
+
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+__device__ __forceinline__ long long h_fix(uint16_t h) {
+  return (long long)((double)(float)__builtin_bit_cast(_Float16, h) * R1_FIX);
+}
+// 8 u8 -> 8 fp16 of (1024 + u), exact: fp16 steps by 1 over [1024, 2048), so the bits are
+// 0x6400 | u and one v_perm_b32 builds two of them.
+typedef uint32_t uint2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t u8x2_f16_biased(uint32_t w, int hi) {
+  return __builtin_amdgcn_perm(0x64646464u, w, hi ? 0x04030402u : 0x04010400u);
+}
 
 // Weights are kept in MFMA B-fragment order: for a [N][K] matrix (K
 // contiguous), block (nt, ks) holds W[16 nt + r][32 ks + 8 g + j] at lane
@@ -91,6 +123,10 @@ struct FragSrc {
   }
 };
 
+// diagnostics: per-workgroup row-kernel stamps [0..9 phases (s_memtime) | 10 HW_ID | 11 XCC_ID |
+// 12..15 sub-phases | 16, 17 start / end s_memrealtime (100 MHz): their ratio gives the shader clock]
+constexpr int ROW_STAMPS = 20;
+
 struct MlpRowArgs {
   const uint8_t* x;
   const uint8_t* y;
@@ -98,6 +134,7 @@ struct MlpRowArgs {
   int n_batches, batch;
   const uint16_t *w1h, *w2h, *w3h, *w2th, *w3th;
   const float *b1, *b2, *b3;
+  const long long* r1p;                // [256][R1_BLK] fixed-point partial row sums of fp16 W1
   float xa, xb, grad_scale;
   float dh1_scale;                     // dH1 goes to HBM as fp16 of dH1 * dh1_scale (a power of two)
   uint16_t* h1;                        // row-major [batch][256]
@@ -250,7 +287,7 @@ __device__ __forceinline__ void copy_part_buf(const uint16_t* src, int ld, __amd
     const short8_t v = *reinterpret_cast<const short8_t*>(src + rr * ld + c);
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), dst, (r * gld + c) * 2,
-                                           (it * PER + i) * RPP * gld * 2, 0);
+                                           (it * PER + i) * RPP * gld * 2, OUT_AUX);
   }
 }
 
@@ -282,9 +319,9 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   constexpr int REGB = BM * HS_LD;   // one LDS region (elements)
   static_assert(3 * BM * XC_LD <= REGB, "X ring must fit region 0");
   constexpr int SMEM = ONE ? REGB + BM * DZL + BM * 32 : 2 * REGB + BM * DZL;
-  // BIG: b1 | b2 staged in LDS (fp32, as uint16 pairs); b3 is read from global so that two
-  // workgroups fit one CU's 160 KB
-  constexpr int BSZ = BIG ? 2 * HID * 2 : 0;
+  // b1' (layer-1 bias with the row-sum correction) | BIG: b2, staged in LDS (fp32, as uint16
+  // pairs); b3 is read from global so that two workgroups fit one CU's 160 KB
+  constexpr int BSZ = BIG ? 2 * HID * 2 : HID * 2;
   static_assert((SMEM + BSZ) * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM + BSZ];
   float* BS = reinterpret_cast<float*>(smem + SMEM);
@@ -306,9 +343,10 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   constexpr int rw = 0;          // ... and rows (all of the tile's)
   floatx4_t acc[MF][NF];
   auto stamp = [&](int i) {
-    if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
+    if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * ROW_STAMPS + i] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
+  if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * ROW_STAMPS + 16] = __builtin_amdgcn_s_memrealtime();
   // Workgroup barrier.  The 128-row tile waits only for LDS
   // traffic: __syncthreads() also drains every outstanding global store (vmcnt(0)), and
   // with all CUs storing the same activation at once that drain stalled the CU for
@@ -322,21 +360,22 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       __syncthreads();
     }
   };
-  if constexpr (BIG) {  // the epilogues read the biases from LDS (published by layer 1's barriers)
-    if (tid < 2 * HID / 4)
-      reinterpret_cast<float4*>(BS)[tid] = reinterpret_cast<const float4*>(tid < HID / 4 ? a.b1 : a.b2 - HID)[tid];
+  {  // the epilogues read the biases from LDS (published by layer 1's barriers)
+    static_assert(NT == HID, "one thread per layer-1 feature");
+    if (BIG && tid < HID / 4) reinterpret_cast<float4*>(BS + HID)[tid] = reinterpret_cast<const float4*>(a.b2)[tid];
+    long long rs = 0;
+#pragma unroll
+    for (int j = 0; j < R1_BLK; ++j) rs += a.r1p[tid * R1_BLK + j];
+    BS[tid] = a.b1[tid] + (a.xb - 1024.f * a.xa) * (float)((double)rs * (1.0 / R1_FIX));
   }
   if (a.stamps && tid == 0) {  // placement: HW_ID (CU / SH / SE) and XCC_ID
-    a.stamps[(long)blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
-    a.stamps[(long)blockIdx.x * 16 + 11] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    a.stamps[(long)blockIdx.x * ROW_STAMPS + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    a.stamps[(long)blockIdx.x * ROW_STAMPS + 11] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
 
   // ---- layer 1: H1 = relu(X W1^T + b1), K = 832 streamed in 13 chunks of 64 ----
   const int xrow = tid >> 2, xcol = (tid & 3) * 16;
   const uint8_t* xg = a.x + (srow0 + xrow) * D_IN + xcol;
-  // Normalisation coefficients as lane values (VGPRs): with both in SGPRs,
-  // ROCm 7.2 emits a packed FMA that breaks the gfx950 constant-bus limit.
-  const float nxa = a.xa + 0.f * (float)lane, nxb = a.xb + 0.f * (float)lane;
   // X row pass p covers rows xrow + p * NT / 4
   auto xload = [&](int c, int p = 0) -> uint4 {
     return (c * 64 + xcol < D_IN) ? *reinterpret_cast<const uint4*>(xg + (long)p * (NT / 4) * D_IN + c * 64)
@@ -485,8 +524,11 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       for (int h = 0; h < 2; ++h) {
         short8_t lo = zero8(), hi = zero8();
         if (c * 128 + xc2 + 16 * h < D_IN) {
-          lo = u8x8_to_bf16(make_uint2(xw[c][h].x, xw[c][h].y), nxa, nxb);
-          hi = u8x8_to_bf16(make_uint2(xw[c][h].z, xw[c][h].w), nxa, nxb);
+          typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+          lo = __builtin_bit_cast(short8_t, u32x4_t{u8x2_f16_biased(xw[c][h].x, 0), u8x2_f16_biased(xw[c][h].x, 1),
+                                                    u8x2_f16_biased(xw[c][h].y, 0), u8x2_f16_biased(xw[c][h].y, 1)});
+          hi = __builtin_bit_cast(short8_t, u32x4_t{u8x2_f16_biased(xw[c][h].z, 0), u8x2_f16_biased(xw[c][h].z, 1),
+                                                    u8x2_f16_biased(xw[c][h].w, 0), u8x2_f16_biased(xw[c][h].w, 1)});
         }
         *reinterpret_cast<short8_t*>(d + 16 * h) = lo;
         *reinterpret_cast<short8_t*>(d + 16 * h + 8) = hi;
@@ -504,7 +546,12 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
 #pragma unroll
           for (int m = 0; m < MF; ++m) af[m] = lds8(ab + (rw + m * 16) * XLD);
         },
-        mfma_ab,
+        [&](const short8_t (&af)[MF], const short8_t (&b)[NF]) {  // fp16 pixels x fp16 W1
+#pragma unroll
+          for (int m = 0; m < MF; ++m)
+#pragma unroll
+            for (int n = 0; n < NF; ++n) acc[m][n] = mfma16h(b[n], af[m], acc[m][n]);
+        },
         [&](int st) {
           // chunk c+1 converted after the first k-step of chunk c, published by this
           // barrier before step 4c+3 prefetches it; its slot held chunk c-2
@@ -539,9 +586,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       auto xcvt = [&](const uint4& v, uint32_t (&pk)[8]) {
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int m = 0; m < 8; ++m)
-          pk[m] = pack2((float)((w[m >> 1] >> ((m & 1) * 16)) & 0xffu) * nxa + nxb,
-                        (float)((w[m >> 1] >> ((m & 1) * 16 + 8)) & 0xffu) * nxa + nxb);
+        for (int m = 0; m < 8; ++m) pk[m] = u8x2_f16_biased(w[m >> 1], m & 1);
       };
       // prologue: chunks 0, 1 converted, 2, 3 waiting in registers
 #pragma unroll
@@ -580,10 +625,9 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
         for (int m = 0; m < MF; ++m) {
           if (m + 2 < MF) af[m + 2] = lds8(ab + (rw + (m + 2) * 16) * 64);
 #pragma unroll
-          for (int n = 0; n < NF; ++n) acc[m][n] = mfma16(r[st % RING][n], af[m], acc[m][n]);
+          for (int n = 0; n < NF; ++n) acc[m][n] = mfma16h(r[st % RING][n], af[m], acc[m][n]);
           if (conv)  // piece m of the pass: bytes 2m, 2m+1
-            pk[m] = pack2((float)((xw[m >> 1] >> ((m & 1) * 16)) & 0xffu) * nxa + nxb,
-                          (float)((xw[m >> 1] >> ((m & 1) * 16 + 8)) & 0xffu) * nxa + nxb);
+            pk[m] = u8x2_f16_biased(xw[m >> 1], m & 1);
           __builtin_amdgcn_sched_barrier(0);
         }
         if (conv) xput(cc, q & 1, pk);
@@ -604,7 +648,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   stamp(1);
   if constexpr (ONE) bar();  // the X ring shares the image H1 goes to
   stamp(12);
-  relu_out(BIG ? BS : a.b1, R1, true);
+  relu_out(BS, R1, true, a.xa);
   stamp(13);
   }
   bar();
@@ -721,8 +765,8 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       const int c = 4 * lg + r;
       if (c < NC) {
 #pragma unroll
-        for (int n = 0; n < NF; ++n) part[c * HID + cw + n * 16 + lr] = d3[n][r];
-        if (wng == 0 && lr == 0) part[NC * HID + c] = db3[r];
+        for (int n = 0; n < NF; ++n) st_out(&part[c * HID + cw + n * 16 + lr], d3[n][r]);
+        if (wng == 0 && lr == 0) st_out(&part[NC * HID + c], db3[r]);
       }
     }
   }
@@ -770,7 +814,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       if (lg == 0) {
         float* part = a.w3p + (long)((row0 + rh) >> 6) * W3P_LD + off;
 #pragma unroll
-        for (int n = 0; n < NF; ++n) part[cw + n * 16 + lr] = cs[n][0];
+        for (int n = 0; n < NF; ++n) st_out(&part[cw + n * 16 + lr], cs[n][0]);
       }
     }
   };
@@ -827,7 +871,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       for (int n = 0; n < NF; ++n) {
         typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
         const u32x2_t h = {hv[n][0], hv[n][1]};
-        __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, OUT_AUX);
       }
     }
     // Transpose-reduce of the 32 column partials over the 16 rows of a DPP row: each
@@ -861,7 +905,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       const int n = 2 * (lr & 1) + ((lr >> 1) & 1), r = 2 * ((lr >> 2) & 1) + ((lr >> 3) & 1);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        a.w3p[(long)((row0 + rw + 64 * j) >> 6) * W3P_LD + W3P_DB1 + cw + n * 16 + 4 * lg + r] = red[j];
+        st_out(&a.w3p[(long)((row0 + rw + 64 * j) >> 6) * W3P_LD + W3P_DB1 + cw + n * 16 + 4 * lg + r], red[j]);
     }
     stamp(15);
   } else {
@@ -877,6 +921,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
     col_sums(R1, W3P_DB1);
   }
   stamp(9);
+  if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * ROW_STAMPS + 17] = __builtin_amdgcn_s_memrealtime();
 }
 
 
@@ -931,6 +976,10 @@ struct WgProblem {
   long w_off, b_off;  // flat destinations of dW ([256][n_real]) and db
   int bias_part;      // this problem's db partial inside the rows kernel's partial rows
 };
+// weight-gradient stamps per logical workgroup: start / main loop done / end (s_memtime), XCC_ID,
+// start / end s_memrealtime (100 MHz)
+constexpr int WG_STAMPS = 6;
+
 struct WgArgs {
   WgProblem p[2];  // dW1 (u8 X), dW2 (H1); dW3 comes from the rows kernel's partials
   int total_tiles;
@@ -941,7 +990,7 @@ struct WgArgs {
   int n_batches, batch;
   const float* w3p;      // [n_w3p][W3P_LD] partial rows of the rows kernel
   int n_w3p;
-  unsigned long long* stamps;  // diagnostics: [logical workgroup][4] start / main loop done / end / XCC (nullptr in production)
+  unsigned long long* stamps;  // diagnostics: [logical workgroup][WG_STAMPS] (nullptr in production)
 };
 
 constexpr int WG_NSLOT = 3;               // LDS ring slots (144 KB): two stages in flight
@@ -992,7 +1041,6 @@ __device__ __forceinline__ short4_t ds_tr16_off(uint32_t a) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
   return r;
 }
-typedef uint32_t uint2v_t __attribute__((ext_vector_type(2)));
 template <int OFF>
 __device__ __forceinline__ uint2v_t ds_tr8_off(uint32_t a) {
   uint2v_t r;
@@ -1057,8 +1105,9 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int nst = min(A.steps_per_slice, A.total_steps - st0);
   const bool u8b = pi == 0;
   if (A.stamps && tid == 0) {
-    A.stamps[logical * 4 + 0] = __builtin_amdgcn_s_memtime();
-    A.stamps[logical * 4 + 3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    A.stamps[logical * WG_STAMPS + 0] = __builtin_amdgcn_s_memtime();
+    A.stamps[logical * WG_STAMPS + 4] = __builtin_amdgcn_s_memrealtime();
+    A.stamps[logical * WG_STAMPS + 3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
   // n-blocks of this wave that hold real columns (dW1's last tile: 16 columns)
   const int nvalid = __builtin_amdgcn_readfirstlane(min(WG_NJ, max(0, (P.n_real - n0 - wn * 16 * WG_NJ + 15) / 16)));
@@ -1294,7 +1343,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     mainloop_pipe(F_{}, I4{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (A.stamps && tid == 0) A.stamps[logical * 4 + 1] = __builtin_amdgcn_s_memtime();
+  if (A.stamps && tid == 0) A.stamps[logical * WG_STAMPS + 1] = __builtin_amdgcn_s_memtime();
 
   // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
   // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
@@ -1333,7 +1382,7 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
       if (n < P.n_real) {
         typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4w, acc[i][j]), out_rs, out_voff,
-                                               (i * WG_NJ + j) * 1024, 0);
+                                               (i * WG_NJ + j) * 1024, OUT_AUX);
       }
     }
 
@@ -1367,10 +1416,13 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q = 4 * (c0 + col) + j;
-      if (q < W3P_N || q >= W3P_DB1) srow[TL_SMALL + q] = tv[j];
+      if (q < W3P_N || q >= W3P_DB1) st_out(&srow[TL_SMALL + q], tv[j]);
     }
   }
-  if (A.stamps && tid == 0) A.stamps[logical * 4 + 2] = __builtin_amdgcn_s_memtime();
+  if (A.stamps && tid == 0) {
+    A.stamps[logical * WG_STAMPS + 2] = __builtin_amdgcn_s_memtime();
+    A.stamps[logical * WG_STAMPS + 5] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1396,13 +1448,18 @@ struct SgdArgs {
   // picked by the parity of the step in flight (xgmi.h)
   float* grad_out_alt;
   const unsigned* ar_ctl;
+  long long* r1p;  // fixed-point partial row sums of the fp16 W1 shadow (tiled mode 2 writes them)
 };
 
-__device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) {
+// Shadow copies of the new weight: fp16 for W1 (layer 1 multiplies exact fp16 pixels), bf16
+// for the rest.  Returns the fixed-point value of the fp16 W1 weight (0 for other parameters).
+__device__ __forceinline__ long long write_shadow(const SgdArgs& a, long p, float w) {
   const uint16_t h = f2bf(w);
   if (p < P_B1) {
     const int o = (int)(p / D_IN), i = (int)(p - (long)o * D_IN);
-    a.w1h[frag_off(o, i, KS1)] = h;                     // layer 1: B[k=i][n=o]
+    const uint16_t h16 = f2h(w);
+    a.w1h[frag_off(o, i, KS1)] = h16;                   // layer 1: B[k=i][n=o]
+    return h_fix(h16);
   } else if (p >= P_W2 && p < P_B2) {
     const int q = (int)(p - P_W2), o = q >> 8, i = q & 255;
     a.w2h[frag_off(o, i, KS2)] = h;                     // layer 2: B[k=i][n=o]
@@ -1412,6 +1469,7 @@ __device__ __forceinline__ void write_shadow(const SgdArgs& a, long p, float w) 
     a.w3h[frag_off(c, i, KS2)] = h;                     // layer 3: B[k=i][n=c]
     a.w3th[frag_off(i, c, 1)] = h;                      // dH2 = dZ W3: B[k=c][n=i]
   }
+  return 0;
 }
 
 // Four threads per float4 group of parameters: each sums every fourth slab
@@ -1423,10 +1481,11 @@ __device__ __forceinline__ float quad_sum(float v) {
   return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
 }
 
-// w0 / m0: the parameter and momentum, loaded by the caller ahead of the slab sums
-__device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p, float gme, float w0, float m0) {
+// w0 / m0: the parameter and momentum, loaded by the caller ahead of the slab sums.  Returns
+// write_shadow's fixed-point fp16 W1 value.
+__device__ __forceinline__ long long sgd_apply(const SgdArgs& a, float* gout, long p, float gme, float w0, float m0) {
   if (gout) gout[p] = gme;
-  if (a.mode == 1) return;
+  if (a.mode == 1) return 0;
   float w = w0;
   float d = gme + a.wd * w;
   if (a.mom) {
@@ -1435,7 +1494,7 @@ __device__ __forceinline__ void sgd_apply(const SgdArgs& a, float* gout, long p,
   }
   w -= a.lr * d;
   a.w[p] = w;
-  write_shadow(a, p, w);
+  return write_shadow(a, p, w);
 }
 
 // SGD_TPG threads per float4 group of parameters: each sums every SGD_TPG-th
@@ -1454,9 +1513,10 @@ __device__ __forceinline__ float group_sum(float v) {
 // floats map back to 4 consecutive parameters of one weight row (or, in the small region, to
 // single parameters).  w / mom / the shadows are then touched in a scattered order, but they
 // are 1 MB arrays that stay in L2.
-__device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
+// Returns this thread's fixed-point fp16 W1 weight (mode 2), for the row sums.
+__device__ __forceinline__ long long sgd_tiled(const SgdArgs& a, long u, int part) {
   const long off = u * 4;
-  if (off >= TL_SMALL + W3P_LD) return;
+  if (off >= TL_SMALL + W3P_LD) return 0;
   long pe = -1;       // this thread's parameter (part < 4)
   int w1row = -1;     // dW1 row (output feature) of the unit, for the db1 term
   if (off < TL_SMALL) {
@@ -1467,7 +1527,7 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
     const int nn = (wave >> 1) * 32 + (ins & 1) * 16 + (lane >> 4) * 4;
     if (tile < 7) {
       const int n = tile * 128 + nn;
-      if (n >= D_IN) return;  // dW1's last tile: 16 real columns (whole group exits together)
+      if (n >= D_IN) return 0;  // dW1's last tile: 16 real columns (whole group exits together)
       pe = P_W1 + (long)m * D_IN + n + part;
       w1row = m;
     } else {
@@ -1512,10 +1572,10 @@ __device__ __forceinline__ void sgd_tiled(const SgdArgs& a, long u, int part) {
     db = group_sum(db);
     gme = a.xa * gme + a.xb * db;
   }
-  if (!mine) return;
+  if (!mine) return 0;
   float* gout = a.grad_out;
   if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
-  sgd_apply(a, gout, pe, gme, w0, m0);
+  return sgd_apply(a, gout, pe, gme, w0, m0);
 }
 
 // float4 units a launch of mlp_sgd_kernel walks: the slab's (tiled) or the parameters'
@@ -1528,7 +1588,24 @@ __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int part = (int)(t % SGD_TPG);
   if (a.slab && a.mode != 0) {
-    sgd_tiled(a, t / SGD_TPG, part);
+    const long long fx = sgd_tiled(a, t / SGD_TPG, part);
+    // W1 row sums: a workgroup of the tiled walk covers 128 units of one tile = 16 rows
+    // (m_base + lane & 15) x 32 columns (one R1 block) of W1; its 512 fixed-point values are
+    // summed per row in LDS (integer: order-free, exact) and written as that block's partials
+    constexpr int UPW = SGD_NT / SGD_TPG;  // units per workgroup
+    static_assert(UPW == 128 && TL_TILE / 4 % UPW == 0, "one (wave, instruction-pair) block per workgroup");
+    const int tile = (int)(blockIdx.x / (TL_TILE / 4 / UPW)), wgt = (int)(blockIdx.x % (TL_TILE / 4 / UPW));
+    const int wv = wgt / 8, mbase = (wv & 1) * 128 + (wgt % 8) * 16, blk = tile * 4 + (wv >> 1);
+    if (a.mode == 2 && a.r1p && tile < 7 && blk < R1_BLK) {  // uniform per workgroup
+      __shared__ unsigned long long rs[16];
+      if (threadIdx.x < 16) rs[threadIdx.x] = 0ull;
+      __syncthreads();
+      const long uu = t / SGD_TPG;
+      const int lane_u = (int)(((uu * 4) % TL_TILE & 255) >> 2);
+      if (fx) atomicAdd(&rs[lane_u & 15], (unsigned long long)fx);
+      __syncthreads();
+      if (threadIdx.x < 16) a.r1p[(mbase + threadIdx.x) * R1_BLK + blk] = (long long)rs[threadIdx.x];
+    }
     return;
   }
   const long p0 = (t / SGD_TPG) * 4;
@@ -1550,6 +1627,17 @@ __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
   float* gout = a.grad_out;
   if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
   sgd_apply(a, gout, p, gme, w0, m0);
+}
+
+// Fixed-point partial row sums of the fp16 W1 shadow, for the update paths that do not walk the
+// tiled slab (shadow refresh, the all-reduced gradient's update, the xGMI update): one
+// workgroup per row, one lane per 32-column block.
+__global__ __launch_bounds__(64) void mlp_w1_rowsum_kernel(const uint16_t* w1h, long long* r1p) {
+  const int m = blockIdx.x, j = threadIdx.x;
+  if (j >= R1_BLK) return;
+  long long s = 0;
+  for (int c = 32 * j; c < 32 * j + 32 && c < D_IN; ++c) s += h_fix(w1h[frag_off(m, c, KS1)]);
+  r1p[m * R1_BLK + j] = s;
 }
 
 // Multi-GPU update (after sl_xgmi_barrier): one thread per 4 parameters sums the W ranks' reduced gradients
@@ -1632,12 +1720,14 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
                 const uint16_t* w3th, const float* params, float xa, float xb,
                 float grad_scale, float dh1_scale,
                 uint16_t* h1, float* w3p, uint16_t* dh2, uint16_t* dh1,
-                float* loss, float* correct, float* logits, int train, hipStream_t stream) {
+                float* loss, float* correct, float* logits, int train, const long long* r1p, hipStream_t stream) {
   if (batch <= 0 || batch % BM != 0) return -1;
   MlpRowArgs a;
   a.x = x; a.y = y; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
   a.w1h = w1h; a.w2h = w2h; a.w3h = w3h; a.w2th = w2th; a.w3th = w3th;
   a.b1 = params + P_B1; a.b2 = params + P_B2; a.b3 = params + P_B3;
+  a.r1p = r1p;
+  if (!r1p) return -3;  // layer 1 needs the W1 row sums (written with the fp16 shadow)
   a.xa = xa; a.xb = xb; a.grad_scale = grad_scale; a.dh1_scale = dh1_scale;
   a.h1 = h1; a.w3p = w3p; a.dh2 = dh2; a.dh1 = dh1;
   a.loss = loss; a.correct = correct; a.logits = logits;
@@ -1701,20 +1791,25 @@ int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, 
 int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_stride, const float* grad_in,
                float* grad_out, float lr, float mu, float wd, float xa, float xb, int mode, uint16_t* w1h,
                uint16_t* w2h,
-               uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, hipStream_t stream) {
+               uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, long long* r1p, hipStream_t stream) {
   SgdArgs a = {};
   a.w = w; a.mom = mom; a.slab = slab; a.slices = slices; a.slab_stride = slab_stride;
   a.grad_in = grad_in; a.grad_out = grad_out; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = mode;
   a.xa = xa; a.xb = xb;
   a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
-  a.grad_out_alt = nullptr; a.ar_ctl = nullptr;
+  a.grad_out_alt = nullptr; a.ar_ctl = nullptr; a.r1p = r1p;
   if (mode != 0 && !slab && !grad_in) return -1;
+  if (mode != 1 && !r1p) return -1;  // every shadow write refreshes the W1 row sums
   if (mode == 1 && !grad_out) return -1;
   if (slab && (slab_stride & 3)) return -1;
   if (slab && slab_stride < TL_STRIDE) return -1;
   const long groups = sgd_units(slab != nullptr && mode != 0);
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
+  if (mode == 0 || (mode == 2 && !slab)) {  // flat paths: the row sums from the new shadow
+    hipLaunchKernelGGL(mlp_w1_rowsum_kernel, dim3(HID), dim3(64), 0, stream, w1h, r1p);
+    SL_CHECK_LAUNCH();
+  }
   return 0;
 }
 
@@ -1734,7 +1829,9 @@ int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa
 
 int sl_mlp_sgd_xgmi(float* w, float* mom, float lr, float mu, float wd, uint16_t* w1h, uint16_t* w2h,
                     uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, char* const* bases,
-                    unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, hipStream_t stream) {
+                    unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, long long* r1p,
+                    hipStream_t stream) {
+  if (!r1p) return -1;
   if (!w || !bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return -1;
   if (slot_bytes < ((P_N + 3) / 4) * 16 || (slot_bytes & 255)) return -1;
   if (chunk4 < 0 || (chunk4 > 0 && (chunk4 * world * 16 < slot_bytes || (chunk4 & 63)))) return -1;
@@ -1746,6 +1843,8 @@ int sl_mlp_sgd_xgmi(float* w, float* mom, float lr, float mu, float wd, uint16_t
   x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world; x.chunk4 = chunk4;
   const long groups = (P_N + 3) / 4;
   hipLaunchKernelGGL(mlp_sgd_xgmi_kernel, dim3((groups + 255) / 256), dim3(256), 0, stream, a, x);
+  SL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(mlp_w1_rowsum_kernel, dim3(HID), dim3(64), 0, stream, w1h, r1p);
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -20,29 +20,39 @@ tr.load_shard(torch.from_numpy(x), torch.from_numpy(y))
 for _ in range(5):
     tr.step()
 bm = _native.lib().sl_mlp_rows_bm(B)
-st = torch.zeros(B // bm * 16, dtype=torch.int64, device="cuda:0")
+S = 20  # stamps per workgroup (ROW_STAMPS in mlp_fused.hip)
+st = torch.zeros(B // bm * S, dtype=torch.int64, device="cuda:0")
 _native.call("sl_mlp_set_stamps", st.data_ptr())
 tr._lc = None; tr._lkey = None
 tr.step()
 torch.cuda.synchronize()
 _native.call("sl_mlp_set_stamps", None)
-s = st.view(-1, 16)[:, :10].cpu().double()
+s = st.view(-1, S)[:, :10].cpu().double()
 d = s[:, 1:] - s[:, :-1]
 names = ["layer1", "relu1", "layer2+h1", "relu2", "layer3+ce", "dW3 part+dH2", "mask2", "dH1+dh2", "mask1+dh1"]
 print(f"B={B} BM={bm} workgroups={s.shape[0]}  total median cycles {float((s[:, 9] - s[:, 0]).median()):.0f}")
 for i, n in enumerate(names):
     print(f"  {n:14s} median {float(d[:, i].median()):8.0f}  mean {float(d[:, i].mean()):8.0f}")
-e = st.view(-1, 16).cpu().double()
+e = st.view(-1, S).cpu().double()
 if bool((e[:, 12] != 0).all()):
     for n, (i, j) in {"l1 end wait": (1, 12), "relu1 body": (12, 13), "relu1 barrier": (13, 2),
                       "l2 end wait": (3, 14), "relu2+w3 tail": (14, 4), "dH1 mask+bar": (8, 15),
                       "dh1 out+colsum": (15, 9)}.items():
         print(f"  {n:14s} median {float((e[:, j] - e[:, i]).median()):8.0f}")
-t0 = s[:, 0] - s[:, 0].min()
-print(f"  start spread: median {float(t0.median()):.0f} max {float(t0.max()):.0f}")
+tot = (s[:, 9] - s[:, 0])
+print(f"  WG total cycles: p50 {float(tot.median()):.0f}  p90 {float(tot.quantile(0.9)):.0f}  max {float(tot.max()):.0f}")
+# s_memtime counts shader clocks per XCC; s_memrealtime is a 100 MHz clock shared by the whole chip
+rt0, rt1 = e[:, 16], e[:, 17]
+if bool((rt1 > rt0).all()):
+    mhz = tot / ((rt1 - rt0) / 100.0)
+    print(f"  shader clock MHz over each WG: median {float(mhz.median()):.0f}  min {float(mhz.min()):.0f}  "
+          f"max {float(mhz.max()):.0f}")
+    print(f"  start spread (100 MHz clock): median {float((rt0 - rt0.min()).median()) * 10:.0f} ns  "
+          f"max {float((rt0 - rt0.min()).max()) * 10:.0f} ns;  first start -> last end "
+          f"{float(rt1.max() - rt0.min()) * 10:.0f} ns")
 
 # ---- occupancy reconstruction from placement ids ----
-raw = st.view(-1, 16).cpu()
+raw = st.view(-1, S).cpu()
 hw = raw[:, 10].numpy().astype("int64")
 xcc = raw[:, 11].numpy().astype("int64") & 0xF
 cu = (hw >> 8) & 0xF

@@ -18,14 +18,14 @@ tr.load_shard(torch.from_numpy(x), torch.from_numpy(y))
 for _ in range(5):
     tr.step()
 nwg = 9 * tr.slices
-st = torch.zeros(nwg * 4, dtype=torch.int64, device="cuda:0")
+st = torch.zeros(nwg * 6, dtype=torch.int64, device="cuda:0")
 _native.call("sl_mlp_set_wg_stamps", st.data_ptr())
 tr._lc = None; tr._lkey = None
 for _ in range(3):
     tr.step()
 torch.cuda.synchronize()
 _native.call("sl_mlp_set_wg_stamps", None)
-s = st.view(nwg, 4).cpu().double()
+s = st.view(nwg, 6).cpu().double()
 t0 = s[:, 0].min()
 tile = torch.arange(nwg) % 9
 for name, sel in (("dW1 tiles 0-5", tile < 6), ("dW1 tile 6 (16 cols)", tile == 6), ("dW2 tiles", tile >= 7)):
@@ -33,3 +33,7 @@ for name, sel in (("dW1 tiles 0-5", tile < 6), ("dW1 tile 6 (16 cols)", tile == 
     print(f"{name:22s} n={int(sel.sum()):3d}  main loop median {float((v[:, 1] - v[:, 0]).median()):8.0f}  "
           f"max {float((v[:, 1] - v[:, 0]).max()):8.0f}  total median {float((v[:, 2] - v[:, 0]).median()):8.0f}  "
           f"start spread {float((v[:, 0] - t0).max()):6.0f}  end max {float((v[:, 2] - t0).max()):8.0f}")
+r = s[:, 5] - s[:, 4]
+mhz = (s[:, 2] - s[:, 0]) / (r / 100.0)
+print(f"shader clock MHz over each WG: median {float(mhz.median()):.0f}  min {float(mhz.min()):.0f}  "
+      f"max {float(mhz.max()):.0f};  first start -> last end {float(s[:, 5].max() - s[:, 4].min()) * 10:.0f} ns")

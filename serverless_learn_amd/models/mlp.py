@@ -36,6 +36,7 @@ MNIST_MEAN = 0.1307
 MNIST_STD = 0.3081
 BLOCK_ROWS = 64  # batch rows per workgroup of the fused row kernel
 W3P_LD = 3088  # row stride of the rows kernel's partial rows: [dW3 | db3 | pad | db1 | db2]
+R1_BLK = 25  # 32-column blocks per W1 row: fixed-point partial row sums of the fp16 shadow
 
 LAYOUT = (
     ("fc1.weight", (HIDDEN, D_IN)),
@@ -128,10 +129,12 @@ def reference_grads_bf16(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor
     r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
     v = {k: t.detach().float() for k, t in views(flat).items()}
     a, b = norm_coeffs()
-    xn = r(x_u8.reshape(-1, D_IN).float() * a + b)
-    w1 = r(v["fc1.weight"])
+    # layer 1: exact normalised pixels against the fp16 W1 shadow (the kernel multiplies the
+    # exact pixels 1024 + u and removes the offset with W1's exact row sums)
+    xe = x_u8.reshape(-1, D_IN).float() * a + b
+    w1 = v["fc1.weight"].to(torch.float16).float()
     w2, w3 = r(v["fc2.weight"]), r(v["fc3.weight"])
-    p1 = xn @ w1.t() + v["fc1.bias"]
+    p1 = xe @ w1.t() + v["fc1.bias"]
     h1 = r(torch.relu(p1))
     p2 = h1 @ w2.t() + v["fc2.bias"]
     h2 = r(torch.relu(p2))
@@ -141,9 +144,8 @@ def reference_grads_bf16(flat: torch.Tensor, x_u8: torch.Tensor, y: torch.Tensor
     dz = r((torch.softmax(z, 1) - F.one_hot(yl, CLASSES).float()) * grad_scale)
     dh2 = r((dz @ w3) * (p2 > 0).float())
     dh1 = r((dh2 @ w2) * (p1 > 0).float())
-    # dW1 uses the exact normalised input: the weight-gradient kernel multiplies the raw
-    # u8 pixels (exact in bf16) and applies the normalisation affinely afterwards
-    xe = x_u8.reshape(-1, D_IN).float() * a + b
+    # dW1 uses the exact normalised input too: the weight-gradient kernel multiplies the raw
+    # u8 pixels (exact in fp16) and applies the normalisation affinely afterwards
     g = torch.cat([(dh1.t() @ xe).reshape(-1), dh1.sum(0), (dh2.t() @ h1).reshape(-1), dh2.sum(0),
                    (dz.t() @ h2).reshape(-1), dz.sum(0)])
     correct = (z.argmax(1) == yl).float().sum()
@@ -288,7 +290,10 @@ class FusedMLPTrainer:
         self.params[:n].copy_(init.to(dev))
         self.mom = torch.zeros_like(self.params) if momentum > 0 else None
         bf = torch.bfloat16
-        self.w1h = torch.zeros(HIDDEN, D_IN_PAD, dtype=bf, device=dev)
+        # W1's shadow is fp16: layer 1 multiplies the exact pixels (fp16 1024 + u) and corrects the
+        # offset with the W1 row sums, kept as 64-bit fixed-point partials (mlp_fused.hip, R1_BLK)
+        self.w1h = torch.zeros(HIDDEN, D_IN_PAD, dtype=torch.float16, device=dev)
+        self.r1p = torch.zeros(HIDDEN * R1_BLK, dtype=torch.int64, device=dev)
         self.w2h = torch.zeros(HIDDEN, HIDDEN, dtype=bf, device=dev)
         self.w2th = torch.zeros(HIDDEN, HIDDEN, dtype=bf, device=dev)
         self.w3h = torch.zeros(16, HIDDEN, dtype=bf, device=dev)
@@ -347,7 +352,7 @@ class FusedMLPTrainer:
         n = self._n
         n.call("sl_mlp_sgd", n.ptr(self.params), None, None, 0, 0, None, None, 0.0, 0.0, 0.0, self.xa, self.xb, 0,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w2th), n.ptr(self.w3h), n.ptr(self.w3th),
-               None, n.stream_ptr())
+               None, n.ptr(self.r1p), n.stream_ptr())
 
     @property
     def dh1_scale(self) -> float:
@@ -371,7 +376,7 @@ class FusedMLPTrainer:
                              p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
                              p(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                              p(self.h1t), p(self.w3p), p(self.dh2t), p(self.dh1t),
-                             p(self.loss), p(self.correct), None, 1),
+                             p(self.loss), p(self.correct), None, 1, p(self.r1p)),
             "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
                               self.slices, self.slab_stride),
@@ -383,14 +388,14 @@ class FusedMLPTrainer:
                                 None if from_grad else p(self.slab), self.slices, self.slab_stride,
                                 p(self.grad) if from_grad else None, p(self.grad) if grad_out else None,
                                 self.lr, self.momentum, self.weight_decay, *self.dw1_coeffs, mode, *ws,
-                                p(self.cursor) if bump else None)
+                                p(self.cursor) if bump else None, p(self.r1p))
         if self.xgmi is not None:
             xg = self.xgmi
             lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.slab_stride, *self.dw1_coeffs,
                                      xg.slot_ptr(0), xg.slot_ptr(1), xg.ctl.data_ptr())
             lc["xbarrier"] = [n.Launch(fn, *xg.args(), *extra) for fn, extra in xg.exchange_launches(self.n_pad)]
             lc["xupdate"] = n.Launch("sl_mlp_sgd_xgmi", p(self.params), p(self.mom), self.lr, self.momentum,
-                                     self.weight_decay, *ws, p(self.cursor), *xg.args())
+                                     self.weight_decay, *ws, p(self.cursor), *xg.args(), p(self.r1p))
         self._lc, self._lkey = lc, key
         return lc
 
@@ -402,7 +407,7 @@ class FusedMLPTrainer:
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                n.ptr(self.h1t), n.ptr(self.w3p), n.ptr(self.dh2t), n.ptr(self.dh1t),
-               n.ptr(self.loss), n.ptr(self.correct), None, 0, n.stream_ptr())
+               n.ptr(self.loss), n.ptr(self.correct), None, 0, n.ptr(self.r1p), n.stream_ptr())
 
     def _wgrad(self):
         self._launches()["wgrad"]()
@@ -537,7 +542,7 @@ class FusedMLPTrainer:
         n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
-               n.ptr(loss), n.ptr(corr), None, 0, n.stream_ptr())
+               n.ptr(loss), n.ptr(corr), None, 0, n.ptr(self.r1p), n.stream_ptr())
         return StepStats(float(loss.mean()), float(corr.mean()), rows)
 
     def logits(self, x_u8: torch.Tensor) -> torch.Tensor:
@@ -550,7 +555,7 @@ class FusedMLPTrainer:
         n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
-               None, None, n.ptr(out), 0, n.stream_ptr())
+               None, None, n.ptr(out), 0, n.ptr(self.r1p), n.stream_ptr())
         return out
 
     def get_flat(self) -> torch.Tensor:
