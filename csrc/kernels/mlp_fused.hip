@@ -40,14 +40,21 @@
 using namespace sl;
 
 namespace {
-// Cache policy of the stores that hand a kernel's outputs to the next launch (H1/dH2/dH1 rows,
-// w3p partials, weight-gradient slabs): 16 = sc1 (write-through), 0 = default write-back.
+// Cache policy of the stores that hand a kernel's outputs to the next launch: 16 = sc1
+// (write-through), 0 = default write-back (kept: write-through halves the launch gaps but
+// stretches the kernels by more, profiles/r05_sc1).  OUT_AUX: whole-line 16-B stores (H1 / dH2 rows,
+// weight-gradient slabs); OUT_AUX_NARROW: the partial-line ones (dH1's 8-B fragment rows, the
+// w3p partials' 4-B stores).
 #ifndef SL_STORE_AUX
 #define SL_STORE_AUX 0
 #endif
+#ifndef SL_STORE_AUX_NARROW
+#define SL_STORE_AUX_NARROW 0
+#endif
 constexpr int OUT_AUX = SL_STORE_AUX;
+constexpr int OUT_AUX_NARROW = SL_STORE_AUX_NARROW;
 __device__ __forceinline__ void st_out(float* p, float v) {
-  if constexpr (OUT_AUX & 16) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (OUT_AUX_NARROW & 16) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
 
@@ -871,7 +878,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       for (int n = 0; n < NF; ++n) {
         typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
         const u32x2_t h = {hv[n][0], hv[n][1]};
-        __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, OUT_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, OUT_AUX_NARROW);
       }
     }
     // Transpose-reduce of the 32 column partials over the 16 rows of a DPP row: each
@@ -1449,6 +1456,7 @@ struct SgdArgs {
   float* grad_out_alt;
   const unsigned* ar_ctl;
   long long* r1p;  // fixed-point partial row sums of the fp16 W1 shadow (tiled mode 2 writes them)
+  unsigned long long* stamps;  // diagnostics, tiled path: [workgroup][2] start / end s_memrealtime
 };
 
 // Shadow copies of the new weight: fp16 for W1 (layer 1 multiplies exact fp16 pixels), bf16
@@ -1585,6 +1593,7 @@ __host__ __device__ constexpr long sgd_units(bool slab) {
 
 __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
+  if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 2] = __builtin_amdgcn_s_memrealtime();
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int part = (int)(t % SGD_TPG);
   if (a.slab && a.mode != 0) {
@@ -1605,6 +1614,10 @@ __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
       if (fx) atomicAdd(&rs[lane_u & 15], (unsigned long long)fx);
       __syncthreads();
       if (threadIdx.x < 16) a.r1p[(mbase + threadIdx.x) * R1_BLK + blk] = (long long)rs[threadIdx.x];
+    }
+    if (a.stamps) {
+      __syncthreads();
+      if (threadIdx.x == 0) a.stamps[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime();
     }
     return;
   }
@@ -1693,6 +1706,12 @@ int sl_mlp_set_stamps(unsigned long long* p) {
   g_stamps = p;
   return 0;
 }
+static unsigned long long* g_sgd_stamps = nullptr;
+int sl_mlp_set_sgd_stamps(unsigned long long* p) {  // SGD stamps (diagnostics, tiled path)
+  g_sgd_stamps = p;
+  return 0;
+}
+int sl_mlp_sgd_wgs() { return (int)((sgd_units(true) * SGD_TPG + SGD_NT - 1) / SGD_NT); }
 static unsigned long long* g_wg_stamps = nullptr;
 int sl_mlp_set_wg_stamps(unsigned long long* p) {  // weight-gradient stamps (diagnostics)
   g_wg_stamps = p;
@@ -1797,7 +1816,7 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   a.grad_in = grad_in; a.grad_out = grad_out; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = mode;
   a.xa = xa; a.xb = xb;
   a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
-  a.grad_out_alt = nullptr; a.ar_ctl = nullptr; a.r1p = r1p;
+  a.grad_out_alt = nullptr; a.ar_ctl = nullptr; a.r1p = r1p; a.stamps = g_sgd_stamps;
   if (mode != 0 && !slab && !grad_in) return -1;
   if (mode != 1 && !r1p) return -1;  // every shadow write refreshes the W1 row sums
   if (mode == 1 && !grad_out) return -1;

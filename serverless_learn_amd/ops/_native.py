@@ -40,6 +40,8 @@ _SIGS: dict[str, list] = {
     "sl_mlp_rows_bm": [I],
     "sl_mlp_set_stamps": [P],
     "sl_mlp_set_wg_stamps": [P],
+    "sl_mlp_set_sgd_stamps": [P],
+    "sl_mlp_sgd_wgs": [],
     "sl_mlp_sgd": [P, P, P, I, L, P, P, F, F, F, F, F, I, P, P, P, P, P, P, P, P],
     "sl_mlp_reduce_xgmi": [P, I, L, F, F, P, P, P, P],
     "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, L, P, P],
