@@ -133,6 +133,14 @@ struct FragSrc {
 // diagnostics: per-workgroup row-kernel stamps [0..9 phases (s_memtime) | 10 HW_ID | 11 XCC_ID |
 // 12..15 sub-phases | 16, 17 start / end s_memrealtime (100 MHz): their ratio gives the shader clock]
 constexpr int ROW_STAMPS = 20;
+// Wave priority of the younger of the two workgroups that share a CU (dispatch order: the grid's
+// second half within each XCD; every one of the 256 CU pairs measured is one older + one younger).
+// 0: off (age decides: the older workgroup wins issue, finishes ~25k cycles earlier and the
+// younger runs its tail alone); 1 (default): the younger raises its priority after layer 1 and
+// the pair ends together (driver form +2.3 %, profiles/r05_prio); 2: after the softmax (neutral).
+#ifndef SL_ROWS_PRIO
+#define SL_ROWS_PRIO 1
+#endif
 
 struct MlpRowArgs {
   const uint8_t* x;
@@ -344,6 +352,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lg = lane >> 4;
   const int row0 = blockIdx.x * BM;
+  const bool young = (int)(blockIdx.x >> 3) >= (int)(gridDim.x >> 4);  // SL_ROWS_PRIO
   const long srow0 = batch_base(a.cursor, a.n_batches, a.batch) + row0;
   const int wng = wave;
   const int cw = wng * 16 * NF;  // this wave's output columns
@@ -653,6 +662,9 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
     }
   }
   stamp(1);
+  if constexpr (SL_ROWS_PRIO == 1) {
+    if (young) __builtin_amdgcn_s_setprio(1);
+  }
   if constexpr (ONE) bar();  // the X ring shares the image H1 goes to
   stamp(12);
   relu_out(BS, R1, true, a.xa);
@@ -742,6 +754,9 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
     }
   }
   if (!TRAIN) return;
+  if constexpr (SL_ROWS_PRIO == 2) {
+    if (young) __builtin_amdgcn_s_setprio(1);
+  }
   bar();
   stamp(5);
 

@@ -83,3 +83,24 @@ print(f"CUs seen {len(by)}  WGs/CU median {np.median([len(v) for v in by.values(
       f"sum(WG time)/span median {np.median(np.array(busy) / np.array(spans)):.2f}")
 xs = collections.Counter(int(x) for x in xcc)
 print("WGs per XCC:", dict(sorted(xs.items())))
+
+# ---- the two workgroups sharing a CU: per-phase cycles of the one that ends first vs last ----
+dph = s[:, 1:] - s[:, :-1]
+first, last, pair_ids = [], [], []
+for k, idx in collections.defaultdict(list, {kk: [i for i in range(len(key)) if int(key[i]) == kk]
+                                             for kk in set(int(v) for v in key)}).items():
+    if len(idx) != 2:
+        continue
+    i, j = sorted(idx, key=lambda q: t1s[q])
+    pair_ids.append((i, j))
+    first.append(dph[i].numpy()); last.append(dph[j].numpy())
+if first:
+    f, l = np.median(np.array(first), 0), np.median(np.array(last), 0)
+    print(f"CU pairs {len(first)}: median phase cycles, WG ending first | WG ending last")
+    for n_, a_, b_ in zip(names, f, l):
+        print(f"  {n_:14s} {a_:8.0f} | {b_:8.0f}")
+    half = s.shape[0] // 16  # per XCD: workgroups (blockIdx >> 3) >= half are the younger ones
+    young_last = sum(1 for i, j in pair_ids if (j >> 3) >= half)
+    mixed = sum(1 for i, j in pair_ids if ((i >> 3) >= half) != ((j >> 3) >= half))
+    print(f"  pairs with one older + one younger workgroup: {mixed}/{len(pair_ids)}; "
+          f"younger ends last: {young_last}/{len(pair_ids)}")
