@@ -126,7 +126,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const uint8_t* __restrict__ ymask,
                                                             uint16_t* __restrict__ dz_out, float* __restrict__ sums,
                                                             const uint16_t* __restrict__ x2,
-                                                            float* __restrict__ sums2, long rows, int C) {
+                                                            float* __restrict__ sums2, long rows, int C,
+                                                            RsumFold fold) {
   // x2/sums2: a second BN fed by the same dz (the downsample shortcut's), whose
   // sums ride along so dz is not read back: sums2 = (sum dz, sum dz*x2).
   __shared__ float part[256][25];
@@ -190,6 +191,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     if (qsel < 2) rsum_add(rep, qsel * C + c, acc);
     else rsum_add(rep2, (qsel - 2) * C + c, acc);
   }
+  rsum_arrive(fold);
 }
 
 // dcoef layout [3][C]: a, b, c with dx = a*dz + b*x + c.  grad_gamma/beta += (flat gradient).
@@ -659,8 +661,9 @@ int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, ymask, dz_out, sums, x2, sums2, rows,
-                     C);
+                     C, rsum_fold_spec(sums, x2 ? sums2 : nullptr, 2 * C, 1));
   SL_CHECK_LAUNCH();
+  if (SL_RSUM_ARRIVE) return 0;
   if (int rc = sl_rsum_fold2(sums, x2 ? sums2 : nullptr, 2 * C, stream)) return rc;
   return 0;
 }

@@ -114,8 +114,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // A thousand workgroups atomically adding into the same n words serialise on
 // those words (MI355X_MICROARCH.md "Global float atomics", contention row), so
 // each workgroup adds into replica (blockIdx % SL_REP) of a [SL_REP][n] array
-// and a separate launch, rsum_fold_kernel (conv.hip, sl_rsum_fold), folds the
-// replicas into out[n] once the producers are done.  The fold used to be done
+// and a separate launch, rsum_fold_kernel (conv.hip, sl_rsum_fold), folds the replicas
+// into out[n] once the producers are done (or, with SL_RSUM_ARRIVE=1, the producer
+// launch's last-arriving workgroup: rsum_arrive below).  The fold used to be done
 // by the last workgroup of the producer itself (agent-release fence + ticket per
 // workgroup): with ~1000-8000 workgroups per launch the per-workgroup release
 // (an L2 writeback on a multi-XCD part) and the single-address ticket cost
@@ -169,6 +170,87 @@ __device__ __forceinline__ void rsum_add(float* rep, long i, float v) {
 #else
   atomicAdd(rep + i, v);
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// Fold by the last-arriving workgroup (SL_RSUM_ARRIVE=1; default off): the producer's own
+// launch folds the replicas into the result row, so no rsum_fold launch follows it.  Measured
+// (profiles/r05_arrive): the 37 fold launches per ResNet-18 step go, but every producer grows
+// by about what its fold launch cost (+2.5-4.6 us: each workgroup now drains its epilogue
+// stores and waits for a returning ticket before it exits, and the last one reads the replicas
+// after that), and the step is 1.3 % slower; the separate launch stays the default.  Each
+// workgroup, after all of its replica atomics (every wave drains them: `s_waitcnt vmcnt(0)`,
+// then a workgroup barrier), takes a ticket with ONE agent-scope atomic add; the workgroup
+// whose add returns gridDim - 1 is the launch's last.  A producer may span several launches
+// adding into the same buffer (the four parity-class launches of a stride-2 data gradient):
+// the last arrival of each launch adds to a launch counter and the one completing `launches`
+// folds.  The replica atomics are performed past the CUs' caches and the folding workgroup
+// reads them with `sc1` loads after its own ticket returned (MI355X_MICROARCH.md, hand-off
+// table, first row); the result row goes out with plain stores and reaches its consumers
+// through the kernel boundary.  Both ticket words live in the buffer's pad (rsum_floats) and
+// are re-armed to 0 by the workgroup that completes them.
+// ---------------------------------------------------------------------------
+#ifndef SL_RSUM_ARRIVE
+#define SL_RSUM_ARRIVE 0
+#endif
+struct RsumFold {
+  float* buf;     // rsum buffer of n values (null: nothing to fold)
+  float* buf2;    // a second buffer folded by the same arrivals (nullable)
+  int n;
+  int launches;   // launches whose workgroups all add into buf (>= 1)
+};
+
+__device__ __forceinline__ void rsum_fold_row(float* buf, int n, int tid, int nthr) {
+  float* res = rsum_result(buf, n);
+  for (int i = tid; i < n; i += nthr) {
+#if SL_DETERMINISTIC
+    unsigned long long* p = reinterpret_cast<unsigned long long*>(buf) + 2 * i;
+    const long long hi = (long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long lo = (long long)__hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    res[i] = (float)((double)hi * (1.0 / SL_FIX_HI) + (double)lo * (1.0 / SL_FIX_LO));
+#else
+    float v[SL_REP];
+#pragma unroll
+    for (int r = 0; r < SL_REP; ++r) v[r] = __hip_atomic_load(buf + (long)r * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < SL_REP; ++r) acc += v[r];  // the order rsum_fold_kernel sums in
+    res[i] = acc;
+#endif
+  }
+}
+
+// host: the fold a producer launch carries (none when the separate fold launch is used)
+__host__ __device__ inline RsumFold rsum_fold_spec(float* buf, float* buf2, int n, int launches) {
+  return SL_RSUM_ARRIVE && buf ? RsumFold{buf, buf2, n, launches} : RsumFold{nullptr, nullptr, 0, 0};
+}
+
+// Every thread of the workgroup calls this once per launch, after all of the workgroup's
+// rsum_add calls into f.buf / f.buf2, in uniform control flow.
+__device__ __forceinline__ void rsum_arrive(const RsumFold& f) {
+  if (!f.buf) return;
+  __shared__ unsigned rsum_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's replica atomics are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* t = reinterpret_cast<unsigned*>(f.buf + (long)(SL_REP + 1) * f.n);
+    unsigned last = 0;
+    if (__hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = 1;
+      if (f.launches > 1) {
+        last = __hip_atomic_fetch_add(t + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)f.launches - 1;
+        if (last) __hip_atomic_store(t + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    rsum_last = last;
+  }
+  __syncthreads();
+  if (rsum_last) {
+    rsum_fold_row(f.buf, f.n, threadIdx.x, blockDim.x);
+    if (f.buf2) rsum_fold_row(f.buf2, f.n, threadIdx.x, blockDim.x);
+  }
 }
 
 }  // namespace sl

@@ -94,6 +94,7 @@ struct ConvEpi {
   const uint16_t* add;  // [M][ldy] bf16 added to the result (nullable)
   float* stats;         // rsum buffer of 2*ncols (sum, sum of squares), zeroed (nullable)
   BnBwdEpi bn;          // data gradient only: ReLU mask + BN-backward sums of the output (bn.x null: off)
+  RsumFold fold;        // stats or bn.sums/sums2, folded by this launch's last workgroup (common.h)
 };
 
 struct Pix {
@@ -409,7 +410,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
         }
       }
   }
-  if (!e.y) return;
+  if (!e.y) {
+    rsum_arrive(e.fold);
+    return;
+  }
   // bf16 tile through LDS -> coalesced 16-B row stores (+ bias, + residual, + fused BN backward)
   uint16_t* Cs = smem;
 #pragma unroll
@@ -474,6 +478,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     __syncthreads();  // staging reads done: the ring holds the fold
     bnb_fold<256, CPR>(e.bn, bacc, reinterpret_cast<float*>(smem), n0, e.ncols);
   }
+  rsum_arrive(e.fold);
 }
 
 // ---------------------------------------------------------------------------
@@ -665,7 +670,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
         }
       }
   }
-  if (!e.y) return;
+  if (!e.y) {
+    rsum_arrive(e.fold);
+    return;
+  }
   uint16_t* Cs = smem;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -715,6 +723,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
     __syncthreads();
     bnb_fold<512, CPR>(e.bn, bacc, reinterpret_cast<float*>(smem), n0, e.ncols);
   }
+  rsum_arrive(e.fold);
 }
 
 // ---------------------------------------------------------------------------
@@ -1346,10 +1355,10 @@ int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w
   if (y && !yf && !bias && OH == H && OW == W && sl_conv3x3_c64_applicable(H, W, C, cout, KH, KW, stride, pad, C)) {
     rc = sl_conv3x3_c64(x, w, C, 0, N, H, y, ldy, nullptr, stats, stream);
   } else {
-    ConvEpi e{w, cout, y, ldy, yf, bias, nullptr, stats, {}};
+    ConvEpi e{w, cout, y, ldy, yf, bias, nullptr, stats, {}, rsum_fold_spec(stats, nullptr, 2 * cout, 1)};
     rc = launch_gemm<false>(g, e, stream);
   }
-  if (rc || !stats) return rc;
+  if (rc || !stats || SL_RSUM_ARRIVE) return rc;
   return sl_rsum_fold(stats, 2 * cout, stream);
 }
 
@@ -1364,8 +1373,11 @@ static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, in
   if (!add_even && !even_only && H == OH && W == OW && ldd == 64 && !(bn && bn->x2) &&
       sl_conv3x3_c64_applicable(OH, OW, ldd, cin, KH, KW, stride, pad, ldd))
     return sl_conv3x3_c64_bn(dy, wt, 64, 1, N, OH, dx, cin, add, nullptr, bn, stream);
-  ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr, {}};
-  if (bn) e.bn = *bn;
+  ConvEpi e{wt, cin, dx, cin, nullptr, nullptr, add, nullptr, {}, {}};
+  if (bn) {
+    e.bn = *bn;
+    e.fold = rsum_fold_spec(bn->sums, bn->x2 ? bn->sums2 : nullptr, 2 * cin, 1);
+  }
   const bool phase_ok = stride == 2 && KH == KW && ((KH == 3 && pad == 1) || (KH == 1 && pad == 0)) &&
                         (ldd & 63) == 0;
   if ((add_even || even_only) && !phase_ok) return -5;
@@ -1397,6 +1409,7 @@ static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, in
       }
     for (int i = 0; i < nq; ++i) {
       ConvEpi ei = e;
+      if (ei.fold.buf) ei.fold.launches = nq;  // the classes' launches all add into the BN sums
       if (add_even && (qs[i].ph || qs[i].pw)) ei.add = nullptr;
       const int rc = launch_gemm<true>(qs[i], ei, stream);
       if (rc) return rc;
@@ -1424,7 +1437,7 @@ int sl_conv_dgrad_bn(const uint16_t* dy, int N, int OH, int OW, int ldd, const u
   if (add_even && !add) return -5;
   int rc = dgrad_launch(g, dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, fuse ? bn : nullptr,
                         stream, add_even != 0);
-  if (rc || !fuse) return rc;
+  if (rc || !fuse || SL_RSUM_ARRIVE) return rc;
   return sl_rsum_fold2(bn->sums, bn->x2 ? bn->sums2 : nullptr, 2 * cin, stream);
 }
 

@@ -94,6 +94,7 @@ struct HaloArgs {
   // coefficients and running statistics, as bn_apply_stats would have
   BnStats bin;
   float bin_count, bin_eps, bin_momentum;
+  RsumFold fold;        // stats or bn.sums, folded by the last workgroup (common.h)
 };
 
 // DEFER (plain forward: no residual, no fused BN backward): the bf16 output tile is staged in
@@ -372,6 +373,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
     __syncthreads();  // the last tile's staging reads are done (no halo follows)
     bnb_fold<NTF, HC / 8>(a.bn, bacc, reinterpret_cast<float*>(smem), 0, HC);
   }
+  rsum_arrive(a.fold);
 }
 
 static int g_halo_enabled = -1;  // -1: from SL_CONV_HALO (default on)
@@ -420,6 +422,8 @@ static int conv3x3_launch(const uint16_t* src, const uint16_t* w, int cin, int f
   if (bn) a.bn = *bn;
   a.bin = BnStats{};
   a.bin_count = bin_count; a.bin_eps = bin_eps; a.bin_momentum = bin_momentum;
+  a.fold = stats ? rsum_fold_spec(stats, nullptr, 2 * HC, 1)
+                 : rsum_fold_spec(bn ? bn->sums : nullptr, nullptr, 2 * HC, 1);
   if (bin) {
     if (cin != 64 || flip || !bin->stats || !bin->gamma || !bin->beta || !bin->coef || bin_count <= 0.f) return -4;
     a.bin = *bin;
@@ -464,7 +468,7 @@ int sl_conv3x3_bnin_fwd(const uint16_t* x, const uint16_t* w, int N, int H, uint
                         float* run_var, float count, float eps, float momentum, hipStream_t stream) {
   const BnStats bin{bstats, gamma, beta, coef, run_mean, run_var};
   const int rc = conv3x3_launch(x, w, 64, 0, N, H, y, ldy, nullptr, stats, nullptr, &bin, count, eps, momentum, stream);
-  if (rc || !stats) return rc;
+  if (rc || !stats || SL_RSUM_ARRIVE) return rc;
   return sl_rsum_fold(stats, 2 * HC, stream);  // as sl_conv_fwd does after its epilogue sums
 }
 
