@@ -453,14 +453,30 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       const float4 bias = *reinterpret_cast<const float4*>(bias_v + col);
 #pragma unroll
       for (int m = 0; m < MF; ++m) {
+        typedef float f2_t __attribute__((ext_vector_type(2)));
+        const f2_t ya = __builtin_elementwise_fma(f2_t{sc, sc}, f2_t{acc[m][n][0], acc[m][n][1]}, f2_t{bias.x, bias.y});
+        const f2_t yb = __builtin_elementwise_fma(f2_t{sc, sc}, f2_t{acc[m][n][2], acc[m][n][3]}, f2_t{bias.z, bias.w});
+        const float y0 = ya[0], y1 = ya[1], y2 = yb[0], y3 = yb[1];  // v_pk_fma_f32
         uint2 v;
-        v.x = pack2(fmaxf(fmaf(sc, acc[m][n][0], bias.x), 0.f), fmaxf(fmaf(sc, acc[m][n][1], bias.y), 0.f));
-        v.y = pack2(fmaxf(fmaf(sc, acc[m][n][2], bias.z), 0.f), fmaxf(fmaf(sc, acc[m][n][3], bias.w), 0.f));
+        v.x = pack2(fmaxf(y0, 0.f), fmaxf(y1, 0.f));
+        v.y = pack2(fmaxf(y2, 0.f), fmaxf(y3, 0.f));
         *reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col) = v;
-        if (ONE && with_mask)
+        if (ONE && with_mask) {
+          // 1[y > 0] from the pre-activation's bits: a positive float is a positive int, so
+          // one v_med3_i32 (clamp to [0, 1]) per value, three v_lshl_or to pack the nibble
+          auto pos = [](float y) {
+            uint32_t r;
+            asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(y));
+            return r;
+          };
+          auto lshl_or = [](uint32_t a, int sh, uint32_t b) {  // (a << sh) | b
+            uint32_t r;
+            asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(sh), "v"(b));
+            return r;
+          };
           M1[(rw + m * 16 + lr) * 64 + (col >> 2)] =
-              (uint8_t)(((v.x & 0xffffu) != 0) | (((v.x >> 16) != 0) << 1) | (((v.y & 0xffffu) != 0) << 2) |
-                        (((v.y >> 16) != 0) << 3));
+              (uint8_t)lshl_or(lshl_or(pos(y3), 1, pos(y2)), 2, lshl_or(pos(y1), 1, pos(y0)));
+        }
       }
     }
   };
@@ -494,9 +510,17 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       for (int m = 0; m < MF; ++m) {
         uint2* e = reinterpret_cast<uint2*>(img + (rw + m * 16 + lr) * HS_LD + col);
         const uint2 h = *e;
+        // per bf16 half: all ones where H > 0 (min(h, 1) then 0 - that, packed 16-bit ops)
+        auto nz = [](uint32_t w) {
+          uint32_t t;
+          // op_sel_hi:[1,0]: the high half takes the inline constant's low half too (a packed
+          // op's inline constant is 32-bit: its high half would be 0)
+          asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]\n\tv_pk_sub_u16 %0, 0, %0" : "=&v"(t) : "v"(w));
+          return t;
+        };
         uint2 v;
-        v.x = pack2((h.x & 0xffffu) ? acc[m][n][0] : 0.f, (h.x >> 16) ? acc[m][n][1] : 0.f);
-        v.y = pack2((h.y & 0xffffu) ? acc[m][n][2] : 0.f, (h.y >> 16) ? acc[m][n][3] : 0.f);
+        v.x = pack2(acc[m][n][0], acc[m][n][1]) & nz(h.x);
+        v.y = pack2(acc[m][n][2], acc[m][n][3]) & nz(h.y);
         *e = v;
       }
     }
