@@ -47,6 +47,14 @@ constexpr int NWF = SL_HALO_WAVES;     // waves of the forward / dgrad kernel
 #ifndef SL_HALO_DEFER
 #define SL_HALO_DEFER 1  // plain forward: output stores deferred into the next tile's k-loop
 #endif
+#ifndef SL_HALO_EPI_PF
+// data gradient (no DEFER): issue the epilogue's residual / BN-input / mask loads at the top of
+// the tile's k-loop instead of after it, so their HBM latency hides under the MFMAs
+#define SL_HALO_EPI_PF 1
+#endif
+#ifndef SL_HALO_LDSBAR
+#define SL_HALO_LDSBAR 1  // LDS-only barriers inside the tile loop (see lds_bar)
+#endif
 #ifndef SL_HALO_KO
 // timing knockouts of conv3x3_kernel (results wrong; profiles/r03_haloko): 1 no epilogue global
 // traffic, 2 no halo loads after the first tile, 3 no MFMAs / fragment reads, 4 no epilogue
@@ -119,6 +127,18 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lg = lane >> 4;
   const int tiles_per_img = a.H / TR;
+  // The tile loop's barriers order LDS traffic only (halo / staging / Ds images): waiting for
+  // lgkmcnt suffices.  __syncthreads() would also drain every outstanding global store
+  // (vmcnt(0)), stalling the data gradient on its own output tile's HBM writes once per tile.
+  auto lds_bar = [&]() __attribute__((always_inline)) {
+    if constexpr (SL_HALO_LDSBAR) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
+  };
 
   // ---- weights -> LDS, once (flip applied here, so the k-loop is tap-agnostic) ----
   for (int q = tid; q < HC * L::WROW; q += NTF) {
@@ -202,9 +222,26 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   if (t < a.tiles) halo_load(t);
   halo_store();
   __syncthreads();
+  // residual / BN operands of this thread's epilogue chunks (tile pixel p = (tid + k NTF) / 8,
+  // channels (tid & 7) * 8 ..): SL_HALO_EPI_PF issues them before the k-loop
+  constexpr int EIT = TPIX * 8 / NTF;
+  const int ec = (tid & 7) * 8;
+  short8_t ea[EIT];
+  BnbIn ebn[EIT];
+  auto epi_loads = [&](int tt) __attribute__((always_inline)) {
+    const long pix0 = (long)tt * TPIX;
+#pragma unroll
+    for (int k = 0; k < EIT; ++k) {
+      const long off = (pix0 + ((tid + k * NTF) >> 3)) * a.ldy + ec;
+      if (SL_HALO_KO == 1) continue;
+      if (a.add) ea[k] = ld8(a.add + off);
+      if (bnb) bnb_load<false>(a.bn, off, ebn[k]);
+    }
+  };
   for (; t < a.tiles; t += gridDim.x) {
     const int next = t + gridDim.x;
     if (next < a.tiles && SL_HALO_KO != 2) halo_load(next);  // lands under this tile's MFMAs
+    if constexpr (!DEFER && SL_HALO_EPI_PF) epi_loads(t);    // ... and so do these
 
     floatx4_t acc[MF][4];
 #pragma unroll
@@ -257,7 +294,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       if (s + 1 < L::NKS && SL_HALO_KO != 3) mfmas(a1, b1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();  // every wave is done with this halo
+    lds_bar();  // every wave is done with this halo
     if (SL_HALO_KO == 4) {
       if (next < a.tiles) {
         halo_store();
@@ -293,7 +330,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       prev_t = t;
       if (next < a.tiles) {
         halo_store();
-        __syncthreads();  // halo and Ds visible to the next k-loop
+        lds_bar();  // halo and Ds visible to the next k-loop
       }
       continue;
     }
@@ -305,20 +342,11 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           Cs[(wave * (TPIX / NWF) + i * 16 + 4 * lg + r) * OUT_LD + j * 16 + lr] = f2bf(acc[i][j][r]);
-    // residual / BN operands of this thread's chunks, in flight under the staging barrier
-    constexpr int EIT = TPIX * 8 / NTF;
+    // without SL_HALO_EPI_PF the operands are issued here, in flight under the staging barrier
     const long pix0 = (long)t * TPIX;  // tiles are whole 8-row bands: pixel index = tile * 256
-    const int c = (tid & 7) * 8;
-    short8_t ea[EIT];
-    BnbIn ebn[EIT];
-#pragma unroll
-    for (int k = 0; k < EIT; ++k) {
-      const long off = (pix0 + ((tid + k * NTF) >> 3)) * a.ldy + c;
-      if (SL_HALO_KO == 1) continue;
-      if (a.add) ea[k] = ld8(a.add + off);
-      if (bnb) bnb_load<false>(a.bn, off, ebn[k]);
-    }
-    __syncthreads();
+    const int c = ec;
+    if constexpr (!SL_HALO_EPI_PF) epi_loads(t);
+    lds_bar();
 #pragma unroll
     for (int k = 0; k < EIT; ++k) {
       const int p = (tid + k * NTF) >> 3;
@@ -335,10 +363,10 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       if (bnb) bnb_chunk<false>(a.bn, ebn[k], v, msc, msh, bacc);
       *reinterpret_cast<short8_t*>(a.y + m * a.ldy + c) = v;
     }
-    __syncthreads();  // staging reads done before the next halo lands
+    lds_bar();  // staging reads done before the next halo lands
     if (next < a.tiles) {
       halo_store();
-      __syncthreads();
+      lds_bar();
     }
   }
 
