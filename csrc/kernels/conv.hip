@@ -81,7 +81,14 @@ struct ConvGeom {
   // transposed gather zeroes.  ph < 0: off.  OH/OW are then the parity-class
   // grid and FH/FW the full output.
   int ph, pw, ntaps, FH, FW;
-  int dh[4], dw[4], tapw[4];
+  // Tap tables of every class the launch covers, concatenated (class c uses entries
+  // cls_tap0[c] ..).  ncls > 1 (SL_CONV_PHASE_MERGE): ONE launch computes all parity classes
+  // of a stride-2 data gradient -- they have the same pixel count, so each class is an equal
+  // block of the grid -- instead of one launch per class; ph is then 0 and the class's own
+  // parity / K sit in cls_ph / cls_pw / cls_K.  add_cls0_only: only class 0 = (0, 0) adds e.add.
+  int dh[9], dw[9], tapw[9];
+  int ncls, add_cls0_only;
+  int cls_K[4], cls_ph[4], cls_pw[4], cls_tap0[4];
 };
 
 struct ConvEpi {
@@ -239,7 +246,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int logical0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_cls = (int)gridDim.x / g.ncls;  // merged parity classes: equal grid blocks
+  const int cls = g.ncls > 1 ? logical0 / per_cls : 0;
+  const int logical = logical0 - cls * per_cls;
+  const int gK = g.cls_K[cls], gph = g.cls_ph[cls], gpw = g.cls_pw[cls], tap0 = g.cls_tap0[cls];
+  const uint16_t* eadd = (g.add_cls0_only && cls) ? nullptr : e.add;
   const int tm = logical / tiles_n, tn = logical - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int wm = wave >> 1, wn = wave & 1;
@@ -285,9 +297,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
       const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
       int dh, dw;
       if (TRANSPOSED && g.ph >= 0) {
-        dh = g.dh[tap];
-        dw = g.dw[tap];
-        kb = g.tapw[tap] * g.SC + ch0;
+        dh = g.dh[tap0 + tap];
+        dw = g.dw[tap0 + tap];
+        kb = g.tapw[tap0 + tap] * g.SC + ch0;
       } else {
         const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
         dh = TRANSPOSED ? -kh : kh;
@@ -303,9 +315,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
       const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
       int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
       if (TRANSPOSED && g.ph >= 0) {
-        kh = g.dh[tap];
-        kw = g.dw[tap];
-        kb = g.tapw[tap] * g.SC + ch0;
+        kh = g.dh[tap0 + tap];
+        kw = g.dw[tap0 + tap];
+        kb = g.tapw[tap0 + tap] * g.SC + ch0;
       }
 #pragma unroll
       for (int j = 0; j < PA; ++j)
@@ -318,7 +330,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
       const int k0 = kt * BK + cb[j] * 8;
-      glds16((pb[j] && k0 < g.K) ? pb[j] + (kb + cb[j] * 8) : g_conv_zero, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK));
+      glds16((pb[j] && k0 < gK) ? pb[j] + (kb + cb[j] * 8) : g_conv_zero, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK));
     }
   };
 
@@ -344,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = zero4();
 
-  const int nk = (g.K + BK - 1) / BK;
+  const int nk = (gK + BK - 1) / BK;
   for (int kt = 0; kt < NSLOT - 1 && kt < nk; ++kt) issue(kt);
   for (int kt = 0; kt < nk; ++kt) {
     vmcnt_stages<PS>(min(NSLOT - 2, nk - 1 - kt));
@@ -442,11 +454,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     long orow = row;  // phase mode: parity-class pixel -> full-output pixel
     if (TRANSPOSED && g.ph >= 0) {
       const Pix q = decode_pix(g, row);
-      orow = ((long)q.n * g.FH + 2 * q.oh + g.ph) * g.FW + 2 * q.ow + g.pw;
+      orow = ((long)q.n * g.FH + 2 * q.oh + gph) * g.FW + 2 * q.ow + gpw;
     }
     eoff[it] = orow * e.ldy + col;
     const bool ok = row < g.M && full;
-    if (ok && e.add) ea[it] = ld8(e.add + eoff[it]);
+    if (ok && eadd) ea[it] = ld8(eadd + eoff[it]);
     if (ok && bnb) bnb_load(e.bn, eoff[it], ebn[it]);
   }
   BnbAcc bacc;
@@ -460,7 +472,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
     uint16_t* dst = e.y + eoff[it];
     if (full) {
-      if (e.add) {
+      if (eadd) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
       }
@@ -469,7 +481,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
     } else {
       for (int t = 0; t < 8 && col + t < e.ncols; ++t) {
         float f = bf2f((uint16_t)v[t]);
-        if (e.add) f += bf2f(e.add[eoff[it] + t]);
+        if (eadd) f += bf2f(eadd[eoff[it] + t]);
         dst[t] = f2bf(f);
       }
     }
@@ -511,7 +523,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lg = lane >> 4;
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int logical0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_cls = (int)gridDim.x / g.ncls;  // merged parity classes (see ConvGeom)
+  const int cls = g.ncls > 1 ? logical0 / per_cls : 0;
+  const int logical = logical0 - cls * per_cls;
+  const int gK = g.cls_K[cls], gph = g.cls_ph[cls], gpw = g.cls_pw[cls], tap0 = g.cls_tap0[cls];
+  const uint16_t* eadd = (g.add_cls0_only && cls) ? nullptr : e.add;
   const int tm = logical / tiles_n, tn = logical - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int wm = wave >> 1, wn = wave & 1;
@@ -557,9 +574,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
     const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
     int dh, dw, kb;
     if (phase) {
-      dh = g.dh[tap];
-      dw = g.dw[tap];
-      kb = g.tapw[tap] * g.SC + ch0;
+      dh = g.dh[tap0 + tap];
+      dw = g.dw[tap0 + tap];
+      kb = g.tapw[tap0 + tap] * g.SC + ch0;
     } else {
       const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
       dh = TRANSPOSED ? -kh : kh;
@@ -598,7 +615,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = zero4();
 
-  const int nk = g.K / BK;  // uniform taps: K is a multiple of 64
+  const int nk = gK / BK;  // uniform taps: K is a multiple of 64
   for (int kt = 0; kt < NSLOT - 1 && kt < nk; ++kt) issue(kt);
   for (int kt = 0; kt < nk; ++kt) {
     // this wave's pieces of stage kt have landed once only stage kt + 1's (if issued) remain
@@ -697,10 +714,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
     long orow = row;
     if (phase) {
       const Pix pq = decode_pix(g, row);
-      orow = ((long)pq.n * g.FH + 2 * pq.oh + g.ph) * g.FW + 2 * pq.ow + g.pw;
+      orow = ((long)pq.n * g.FH + 2 * pq.oh + gph) * g.FW + 2 * pq.ow + gpw;
     }
     eoff[it] = orow * e.ldy + col;
-    if (row < g.M && e.add) ea[it] = ld8(e.add + eoff[it]);
+    if (row < g.M && eadd) ea[it] = ld8(eadd + eoff[it]);
     if (row < g.M && bnb) bnb_load(e.bn, eoff[it], ebn[it]);
   }
   BnbAcc bacc;
@@ -712,7 +729,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
     const int rl = tid / CPR + it * (512 / CPR), row = m0 + rl;
     if (row >= g.M) continue;
     short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
-    if (e.add) {
+    if (eadd) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
     }
@@ -1215,6 +1232,13 @@ static int fill_geom(ConvGeom& g, const uint16_t* src, int N, int SH, int SW, in
   g.ntaps = 0;
   g.FH = OH;
   g.FW = OW;
+  g.ncls = 1;
+  g.add_cls0_only = 0;
+  for (int c = 0; c < 4; ++c) {
+    g.cls_K[c] = g.K;
+    g.cls_ph[c] = g.cls_pw[c] = -1;
+    g.cls_tap0[c] = 0;
+  }
   const long M = (long)N * OH * OW;
   if (g.c_shift < 3 || M <= 0 || M > (1L << 30) || g.s_shift < 0 || OH <= 0 || OW <= 0 || KH * KW > 64) return -1;
   g.M = (int)M;
@@ -1248,13 +1272,15 @@ struct GemmPlan {
   long grid;
 };
 
+// mult: launches merged into one grid (the parity classes of a stride-2 data gradient);
+// the tile shape is chosen for the whole grid, p.grid counts one class's tiles
 template <bool T>
-static GemmPlan plan_gemm(const ConvGeom& g, const ConvEpi& e) {
+static GemmPlan plan_gemm(const ConvGeom& g, const ConvEpi& e, int mult = 1) {
   GemmPlan p{};
   // 256 x 128 tiles: uniform taps (64-channel stages), whole 128-column tiles, and enough
   // tiles for every CU; transposed gathers only in phase mode or at stride 1
   const long big_tiles = (long)((g.M + 255) / 256) * (e.ncols / 128);
-  if (gemm_big_enabled() && (g.SC & 63) == 0 && (g.K & 63) == 0 && (e.ncols & 127) == 0 && big_tiles >= 256 &&
+  if (gemm_big_enabled() && (g.SC & 63) == 0 && (g.K & 63) == 0 && (e.ncols & 127) == 0 && big_tiles * mult >= 256 &&
       (!T || g.ph >= 0 || g.stride == 1) && (g.wld & 7) == 0 && (!e.y || (e.ldy & 7) == 0)) {
     p.big = 1; p.BM = 256; p.BN = 128; p.tiles_n = e.ncols / 128; p.grid = big_tiles;
     return p;
@@ -1263,7 +1289,7 @@ static GemmPlan plan_gemm(const ConvGeom& g, const ConvEpi& e) {
   // prefer 128-row tiles while they still fill the 512 two-per-CU slots once
   // (ResNet-18 stage 4: 512 128x128 tiles beat 1024 64x128 tiles)
   const int tn128 = (e.ncols + (small_n ? 63 : 127)) / (small_n ? 64 : 128);
-  const bool small_m = (long)((g.M + 127) / 128) * tn128 < gemm_smallm_tiles();
+  const bool small_m = (long)((g.M + 127) / 128) * tn128 * mult < gemm_smallm_tiles();
   p.BM = small_m ? 64 : 128;
   p.BN = small_n ? 64 : 128;
   p.tiles_n = (e.ncols + p.BN - 1) / p.BN;
@@ -1273,8 +1299,8 @@ static GemmPlan plan_gemm(const ConvGeom& g, const ConvEpi& e) {
 
 template <bool T>
 static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) {
-  const GemmPlan p = plan_gemm<T>(g, e);
-  dim3 grid((unsigned)p.grid);
+  const GemmPlan p = plan_gemm<T>(g, e, g.ncls);
+  dim3 grid((unsigned)(p.grid * g.ncls));
   if (p.big) {
     hipLaunchKernelGGL((conv_gemm_big_kernel<T>), grid, dim3(512), 0, stream, g, e, p.tiles_n);
     SL_CHECK_LAUNCH();
@@ -1327,6 +1353,9 @@ extern "C" int sl_rsum_fold2(float* buf, float* buf2, int n, hipStream_t stream)
 extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream) { return sl_rsum_fold2(buf, nullptr, n, stream); }
 
 static int g_conv_phase = 1;  // stride-2 dgrad by parity classes (sl_conv_set_phase)
+#ifndef SL_CONV_PHASE_MERGE
+#define SL_CONV_PHASE_MERGE 1  // all parity classes of one data gradient in ONE launch
+#endif
 
 extern "C" {
 int sl_conv_set_phase(int on) {
@@ -1405,8 +1434,34 @@ static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, in
         if (t == 0) return -6;  // a class with no taps would have to be zero-filled
         q.ntaps = t;
         q.K = t * ldd;
+        q.cls_K[0] = q.K;
+        q.cls_ph[0] = ph;
+        q.cls_pw[0] = pw;
         qs[nq++] = q;
       }
+    bool merge = SL_CONV_PHASE_MERGE && nq > 1 && qs[0].ph == 0 && qs[0].pw == 0;
+    for (int i = 1; i < nq; ++i) merge = merge && qs[i].M == qs[0].M;
+    if (merge) {  // one launch, class i = grid block i (class 0 = (0, 0) holds the add_even term)
+      ConvGeom m = qs[0];
+      m.ncls = nq;
+      m.add_cls0_only = add_even ? 1 : 0;
+      m.K = 0;
+      int t0 = 0;
+      for (int i = 0; i < nq; ++i) {
+        m.cls_K[i] = qs[i].K;
+        m.cls_ph[i] = qs[i].ph;
+        m.cls_pw[i] = qs[i].pw;
+        m.cls_tap0[i] = t0;
+        for (int t = 0; t < qs[i].ntaps; ++t) {
+          m.dh[t0 + t] = qs[i].dh[t];
+          m.dw[t0 + t] = qs[i].dw[t];
+          m.tapw[t0 + t] = qs[i].tapw[t];
+        }
+        t0 += qs[i].ntaps;
+        m.K = m.K > qs[i].K ? m.K : qs[i].K;
+      }
+      return launch_gemm<true>(m, e, stream);
+    }
     for (int i = 0; i < nq; ++i) {
       ConvEpi ei = e;
       if (ei.fold.buf) ei.fold.launches = nq;  // the classes' launches all add into the BN sums
