@@ -1657,7 +1657,12 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
     a.tiles_k = a.g.K / 128;
     const int tiles = a.tiles_co * a.tiles_k;
     const int total_steps = (a.g.M + 63) / 64;
-    const int target = target_wgs > 0 ? target_wgs / 2 : 256;  // one workgroup per CU
+    static int big_target = -1;  // SL_WGRAD_BIG_TARGET: workgroup target of this kernel alone (A/B runs)
+    if (big_target < 0) {
+      const char* ev = getenv("SL_WGRAD_BIG_TARGET");
+      big_target = ev ? atoi(ev) : 0;
+    }
+    const int target = big_target > 0 ? big_target : target_wgs > 0 ? target_wgs / 2 : 256;  // one workgroup per CU
     int slices = tiles >= target ? 1 : (target + tiles - 1) / tiles;
     if (slices > total_steps) slices = total_steps;
     a.steps_per_slice = (total_steps + slices - 1) / slices;

@@ -141,7 +141,7 @@ def conv_dgrad(dy, wt, cin: int, k: int, stride: int, pad: int, dx, add=None, bn
 
 # split-K target for the implicit-GEMM weight gradient (workgroups per launch);
 # SL_WGRAD_WGS overrides it for A/B runs
-_WGRAD_WGS = int(os.environ.get("SL_WGRAD_WGS", "768"))  # swept 512..2048, profiles/r01_v16
+_WGRAD_WGS = int(os.environ.get("SL_WGRAD_WGS", "384"))  # re-swept on round-5 kernels: profiles/r05_sweep
 
 
 NEED_WS = 7  # csrc/kernels/common.h SL_NEED_WS
