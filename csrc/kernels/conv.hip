@@ -744,6 +744,235 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 }
 
 // ---------------------------------------------------------------------------
+// Stride-2 3x3 (pad 1) data gradient, all four parity classes in ONE workgroup
+// (SL_CONV_S2_FUSED).  Output pixel (2i+ph, 2j+pw) of class (ph, pw) sums
+// dY[i+dh][j+dw] . Wt[tap] over its taps, and every (class, tap) pair reads one
+// of only FOUR shifted windows of dY: (dh, dw) in {0,1}^2.  The per-class GEMMs
+// (the phase launches above) gather dY once per pair, 9 windows per tile, and
+// the L2 -> LDS fill of those gathers is what bounds them (profiles/r04_dgrad:
+// the GEMM core at ~4x its HBM bound).  Here a workgroup owns BM dY positions
+// (i, j) x BN input channels of ALL four classes: per 32-channel chunk it stages
+// each window once (4 A tiles) with the weight tiles of the pairs that read it
+// (4 + 2 + 2 + 1 B tiles) and accumulates into four register tiles.
+//
+//   window (0,0): (class (0,0), tap (1,1)), ((0,1), (1,2)), ((1,0), (2,1)), ((1,1), (2,2))
+//   window (0,1): ((0,1), (1,0)), ((1,1), (2,0))
+//   window (1,0): ((1,0), (0,1)), ((1,1), (0,2))
+//   window (1,1): ((1,1), (0,0))
+//
+// Stages are 32 deep (one 16x16x32 MFMA step): 64-B LDS rows, 16-B chunk c of row
+// r at position c ^ ((r >> 2) & 3) (the 16 rows of a fragment read then cover 16
+// distinct bank groups); a slot = A (BM rows) + up to four B tiles (BN rows); three
+// slots (two stages in flight): 72 KB at BM = 128, BN = 64, two workgroups per CU.
+// Epilogue per class: the bf16 tile through LDS, residual add (class (0, 0) only
+// with add_even), fused BN backward (bn_bwd_epi.h: sums over all four classes).
+// ---------------------------------------------------------------------------
+#ifndef SL_CONV_S2_FUSED
+#define SL_CONV_S2_FUSED 1
+#endif
+namespace {
+constexpr int S2_BK = 32;
+__device__ __forceinline__ int s2_swz(int c, int r) { return c ^ ((r >> 2) & 3); }
+// pairs of window w: count, class (ph * 2 + pw), weight tap (kh * 3 + kw)
+__host__ __device__ constexpr int s2_npairs(int w) { return w == 0 ? 4 : w == 3 ? 1 : 2; }
+__host__ __device__ constexpr int s2_cls(int w, int q) {
+  return w == 0 ? q : w == 1 ? (q == 0 ? 1 : 3) : w == 2 ? (q == 0 ? 2 : 3) : 3;
+}
+__host__ __device__ constexpr int s2_tap(int w, int q) {
+  return w == 0 ? (q == 0 ? 4 : q == 1 ? 5 : q == 2 ? 7 : 8) : w == 1 ? (q == 0 ? 3 : 6) : w == 2 ? (q == 0 ? 1 : 2) : 0;
+}
+}  // namespace
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(ConvGeom g, ConvEpi e, int tiles_n, int add_even) {
+  constexpr int MT = BM / 32, NT = BN / 32;      // 16x16 tiles per wave (2 x 2 waves)
+  constexpr int PA = BM / 64;                    // A pieces (16 rows x 64 B) per wave per stage
+  constexpr int PBQ = BN / 64;                   // B pieces per wave per pair
+  constexpr int A_EL = BM * S2_BK, B_EL = BN * S2_BK;
+  constexpr int SLOT = A_EL + 4 * B_EL;          // elements
+  constexpr int NSLOT = 3;
+  constexpr int CS_LD = BN + 8;
+  static_assert(BM * CS_LD <= NSLOT * SLOT, "epilogue tile must fit the ring");
+  static_assert(PA >= 1 && PBQ >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSLOT * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = logical / tiles_n, tn = logical - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // A rows of this lane: piece j covers rows 16 (wave * PA + j) .. +15 -> row + lane / 4,
+  // LDS chunk lane % 4 <- source chunk s2_swz(lane % 4, row)
+  int abase[PA], ai[PA], aj[PA];
+  bool aok[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int row = 16 * (wave * PA + j) + (lane >> 2);
+    const Pix p = decode_pix(g, m0 + row);
+    aok[j] = p.ok;
+    ai[j] = p.oh;
+    aj[j] = p.ow;
+    abase[j] = ((p.n * g.SH + p.oh) * g.SW + p.ow) * g.SC + s2_swz(lane & 3, row) * 8;
+  }
+  int bbase[PBQ];
+  bool bok[PBQ];
+#pragma unroll
+  for (int j = 0; j < PBQ; ++j) {
+    const int row = 16 * (wave * PBQ + j) + (lane >> 2);
+    const int col = n0 + row;
+    bok[j] = col < e.ncols;
+    bbase[j] = col * g.wld + s2_swz(lane & 3, row) * 8;
+  }
+  // stage s = 4 * chunk + window
+  auto issue = [&](int s, auto wc) __attribute__((always_inline)) {
+    constexpr int W = decltype(wc)::value;
+    constexpr int DH = W >> 1, DW = W & 1;
+    uint16_t* As = smem + (s % NSLOT) * SLOT;
+    const int ch0 = (s >> 2) * S2_BK;
+    const int soff = (DH * g.SW + DW) * g.SC + ch0;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const bool v = aok[j] && ai[j] + DH < g.SH && aj[j] + DW < g.SW;
+      glds16(v ? g.src + (abase[j] + soff) : g_conv_zero, (SL_LDS void*)(As + (wave * PA + j) * 16 * S2_BK));
+    }
+#pragma unroll
+    for (int q = 0; q < s2_npairs(W); ++q) {
+      uint16_t* Bs = As + A_EL + q * B_EL;
+      const int kb = s2_tap(W, q) * g.SC + ch0;
+#pragma unroll
+      for (int j = 0; j < PBQ; ++j)
+        glds16(bok[j] ? e.w + (bbase[j] + kb) : g_conv_zero, (SL_LDS void*)(Bs + (wave * PBQ + j) * 16 * S2_BK));
+    }
+  };
+
+  uint32_t aoff[MT], boff[NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int r = wm * (BM / 2) + i * 16 + lr;
+    aoff[i] = (uint32_t)((r * S2_BK + s2_swz(lg, r) * 8) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int r = wn * (BN / 2) + j * 16 + lr;
+    boff[j] = (uint32_t)((r * S2_BK + s2_swz(lg, r) * 8) * 2);
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
+
+  floatx4_t acc[4][MT][NT];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[c][i][j] = zero4();
+
+  const int nchunk = g.SC / S2_BK;
+  const int nk = 4 * nchunk;
+  using W0 = std::integral_constant<int, 0>;
+  using W1 = std::integral_constant<int, 1>;
+  using W2 = std::integral_constant<int, 2>;
+  using W3 = std::integral_constant<int, 3>;
+  issue(0, W0{});
+  issue(1, W1{});
+  auto stage = [&](int s, auto wc) __attribute__((always_inline)) {
+    constexpr int W = decltype(wc)::value;
+    constexpr int WN1 = (W + 1) & 3, WN2 = (W + 2) & 3;
+    // stage s landed once only stage s + 1's pieces (if issued) remain outstanding
+    if (s + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PA + s2_npairs(WN1) * PBQ) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // everyone's pieces landed; slot (s - 1) % 3 is free
+    if (s + 2 < nk) issue(s + 2, std::integral_constant<int, WN2>{});
+    const uint32_t sb = lds0 + (uint32_t)((s % NSLOT) * SLOT * 2);
+    short8_t af[MT], bf[4][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) af[i] = ds_b128(sb + aoff[i]);
+#pragma unroll
+    for (int q = 0; q < s2_npairs(W); ++q)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[q][j] = ds_b128(sb + (uint32_t)((A_EL + q * B_EL) * 2) + boff[j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < s2_npairs(W); ++q)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[s2_cls(W, q)][i][j] = mfma16(af[i], bf[q][j], acc[s2_cls(W, q)][i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int c = 0; c < nchunk; ++c) {
+    stage(4 * c + 0, W0{});
+    stage(4 * c + 1, W1{});
+    stage(4 * c + 2, W2{});
+    stage(4 * c + 3, W3{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue, one class at a time: bf16 tile through LDS -> 16-B row stores ----
+  constexpr int CPR = BN / 8;
+  constexpr int EIT = BM * CPR / 256;
+  const int cc = (tid % CPR) * 8, col = n0 + cc;
+  const bool full = col + 8 <= e.ncols;
+  const bool bnb = e.bn.x != nullptr;
+  BnbAcc bacc;
+  float msc[8], msh[8];
+  if (bnb) bnb_init(e.bn, e.ncols, full ? col : 0, bacc, msc, msh);
+  uint16_t* Cs = smem;
+#pragma unroll
+  for (int cls = 0; cls < 4; ++cls) {
+    const int ph = cls >> 1, pw = cls & 1;
+    const uint16_t* eadd = (add_even && cls) ? nullptr : e.add;
+    if (cls) __syncthreads();  // the previous class's staging reads are done
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int cl = wn * (BN / 2) + j * 16 + lr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cs[(wm * (BM / 2) + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[cls][i][j][r]);
+      }
+    long eoff[EIT];
+    short8_t ea[EIT];
+    BnbIn ebn[EIT];
+#pragma unroll
+    for (int it = 0; it < EIT; ++it) {
+      const int row = m0 + tid / CPR + it * (256 / CPR);
+      const Pix q = decode_pix(g, row);
+      eoff[it] = (((long)q.n * g.FH + 2 * q.oh + ph) * g.FW + 2 * q.ow + pw) * e.ldy + col;
+      const bool ok = row < g.M && full;
+      if (ok && eadd) ea[it] = ld8(eadd + eoff[it]);
+      if (ok && bnb) bnb_load(e.bn, eoff[it], ebn[it]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < EIT; ++it) {
+      const int rl = tid / CPR + it * (256 / CPR), row = m0 + rl;
+      if (row >= g.M || !full) continue;  // the host guarantees ncols % 8 == 0
+      short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+      if (eadd) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
+      }
+      if (bnb) bnb_chunk(e.bn, ebn[it], v, msc, msh, bacc);
+      *reinterpret_cast<short8_t*>(e.y + eoff[it]) = v;
+    }
+  }
+  if (bnb) {
+    __syncthreads();
+    bnb_fold<256, CPR>(e.bn, bacc, reinterpret_cast<float*>(smem), n0, e.ncols);
+  }
+  rsum_arrive(e.fold);
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradient.  Output tile BMO (co) x 128 (k); the batch*pixel index m is
 // the reduction, split into `slices` contiguous ranges.  Per stage, 64 m-rows
 // of dY [m][co] (BMO wide) and of im2col(X) [m][k] (128 wide) land as
@@ -1353,6 +1582,14 @@ extern "C" int sl_rsum_fold2(float* buf, float* buf2, int n, hipStream_t stream)
 extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream) { return sl_rsum_fold2(buf, nullptr, n, stream); }
 
 static int g_conv_phase = 1;  // stride-2 dgrad by parity classes (sl_conv_set_phase)
+static int s2_enabled() {  // SL_CONV_S2=0: the parity-class GEMM launches instead (A/B runs)
+  static int v = -1;
+  if (v < 0) {
+    const char* ev = getenv("SL_CONV_S2");
+    v = (ev && ev[0] == '0') ? 0 : 1;
+  }
+  return v;
+}
 #ifndef SL_CONV_PHASE_MERGE
 #define SL_CONV_PHASE_MERGE 1  // all parity classes of one data gradient in ONE launch
 #endif
@@ -1410,6 +1647,20 @@ static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, in
   const bool phase_ok = stride == 2 && KH == KW && ((KH == 3 && pad == 1) || (KH == 1 && pad == 0)) &&
                         (ldd & 63) == 0;
   if ((add_even || even_only) && !phase_ok) return -5;
+  if (SL_CONV_S2_FUSED && s2_enabled() && phase_ok && KH == 3 && !even_only && g_conv_phase && !(H & 1) && !(W & 1) &&
+      (ldd % S2_BK) == 0 && (cin & 7) == 0 && g.SH * 2 == H && g.SW * 2 == W) {
+    // all four parity classes in one workgroup (conv_dgrad_s2_kernel)
+    ConvGeom q = g;
+    q.OH = H / 2; q.OW = W / 2; q.hw_shift = ilog2(q.OH * q.OW); q.w_shift = ilog2(q.OW);
+    q.M = N * q.OH * q.OW; q.FH = H; q.FW = W; q.wld = KH * KW * ldd;
+    constexpr int BM = 128, BN = 64;
+    const int tiles_n = (cin + BN - 1) / BN;
+    const long grid = (long)((q.M + BM - 1) / BM) * tiles_n;
+    hipLaunchKernelGGL((conv_dgrad_s2_kernel<BM, BN>), dim3((unsigned)grid), dim3(256), 0, stream, q, e, tiles_n,
+                       add_even ? 1 : 0);
+    SL_CHECK_LAUNCH();
+    return 0;
+  }
   if (((g_conv_phase && KH == 3) || add_even || even_only) && phase_ok) {
     // parity classes of dX, each a dense GEMM over its own taps: (ph + pad - kh) even, dy row
     // (oh + pad - kh) / 2 = i + (ph + pad - kh) / 2 -- 1, 2, 2, 4 of the 9 taps of a 3x3/p1
