@@ -783,14 +783,15 @@ __host__ __device__ constexpr int s2_tap(int w, int q) {
 }
 }  // namespace
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(ConvGeom g, ConvEpi e, int tiles_n, int add_even) {
+template <int BM, int BN, int NSLOT, int OCC>
+__global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, ConvEpi e, int tiles_n, int add_even) {
   constexpr int MT = BM / 32, NT = BN / 32;      // 16x16 tiles per wave (2 x 2 waves)
   constexpr int PA = BM / 64;                    // A pieces (16 rows x 64 B) per wave per stage
   constexpr int PBQ = BN / 64;                   // B pieces per wave per pair
   constexpr int A_EL = BM * S2_BK, B_EL = BN * S2_BK;
   constexpr int SLOT = A_EL + 4 * B_EL;          // elements
-  constexpr int NSLOT = 3;
+  constexpr int AHEAD = NSLOT - 1;               // stages in flight
+  static_assert(AHEAD == 1 || AHEAD == 2, "2- or 3-slot ring");
   constexpr int CS_LD = BN + 8;
   static_assert(BM * CS_LD <= NSLOT * SLOT, "epilogue tile must fit the ring");
   static_assert(PA >= 1 && PBQ >= 1, "tile too small");
@@ -876,18 +877,18 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(ConvGeom g, ConvE
   using W2 = std::integral_constant<int, 2>;
   using W3 = std::integral_constant<int, 3>;
   issue(0, W0{});
-  issue(1, W1{});
+  if constexpr (AHEAD == 2) issue(1, W1{});
   auto stage = [&](int s, auto wc) __attribute__((always_inline)) {
     constexpr int W = decltype(wc)::value;
-    constexpr int WN1 = (W + 1) & 3, WN2 = (W + 2) & 3;
+    constexpr int WN1 = (W + 1) & 3, WNA = (W + AHEAD) & 3;
     // stage s landed once only stage s + 1's pieces (if issued) remain outstanding
-    if (s + 1 < nk) {
+    if (AHEAD == 2 && s + 1 < nk) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PA + s2_npairs(WN1) * PBQ) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __builtin_amdgcn_s_barrier();  // everyone's pieces landed; slot (s - 1) % 3 is free
-    if (s + 2 < nk) issue(s + 2, std::integral_constant<int, WN2>{});
+    __builtin_amdgcn_s_barrier();  // everyone's pieces landed; slot (s - 1) % NSLOT is free
+    if (s + AHEAD < nk) issue(s + AHEAD, std::integral_constant<int, WNA>{});
     const uint32_t sb = lds0 + (uint32_t)((s % NSLOT) * SLOT * 2);
     short8_t af[MT], bf[4][NT];
 #pragma unroll
@@ -1582,6 +1583,14 @@ extern "C" int sl_rsum_fold2(float* buf, float* buf2, int n, hipStream_t stream)
 extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream) { return sl_rsum_fold2(buf, nullptr, n, stream); }
 
 static int g_conv_phase = 1;  // stride-2 dgrad by parity classes (sl_conv_set_phase)
+static int s2_wide() {  // SL_CONV_S2_WIDE (A/B runs): tile of the >= 128-channel data gradients
+  static int v = -1;
+  if (v < 0) {
+    const char* ev = getenv("SL_CONV_S2_WIDE");
+    v = ev ? atoi(ev) : 0;
+  }
+  return v;
+}
 static int s2_enabled() {  // SL_CONV_S2=0: the parity-class GEMM launches instead (A/B runs)
   static int v = -1;
   if (v < 0) {
@@ -1653,11 +1662,17 @@ static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, in
     ConvGeom q = g;
     q.OH = H / 2; q.OW = W / 2; q.hw_shift = ilog2(q.OH * q.OW); q.w_shift = ilog2(q.OW);
     q.M = N * q.OH * q.OW; q.FH = H; q.FW = W; q.wld = KH * KW * ldd;
-    constexpr int BM = 128, BN = 64;
+    // 64 input channels: 128 x 64 tiles, 3-slot ring, two workgroups per CU; wider: a 128-channel
+    // tile so each dY window is staged once per 128 channels (SL_CONV_S2_WIDE: 1 = 64 x 128 with
+    // a 3-slot ring, one workgroup per CU; 2 = 64 x 128 with a 2-slot ring, two per CU; 0 = off)
+    const int wide = cin >= 128 && (cin % 128) == 0 ? s2_wide() : 0;
+    const int BM = wide ? 64 : 128, BN = wide ? 128 : 64;
     const int tiles_n = (cin + BN - 1) / BN;
-    const long grid = (long)((q.M + BM - 1) / BM) * tiles_n;
-    hipLaunchKernelGGL((conv_dgrad_s2_kernel<BM, BN>), dim3((unsigned)grid), dim3(256), 0, stream, q, e, tiles_n,
-                       add_even ? 1 : 0);
+    const dim3 grid((unsigned)((long)((q.M + BM - 1) / BM) * tiles_n));
+    const int ae = add_even ? 1 : 0;
+    if (wide == 1) hipLaunchKernelGGL((conv_dgrad_s2_kernel<64, 128, 3, 1>), grid, dim3(256), 0, stream, q, e, tiles_n, ae);
+    else if (wide == 2) hipLaunchKernelGGL((conv_dgrad_s2_kernel<64, 128, 2, 2>), grid, dim3(256), 0, stream, q, e, tiles_n, ae);
+    else hipLaunchKernelGGL((conv_dgrad_s2_kernel<128, 64, 3, 2>), grid, dim3(256), 0, stream, q, e, tiles_n, ae);
     SL_CHECK_LAUNCH();
     return 0;
   }
