@@ -102,6 +102,18 @@ __device__ __forceinline__ short8_t u8x8_to_bf16(uint2 v, float a, float b) {
   return r;
 }
 
+// Two waves per SIMD in one workgroup: the second-dispatched half loses issue arbitration to
+// the older half at every segment (priority, then age: MI355X_MICROARCH.md, two waves per
+// SIMD).  SL_WAVE_PRIO: that half raises its priority once, before the main loop (measured
+// neutral on the 8-wave conv and MLP weight-gradient kernels: profiles/r05_ce; off).
+#ifndef SL_WAVE_PRIO
+#define SL_WAVE_PRIO 0
+#endif
+__device__ __forceinline__ void younger_half_prio() {
+  if (SL_WAVE_PRIO && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= (int)(blockDim.x >> 7))
+    __builtin_amdgcn_s_setprio(1);
+}
+
 // XCD-aware bijective remap of a 1-D grid (cdna_hip_programming.md §5 T1):
 // consecutive logical tiles land on the same XCD so they share its L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

@@ -511,6 +511,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 
 template <bool TRANSPOSED>
 __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
+  younger_half_prio();
   constexpr int BM = 256, BN = 128, NSLOT = 3;
   constexpr int MT = 4, NT = 4;     // 16 x 16 MFMA tiles per wave (64 x 64)
   constexpr int PA = 4, PB = 2;     // DMA pieces (8 rows x 64 k, 1 KB) per wave per stage
@@ -1272,6 +1273,7 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
 #define SL_WGRAD_BIG 1
 #endif
 __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
+  younger_half_prio();
   constexpr int BMO = 256, BNO = 128, NSLOT = 3, WGM = 64;
   constexpr int WA = BMO / 8, WB = BNO / 8;       // 16-B chunks per image row: 32 / 16
   constexpr int MT = 4, NT = 4;                   // 64 x 64 per wave (4 co x 2 k waves)

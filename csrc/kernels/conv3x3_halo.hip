@@ -116,6 +116,7 @@ __device__ __forceinline__ int cs_swz(int p, int chunk) { return p * (HC * 2) + 
 // apply BN-on-load (a.bin).  Separate instances, so neither carries the other's registers.
 template <int CIN, bool DEFER, bool BNB>
 __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
+  younger_half_prio();
   using L = Lay<CIN>;
   constexpr int HL = (L::HALO_CHUNKS + NTF - 1) / NTF;  // halo chunks per thread
   static_assert(!DEFER || L::REGION + L::W_BYTES + DEFER_BYTES <= 160 * 1024, "deferred image must fit LDS");
@@ -641,6 +642,7 @@ __global__ __launch_bounds__(256) void halo_wgrad_reduce_kernel(const float4* __
 }
 
 __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs a) {
+  younger_half_prio();
   __shared__ __attribute__((aligned(16))) uint8_t smem[WX_BYTES + WY_BYTES];
   uint8_t* Xs = smem;
   uint8_t* Ys = smem + WX_BYTES;

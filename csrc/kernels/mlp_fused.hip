@@ -1135,6 +1135,7 @@ constexpr int WG_NJ = 2;  // 16-column B fragments per wave
 constexpr int WG_NF = WG_MI + WG_NJ;       // fragments per wave per k-step
 
 __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
+  younger_half_prio();
   __shared__ __attribute__((aligned(16))) uint16_t smem[WG_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
