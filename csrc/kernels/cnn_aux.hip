@@ -250,11 +250,14 @@ __global__ __launch_bounds__(256) void bn_apply_stats_kernel(const uint16_t* __r
                                                              const uint16_t* __restrict__ res, BnStats rb,
                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ mask_out,
                                                              long rows, int C, int relu, int mode, float count,
-                                                             float eps, float momentum) {
+                                                             float eps, float momentum, int consume) {
   const int cpr = C >> 3;
   const long total = rows * cpr;
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(t0 % cpr) * 8;
+  __shared__ float fold_b[SL_RSUM_LDS], fold_r[SL_RSUM_LDS];
+  b.stats = rsum_consume(b.stats, 2 * C, fold_b, consume);
+  if (mode >= 2) rb.stats = rsum_consume(rb.stats, 2 * C, fold_r, consume);
   float sc[8], sh[8], rsc[8], rsh[8];
   bn_coef8(b, C, c0, count, eps, sc, sh);
   if (mode >= 2) bn_coef8(rb, C, c0, count, eps, rsc, rsh);
@@ -306,11 +309,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_sums_kernel(const uint16_t* 
                                                                 float* __restrict__ grad_gamma,
                                                                 float* __restrict__ grad_beta,
                                                                 uint16_t* __restrict__ dx, long rows, int C,
-                                                                float count) {
+                                                                float count, int consume) {
   const int cpr = C >> 3;
   const long total = rows * cpr;
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(t0 % cpr) * 8;
+  __shared__ float fold_s[SL_RSUM_LDS];
+  sums = rsum_consume(sums, 2 * C, fold_s, consume);
   float ca[8], cb[8], cc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -378,11 +383,15 @@ __device__ __forceinline__ void bn_bwd_abc8(const BnBwdSide& b, int C, int c0, f
 // bn_bwd_apply_sums for the two BNs of a downsample block (bn2 on c2, the
 // shortcut's BN on cs), which share dz: dz is read once for both dx outputs.
 __global__ __launch_bounds__(256) void bn_bwd_apply_dual_kernel(const uint16_t* __restrict__ dz, BnBwdSide a,
-                                                                BnBwdSide b, long rows, int C, float count) {
+                                                                BnBwdSide b, long rows, int C, float count,
+                                                                int consume) {
   const int cpr = C >> 3;
   const long total = rows * cpr;
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(t0 % cpr) * 8;
+  __shared__ float fold_a[SL_RSUM_LDS], fold_b[SL_RSUM_LDS];
+  a.sums = rsum_consume(a.sums, 2 * C, fold_a, consume);
+  b.sums = rsum_consume(b.sums, 2 * C, fold_b, consume);
   float aa[8], ab[8], ac[8], ba[8], bb[8], bc[8];
   bn_bwd_abc8(a, C, c0, count, aa, ab, ac);
   bn_bwd_abc8(b, C, c0, count, ba, bb, bc);
@@ -596,6 +605,7 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict
 
 // ---------------------------------------------------------------------------
 extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream);  // conv.hip
+extern "C" int sl_rsum_defer();  // conv.hip
 extern "C" int sl_rsum_fold2(float* buf, float* buf2, int n, hipStream_t stream);  // conv.hip
 
 extern "C" {
@@ -663,7 +673,7 @@ int sl_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, stream, dy, y, x, mcoef, ymask, dz_out, sums, x2, sums2, rows,
                      C, rsum_fold_spec(sums, x2 ? sums2 : nullptr, 2 * C, 1));
   SL_CHECK_LAUNCH();
-  if (SL_RSUM_ARRIVE) return 0;
+  if (SL_RSUM_ARRIVE || (sl_rsum_defer() && 2 * C <= SL_RSUM_LDS)) return 0;
   if (int rc = sl_rsum_fold2(sums, x2 ? sums2 : nullptr, 2 * C, stream)) return rc;
   return 0;
 }
@@ -697,7 +707,7 @@ int sl_bn_apply_stats(const uint16_t* x, const float* stats, const float* gamma,
   BnStats b{stats, gamma, beta, coef, run_mean, run_var};
   BnStats rb{rstats, rgamma, rbeta, rcoef, rrun_mean, rrun_var};
   hipLaunchKernelGGL(bn_apply_stats_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0, stream, x, b, res, rb, y,
-                     mask_out, rows, C, relu, mode, count, eps, momentum);
+                     mask_out, rows, C, relu, mode, count, eps, momentum, sl_rsum_defer());
   SL_CHECK_LAUNCH();
   return 0;
 }
@@ -710,7 +720,7 @@ int sl_bn_bwd_apply_dual(const uint16_t* dz, const uint16_t* xa, const float* su
   BnBwdSide a{xa, sums_a, coef_a, gg_a, gb_a, dx_a};
   BnBwdSide b{xb, sums_b, coef_b, gg_b, gb_b, dx_b};
   hipLaunchKernelGGL(bn_bwd_apply_dual_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0,
-                     stream, dz, a, b, rows, C, count);
+                     stream, dz, a, b, rows, C, count, sl_rsum_defer());
   SL_CHECK_LAUNCH();
   return 0;
 }
@@ -720,7 +730,7 @@ int sl_bn_bwd_apply_sums(const uint16_t* dy, const uint16_t* y, const uint16_t* 
                          float count, hipStream_t stream) {
   if ((C & 7) || 256 % (C / 8) != 0) return -1;
   hipLaunchKernelGGL(bn_bwd_apply_sums_kernel, dim3(blocks_for(rows * (C / 8), bn_apply_cap())), dim3(256), 0, stream, dy, y, x, mcoef,
-                     sums, coef, grad_gamma, grad_beta, dx, rows, C, count);
+                     sums, coef, grad_gamma, grad_beta, dx, rows, C, count, sl_rsum_defer());
   SL_CHECK_LAUNCH();
   return 0;
 }

@@ -171,8 +171,23 @@ __host__ __device__ __forceinline__ double fix_value(const unsigned long long* p
   return (double)(long long)p[0] * (1.0 / SL_FIX_HI) + (double)(long long)p[1] * (1.0 / SL_FIX_LO);
 }
 
+// Consumer-side fold (SL_RSUM_CONSUMER=1; default off: measured 1.6 % slower, profiles/r05_cons --
+// every consumer workgroup's 16 KB fold prologue costs more than the fold launch it removes):
+// the kernels that read a folded row
+// (BN apply, BN-backward apply, the direct 3x3 conv's BN-on-load) sum the replicas into LDS in
+// their prologue, and their workgroup 0 also writes the result row for later readers, so the
+// producer needs no fold launch when the host defers it (sl_rsum_set_defer; the ResNet engine
+// does so for its step).  For that, n values x the replicas in use stay within 16 KB:
+// rsum_reps(n) = min(SL_REP, 4096 / n) (64 channels: 32, 128: 16, 256: 8, 512: 4).
+#ifndef SL_RSUM_CONSUMER
+#define SL_RSUM_CONSUMER 0
+#endif
+constexpr int SL_RSUM_LDS = 1024;  // largest n folded in a consumer (C <= 512)
+__host__ __device__ constexpr int rsum_reps(int n) {
+  return !SL_RSUM_CONSUMER ? SL_REP : (4096 / n >= SL_REP ? SL_REP : (4096 / n < 1 ? 1 : 4096 / n));
+}
 __device__ __forceinline__ float* rsum_replica(float* buf, int n) {
-  return SL_DETERMINISTIC ? buf : buf + (long)(blockIdx.x % SL_REP) * n;
+  return SL_DETERMINISTIC ? buf : buf + (long)(blockIdx.x % rsum_reps(n)) * n;
 }
 __device__ __forceinline__ float* rsum_result(float* buf, int n) { return buf + (long)SL_REP * n; }
 // add v to entry i of a replica returned by rsum_replica
@@ -230,6 +245,68 @@ __device__ __forceinline__ void rsum_fold_row(float* buf, int n, int tid, int nt
     res[i] = acc;
 #endif
   }
+}
+
+// Consumer prologue: the folded n values of the rsum buffer whose result row is `res`, in
+// `lds` (SL_RSUM_LDS floats); workgroup 0 also stores them to the result row.  Every thread
+// calls it (it ends with a workgroup barrier); res null or on == 0 (the launcher ran outside a
+// deferral: res is a folded row, or any plain array of n values): returns res.
+__device__ __forceinline__ const float* rsum_consume(const float* res, int n, float* lds, int on) {
+  if (!SL_RSUM_CONSUMER || !on || !res || n > SL_RSUM_LDS) return res;
+  const float* buf = res - (long)SL_REP * n;
+#if SL_DETERMINISTIC
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float acc = (float)fix_value(reinterpret_cast<const unsigned long long*>(buf) + 2 * i);
+    lds[i] = acc;
+    if (blockIdx.x == 0) const_cast<float*>(res)[i] = acc;
+  }
+#else
+  // every thread issues its (at most 16) replica loads at once: R * n <= 4096 values over the
+  // workgroup; n <= blockDim: tpe threads per value, each summing R / tpe replicas into LDS
+  const int R = rsum_reps(n), tid = threadIdx.x, nt = blockDim.x;
+  if (n <= nt) {
+    const int tpe = nt / n, e = tid % n, g = tid / n;
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int r = g + k * tpe;
+      v[k] = (g < tpe && r < R) ? buf[(long)r * n + e] : 0.f;
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += v[k];
+    if (g < tpe) lds[g * n + e] = acc;  // tpe * n <= nt <= SL_RSUM_LDS
+    __syncthreads();
+    if (tid < n) {
+      float t = lds[tid];
+      for (int q = 1; q < tpe; ++q) t += lds[q * n + tid];
+      lds[tid] = t;
+      if (blockIdx.x == 0) const_cast<float*>(res)[tid] = t;
+    }
+  } else {  // n = 512 / 1024: R <= 8, at most 4 values per thread
+    float v[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int e = tid + j * nt;
+        v[j][r] = (e < n && r < R) ? buf[(long)r * n + e] : 0.f;
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + j * nt;
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) t += v[j][r];
+      if (e < n) {
+        lds[e] = t;
+        if (blockIdx.x == 0) const_cast<float*>(res)[e] = t;
+      }
+    }
+  }
+#endif
+  __syncthreads();
+  return lds;
 }
 
 // host: the fold a producer launch carries (none when the separate fold launch is used)

@@ -52,6 +52,9 @@ using namespace sl;
 #ifndef SL_WGRAD_SHIFT
 #define SL_WGRAD_SHIFT 1  // conv_wgrad: shift-only gather addressing for power-of-two shapes
 #endif
+#ifndef SL_MFMA_PRIO
+#define SL_MFMA_PRIO 0  // s_setprio 1 around the big GEMM / weight-gradient MFMA clusters (A/B knob)
+#endif
 #ifndef SL_GEMM128_SLOTS
 #define SL_GEMM128_SLOTS 2
 #endif
@@ -639,10 +642,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
       if (h == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(MT + NT) : "memory");
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      if (SL_MFMA_PRIO) __builtin_amdgcn_s_setprio(1);  // (cdna_hip_programming.md T5)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[h][i], bf[h][j], acc[i][j]);
+      if (SL_MFMA_PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1375,10 +1380,12 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
       if (h == 0) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");  // h0 landed (counter max 15 < 16 h1 reads)
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      if (SL_MFMA_PRIO) __builtin_amdgcn_s_setprio(1);  // (cdna_hip_programming.md T5)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[h][i], bf[h][j], acc[i][j]);
+      if (SL_MFMA_PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1584,6 +1591,16 @@ extern "C" int sl_rsum_fold2(float* buf, float* buf2, int n, hipStream_t stream)
 
 extern "C" int sl_rsum_fold(float* buf, int n, hipStream_t stream) { return sl_rsum_fold2(buf, nullptr, n, stream); }
 
+// Deferred folds (SL_RSUM_CONSUMER): while on, the producers' launchers skip their fold launch
+// and the consuming kernels fold in their prologue (common.h rsum_consume).  The ResNet engine
+// turns it on around its forward / backward; standalone calls (tests) keep the fold launches.
+static int g_rsum_defer = 0;
+extern "C" int sl_rsum_set_defer(int on) {
+  g_rsum_defer = SL_RSUM_CONSUMER ? on : 0;
+  return 0;
+}
+extern "C" int sl_rsum_defer() { return g_rsum_defer; }
+
 static int g_conv_phase = 1;  // stride-2 dgrad by parity classes (sl_conv_set_phase)
 static int s2_wide() {  // SL_CONV_S2_WIDE (A/B runs): tile of the >= 128-channel data gradients
   static int v = -1;
@@ -1635,7 +1652,7 @@ int sl_conv_fwd(const uint16_t* x, int N, int H, int W, int C, const uint16_t* w
     ConvEpi e{w, cout, y, ldy, yf, bias, nullptr, stats, {}, rsum_fold_spec(stats, nullptr, 2 * cout, 1)};
     rc = launch_gemm<false>(g, e, stream);
   }
-  if (rc || !stats || SL_RSUM_ARRIVE) return rc;
+  if (rc || !stats || SL_RSUM_ARRIVE || (g_rsum_defer && 2 * cout <= SL_RSUM_LDS)) return rc;
   return sl_rsum_fold(stats, 2 * cout, stream);
 }
 
@@ -1760,7 +1777,7 @@ int sl_conv_dgrad_bn(const uint16_t* dy, int N, int OH, int OW, int ldd, const u
   if (add_even && !add) return -5;
   int rc = dgrad_launch(g, dy, N, OH, OW, ldd, wt, cin, KH, KW, stride, pad, H, W, dx, add, fuse ? bn : nullptr,
                         stream, add_even != 0);
-  if (rc || !fuse || SL_RSUM_ARRIVE) return rc;
+  if (rc || !fuse || SL_RSUM_ARRIVE || (g_rsum_defer && 2 * cin <= SL_RSUM_LDS)) return rc;
   return sl_rsum_fold2(bn->sums, bn->x2 ? bn->sums2 : nullptr, 2 * cin, stream);
 }
 

@@ -103,6 +103,7 @@ struct HaloArgs {
   BnStats bin;
   float bin_count, bin_eps, bin_momentum;
   RsumFold fold;        // stats or bn.sums, folded by the last workgroup (common.h)
+  int bin_consume;      // bin.stats is an unfolded rsum buffer's result row: fold it here (rsum_consume)
 };
 
 // DEFER (plain forward: no residual, no fused BN backward): the bf16 output tile is staged in
@@ -155,8 +156,12 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   const bool bni = CIN == 64 && !BNB && a.bin.stats != nullptr;
   float isc[8], ish[8];
   if (bni) {
-    bn_coef8(a.bin, HC, (tid & 7) * 8, a.bin_count, a.bin_eps, isc, ish);
-    if (blockIdx.x == 0) bn_publish(a.bin, HC, a.bin_count, a.bin_eps, a.bin_momentum);
+    // the input BN's replicas folded into the (still free) halo region (rsum_consume)
+    BnStats bs = a.bin;
+    bs.stats = rsum_consume(a.bin.stats, 2 * HC, reinterpret_cast<float*>(Hs), a.bin_consume);
+    bn_coef8(bs, HC, (tid & 7) * 8, a.bin_count, a.bin_eps, isc, ish);
+    if (blockIdx.x == 0) bn_publish(bs, HC, a.bin_count, a.bin_eps, a.bin_momentum);
+    __syncthreads();  // the fold's reads are done before the first halo lands in Hs
   }
 
   // ---- halo tile: global -> registers (prefetch) -> LDS ----
@@ -405,6 +410,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   rsum_arrive(a.fold);
 }
 
+extern "C" int sl_rsum_defer();  // conv.hip
 static int g_halo_enabled = -1;  // -1: from SL_CONV_HALO (default on)
 static int g_num_cus = 0;
 
@@ -451,6 +457,7 @@ static int conv3x3_launch(const uint16_t* src, const uint16_t* w, int cin, int f
   if (bn) a.bn = *bn;
   a.bin = BnStats{};
   a.bin_count = bin_count; a.bin_eps = bin_eps; a.bin_momentum = bin_momentum;
+  a.bin_consume = sl_rsum_defer();
   a.fold = stats ? rsum_fold_spec(stats, nullptr, 2 * HC, 1)
                  : rsum_fold_spec(bn ? bn->sums : nullptr, nullptr, 2 * HC, 1);
   if (bin) {
@@ -497,7 +504,7 @@ int sl_conv3x3_bnin_fwd(const uint16_t* x, const uint16_t* w, int N, int H, uint
                         float* run_var, float count, float eps, float momentum, hipStream_t stream) {
   const BnStats bin{bstats, gamma, beta, coef, run_mean, run_var};
   const int rc = conv3x3_launch(x, w, 64, 0, N, H, y, ldy, nullptr, stats, nullptr, &bin, count, eps, momentum, stream);
-  if (rc || !stats || SL_RSUM_ARRIVE) return rc;
+  if (rc || !stats || SL_RSUM_ARRIVE || sl_rsum_defer()) return rc;
   return sl_rsum_fold(stats, 2 * HC, stream);  // as sl_conv_fwd does after its epilogue sums
 }
 

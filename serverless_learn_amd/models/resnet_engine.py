@@ -241,6 +241,10 @@ class FusedResNetTrainer:
         K.conv_fwd(x, conv.w, c.cout, c.k, c.stride, c.pad, y=out, stats=bn.stats_buf)
 
     def forward(self, train: bool = True):
+        with self.K.rsum_deferred():  # BN-sum folds in the consuming kernels (ops/cnn.py)
+            return self._forward(train)
+
+    def _forward(self, train: bool = True):
         K, spec = self.K, self.spec
         self.arena.zero_()
         K.input_norm(self.x, self.y, self.cursor, self.batch, self.x0, self.labels, CIFAR_MEAN, CIFAR_STD)
@@ -284,6 +288,10 @@ class FusedResNetTrainer:
                      self.fc_gb if train else None, self.grad_scale)
 
     def backward(self):
+        with self.K.rsum_deferred():
+            return self._backward()
+
+    def _backward(self):
         K, spec = self.K, self.spec
         handles = []
         pending_from = spec.n_flat  # grad[pending_from:] is final and not yet reduced

@@ -34,6 +34,7 @@ N.register("sl_bn_bwd_finalize", [P, P, P, P, P, I, F, P])
 N.register("sl_bn_bwd_apply", [P, P, P, P, P, L, I, P])
 N.register("sl_rsum_floats", [I], ctypes.c_long)
 N.register("sl_rsum_result_offset", [I], ctypes.c_long)
+N.register("sl_rsum_set_defer", [I])
 N.register("sl_bn_apply_stats", [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, F, F, F, P])
 N.register("sl_bn_bwd_apply_sums", [P, P, P, P, P, P, P, P, P, L, I, F, P])
 N.register("sl_bn_bwd_apply_dual", [P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, F, P])
@@ -66,6 +67,21 @@ def _f32(t):
 def rsum_floats(n: int) -> int:
     """Size of a cross-workgroup sum buffer for n values (replicas | result | pad)."""
     return int(N.lib().sl_rsum_floats(n))
+
+
+class rsum_deferred:
+    """While active, the conv / BN-reduce launchers skip their separate BN-sum fold launch and
+    the consuming kernels fold the replicas in their prologue (csrc/kernels/common.h,
+    rsum_consume).  The ResNet engine wraps its forward and backward in it; standalone calls
+    (tests) keep folded result rows right after each producer."""
+
+    def __enter__(self):
+        N.call("sl_rsum_set_defer", 1)
+        return self
+
+    def __exit__(self, *exc):
+        N.call("sl_rsum_set_defer", 0)
+        return False
 
 
 def rsum_result(buf: torch.Tensor, n: int) -> torch.Tensor:
