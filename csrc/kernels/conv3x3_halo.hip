@@ -41,7 +41,7 @@ constexpr int TPIX = TR * IW;          // 256 output pixels per tile
 constexpr int HR = TR + 2, HCOL = IW + 2;  // halo 10 x 34 pixels
 constexpr int NTH = 256;
 #ifndef SL_HALO_WAVES
-#define SL_HALO_WAVES 8  // 8 measured +1% over 4 (two waves per SIMD)
+#define SL_HALO_WAVES 8  // 8 measured +1% over 4 (two waves per SIMD); the deferred forward needs 8
 #endif
 constexpr int NWF = SL_HALO_WAVES;     // waves of the forward / dgrad kernel
 #ifndef SL_HALO_DEFER
@@ -121,6 +121,8 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   using L = Lay<CIN>;
   constexpr int HL = (L::HALO_CHUNKS + NTF - 1) / NTF;  // halo chunks per thread
   static_assert(!DEFER || L::REGION + L::W_BYTES + DEFER_BYTES <= 160 * 1024, "deferred image must fit LDS");
+  // the deferred stores cover a tile in 4 passes of NTF / 8 pixels (k-step pairs 1, 3, 5, 7)
+  static_assert(!DEFER || 4 * NTF / 8 == TPIX, "DEFER needs 8 waves (SL_HALO_WAVES=4 stored half the tile)");
   __shared__ __attribute__((aligned(16))) uint8_t smem[L::REGION + L::W_BYTES + (DEFER ? DEFER_BYTES : 0)];
   uint8_t* Hs = smem;
   uint8_t* Ws = smem + L::REGION;
