@@ -317,6 +317,9 @@ __host__ __device__ inline RsumFold rsum_fold_spec(float* buf, float* buf2, int 
 // Every thread of the workgroup calls this once per launch, after all of the workgroup's
 // rsum_add calls into f.buf / f.buf2, in uniform control flow.
 __device__ __forceinline__ void rsum_arrive(const RsumFold& f) {
+#if !SL_RSUM_ARRIVE
+  (void)f;  // off: no ticket word, and no LDS word either (it would cost 4 B in every producer)
+#else
   if (!f.buf) return;
   __shared__ unsigned rsum_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's replica atomics are done
@@ -340,6 +343,7 @@ __device__ __forceinline__ void rsum_arrive(const RsumFold& f) {
     rsum_fold_row(f.buf, f.n, threadIdx.x, blockDim.x);
     if (f.buf2) rsum_fold_row(f.buf2, f.n, threadIdx.x, blockDim.x);
   }
+#endif
 }
 
 }  // namespace sl

@@ -797,7 +797,7 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
   constexpr int A_EL = BM * S2_BK, B_EL = BN * S2_BK;
   constexpr int SLOT = A_EL + 4 * B_EL;          // elements
   constexpr int AHEAD = NSLOT - 1;               // stages in flight
-  static_assert(AHEAD == 1 || AHEAD == 2, "2- or 3-slot ring");
+  static_assert(AHEAD >= 1 && AHEAD <= 3, "2- to 4-slot ring");
   constexpr int CS_LD = BN + 8;
   static_assert(BM * CS_LD <= NSLOT * SLOT, "epilogue tile must fit the ring");
   static_assert(PA >= 1 && PBQ >= 1, "tile too small");
@@ -883,13 +883,17 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
   using W2 = std::integral_constant<int, 2>;
   using W3 = std::integral_constant<int, 3>;
   issue(0, W0{});
-  if constexpr (AHEAD == 2) issue(1, W1{});
+  if constexpr (AHEAD >= 2) issue(1, W1{});
+  if constexpr (AHEAD >= 3) issue(2, W2{});
   auto stage = [&](int s, auto wc) __attribute__((always_inline)) {
     constexpr int W = decltype(wc)::value;
-    constexpr int WN1 = (W + 1) & 3, WNA = (W + AHEAD) & 3;
-    // stage s landed once only stage s + 1's pieces (if issued) remain outstanding
-    if (AHEAD == 2 && s + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PA + s2_npairs(WN1) * PBQ) : "memory");
+    constexpr int WN1 = (W + 1) & 3, WN2 = (W + 2) & 3, WNA = (W + AHEAD) & 3;
+    constexpr int P1 = PA + s2_npairs(WN1) * PBQ, P2 = PA + s2_npairs(WN2) * PBQ;  // pieces of s + 1, s + 2
+    // stage s landed once only the younger stages' pieces (those issued) remain outstanding
+    if (AHEAD == 3 && s + 2 < nk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P1 + P2) : "memory");
+    } else if (AHEAD >= 2 && s + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P1) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1684,13 +1688,16 @@ static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, in
     // 64 input channels: 128 x 64 tiles, 3-slot ring, two workgroups per CU; wider: a 128-channel
     // tile so each dY window is staged once per 128 channels (SL_CONV_S2_WIDE: 1 = 64 x 128 with
     // a 3-slot ring, one workgroup per CU; 2 = 64 x 128 with a 2-slot ring, two per CU; 0 = off)
+    // 3 = 64 x 64 tiles with a 4-slot ring (three stages in flight), two per CU: the deep
+    // stages' long k-loops (stage 4: 64 stages) wait on the LDS-DMA latency
     const int wide = cin >= 128 && (cin % 128) == 0 ? s2_wide() : 0;
-    const int BM = wide ? 64 : 128, BN = wide ? 128 : 64;
+    const int BM = wide ? 64 : 128, BN = wide == 1 || wide == 2 ? 128 : 64;
     const int tiles_n = (cin + BN - 1) / BN;
     const dim3 grid((unsigned)((long)((q.M + BM - 1) / BM) * tiles_n));
     const int ae = add_even ? 1 : 0;
     if (wide == 1) hipLaunchKernelGGL((conv_dgrad_s2_kernel<64, 128, 3, 1>), grid, dim3(256), 0, stream, q, e, tiles_n, ae);
     else if (wide == 2) hipLaunchKernelGGL((conv_dgrad_s2_kernel<64, 128, 2, 2>), grid, dim3(256), 0, stream, q, e, tiles_n, ae);
+    else if (wide == 3) hipLaunchKernelGGL((conv_dgrad_s2_kernel<64, 64, 4, 2>), grid, dim3(256), 0, stream, q, e, tiles_n, ae);
     else hipLaunchKernelGGL((conv_dgrad_s2_kernel<128, 64, 3, 2>), grid, dim3(256), 0, stream, q, e, tiles_n, ae);
     SL_CHECK_LAUNCH();
     return 0;
