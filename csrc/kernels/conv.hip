@@ -1614,19 +1614,23 @@ static int s2_wide() {  // SL_CONV_S2_WIDE (A/B runs): tile of the >= 128-channe
   }
   return v;
 }
-static int s2_enabled() {  // SL_CONV_S2=0: the parity-class GEMM launches instead (A/B runs)
-  static int v = -1;
-  if (v < 0) {
+static int g_conv_s2 = -1;  // -1: from SL_CONV_S2 (default on); sl_conv_set_s2 overrides
+static int s2_enabled() {  // off: the parity-class GEMM launches instead (A/B runs, tests)
+  if (g_conv_s2 < 0) {
     const char* ev = getenv("SL_CONV_S2");
-    v = (ev && ev[0] == '0') ? 0 : 1;
+    g_conv_s2 = (ev && ev[0] == '0') ? 0 : 1;
   }
-  return v;
+  return g_conv_s2;
 }
 #ifndef SL_CONV_PHASE_MERGE
 #define SL_CONV_PHASE_MERGE 1  // all parity classes of one data gradient in ONE launch
 #endif
 
 extern "C" {
+int sl_conv_set_s2(int on) {
+  g_conv_s2 = on ? 1 : 0;
+  return 0;
+}
 int sl_conv_set_phase(int on) {
   g_conv_phase = on;
   return 0;

@@ -35,6 +35,7 @@ N.register("sl_bn_bwd_apply", [P, P, P, P, P, L, I, P])
 N.register("sl_rsum_floats", [I], ctypes.c_long)
 N.register("sl_rsum_result_offset", [I], ctypes.c_long)
 N.register("sl_rsum_set_defer", [I])
+N.register("sl_conv_set_s2", [I])
 N.register("sl_bn_apply_stats", [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, I, F, F, F, P])
 N.register("sl_bn_bwd_apply_sums", [P, P, P, P, P, P, P, P, P, L, I, F, P])
 N.register("sl_bn_bwd_apply_dual", [P, P, P, P, P, P, P, P, P, P, P, P, P, L, I, F, P])

@@ -43,6 +43,24 @@ CONV_CASES = [
 
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_fwd_dgrad_wgrad(case):
+    _conv_case(case)
+
+
+# the stride-2 3x3 data gradients with the class-fused kernel switched off: all parity classes
+# in ONE implicit-GEMM launch (conv.hip, merged ConvGeom) -- the path the fused kernel replaced
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[4] == 3 and c[5] == 2 and c[1] % 2 == 0])
+def test_conv_stride2_dgrad_merged_gemm_path(case):
+    from serverless_learn_amd.ops import _native as N
+    from serverless_learn_amd.ops import cnn as K  # noqa: F401  (registers sl_conv_set_s2)
+
+    N.call("sl_conv_set_s2", 0)
+    try:
+        _conv_case(case)
+    finally:
+        N.call("sl_conv_set_s2", 1)
+
+
+def _conv_case(case):
     from serverless_learn_amd.ops import cnn as K
 
     n, h, c, cout, k, s, p = case
