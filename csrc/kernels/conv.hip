@@ -767,18 +767,32 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 //   window (1,1): ((1,1), (0,0))
 //
 // Stages are 32 deep (one 16x16x32 MFMA step): 64-B LDS rows, 16-B chunk c of row
-// r at position c ^ ((r >> 2) & 3) (the 16 rows of a fragment read then cover 16
-// distinct bank groups); a slot = A (BM rows) + up to four B tiles (BN rows); three
-// slots (two stages in flight): 72 KB at BM = 128, BN = 64, two workgroups per CU.
-// Epilogue per class: the bf16 tile through LDS, residual add (class (0, 0) only
-// with add_even), fused BN backward (bn_bwd_epi.h: sums over all four classes).
+// r at position c ^ g((r >> 2) & 3), g = {0, 2, 3, 1}: every ds_read_b128 lane group
+// ({0-3, 12-15, 20-27}, ... -- rows q and k-chunks 0 / 1 mixed) then hits 16 distinct
+// 16-B bank blocks.  (The round-5 first cut used g(q) = q, right for 16 contiguous lanes
+// but 2-way on the real groups: 45 % of LDS cycles were conflicts, profiles/r05_soak.)
+// A slot = A (BM rows) + up to four B tiles (BN rows); three slots (two stages in
+// flight): 72 KB at BM = 128, BN = 64, two workgroups per CU.
+// The MFMAs take the weight fragment as their first operand (C^T = B^T A^T), so a lane
+// accumulates 4 consecutive CHANNELS of one pixel: the epilogue stages a class's bf16
+// tile with one ds_write_b64 per 16x16 tile (4 x ds_write_b16 before), rows >= 8 of a
+// tile with the two 8-B halves of each 16-B chunk exchanged (conflict-free stores),
+// then residual add (class (0, 0) only with add_even), fused BN backward (bn_bwd_epi.h:
+// sums over all four classes).
 // ---------------------------------------------------------------------------
 #ifndef SL_CONV_S2_FUSED
 #define SL_CONV_S2_FUSED 1
 #endif
 namespace {
 constexpr int S2_BK = 32;
+#ifndef SL_S2_LAYOUT
+#define SL_S2_LAYOUT 1  // 0: the first cut's swizzle / MFMA orientation / b16 epilogue (A/B)
+#endif
+#if SL_S2_LAYOUT
+__device__ __forceinline__ int s2_swz(int c, int r) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }
+#else
 __device__ __forceinline__ int s2_swz(int c, int r) { return c ^ ((r >> 2) & 3); }
+#endif
 // pairs of window w: count, class (ph * 2 + pw), weight tap (kh * 3 + kw)
 __host__ __device__ constexpr int s2_npairs(int w) { return w == 0 ? 4 : w == 3 ? 1 : 2; }
 __host__ __device__ constexpr int s2_cls(int w, int q) {
@@ -915,7 +929,11 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
+#if SL_S2_LAYOUT
+          acc[s2_cls(W, q)][i][j] = mfma16(bf[q][j], af[i], acc[s2_cls(W, q)][i][j]);
+#else
           acc[s2_cls(W, q)][i][j] = mfma16(af[i], bf[q][j], acc[s2_cls(W, q)][i][j]);
+#endif
     __builtin_amdgcn_sched_barrier(0);
   };
   for (int c = 0; c < nchunk; ++c) {
@@ -946,9 +964,19 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
+#if SL_S2_LAYOUT
+        // lane: pixel row i * 16 + lr, channels j * 16 + 4 lg .. +3
+        const int rl = wm * (BM / 2) + i * 16 + lr;
+        const int cl = (wn * (BN / 2) + j * 16 + 4 * lg) ^ (((lr >> 3) & 1) << 2);
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(acc[cls][i][j][0]) | ((uint32_t)f2bf(acc[cls][i][j][1]) << 16);
+        pk.y = (uint32_t)f2bf(acc[cls][i][j][2]) | ((uint32_t)f2bf(acc[cls][i][j][3]) << 16);
+        *reinterpret_cast<uint2*>(Cs + rl * CS_LD + cl) = pk;
+#else
         const int cl = wn * (BN / 2) + j * 16 + lr;
 #pragma unroll
         for (int r = 0; r < 4; ++r) Cs[(wm * (BM / 2) + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[cls][i][j][r]);
+#endif
       }
     long eoff[EIT];
     short8_t ea[EIT];
@@ -968,6 +996,9 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
       const int rl = tid / CPR + it * (256 / CPR), row = m0 + rl;
       if (row >= g.M || !full) continue;  // the host guarantees ncols % 8 == 0
       short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+#if SL_S2_LAYOUT
+      if ((rl >> 3) & 1) v = __builtin_shufflevector(v, v, 4, 5, 6, 7, 0, 1, 2, 3);
+#endif
       if (eadd) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
