@@ -72,6 +72,29 @@ constexpr int STAGE_BYTES = TPIX * OUT_LD * 2;
 // have zero weights).  Pixel / weight-row strides in 16-B chunks are chosen
 // = 10 (mod 16) or brute-forced so ds_read_b128 lane groups stay (near)
 // conflict-free.
+// Branch-free loads (SL_HALO_BRFREE).  A load issued under a divergent (or path-dependent)
+// condition, with the other path writing the same registers (the zero / 0xff default),
+// leaves the compiler's wait-count pass a pending write on that path: it then drains ALL
+// outstanding loads (s_waitcnt vmcnt(0) / (4)) before the next VALU write to those registers
+// -- in these kernels right after the next tile's prefetch was issued, exposing its full
+// HBM latency on every tile.  Every lane therefore loads unconditionally from a valid
+// address (padding / surplus lanes: a clamped in-image pixel; absent operands: another
+// tensor of the same shape) and the value is masked where it is consumed.
+#ifndef SL_HALO_BRFREE
+#define SL_HALO_BRFREE 1
+#endif
+// keep v live here (the wait-count pass then settles its load on every path)
+template <typename T>
+__device__ __forceinline__ void halo_consume(const T& v) {
+  if constexpr (SL_HALO_BRFREE) {
+    if constexpr (sizeof(T) == 16) {
+      asm volatile("" ::"v"(__builtin_bit_cast(short8_t, v)));  // uint4 is a struct
+    } else {
+      asm volatile("" ::"v"(v));
+    }
+  }
+}
+
 template <int CIN>
 struct Lay {
   static constexpr int DCH = CIN / 8;                    // data chunks per halo pixel
@@ -172,6 +195,8 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
   auto halo_load = [&](int tile) {
     const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
     hok = 0;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.src) + (long)img * a.H * IW * CIN, 0,
+                                                      a.H * IW * CIN * 2, 0x00020000);
 #pragma unroll
     for (int i = 0; i < HL; ++i) {
       const int q = tid + i * NTF;
@@ -179,10 +204,22 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       const int hr = pix / HCOL, hc = pix - hr * HCOL;
       const int ih = r0 - 1 + hr, iw = hc - 1;
       const bool ok = q < L::HALO_CHUNKS && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW;
-      hv[i] = ok ? *reinterpret_cast<const uint4*>(a.src + (((long)img * a.H + ih) * IW + iw) * CIN + c * 8)
-                 : make_uint4(0, 0, 0, 0);
+      if constexpr (SL_HALO_BRFREE) {
+        // out-of-range buffer offset: the load returns zeros without a memory access
+        const int off = ok ? ((ih * IW + iw) * CIN + c * 8) * 2 : (int)0x7ffffff0;
+        hv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      } else {
+        hv[i] = ok ? *reinterpret_cast<const uint4*>(a.src + (((long)img * a.H + ih) * IW + iw) * CIN + c * 8)
+                   : make_uint4(0, 0, 0, 0);
+      }
       hok |= (unsigned)ok << i;
     }
+  };
+  // the wait-count pass does not pair the conditional prefetch with its conditional store:
+  // settle the prefetch registers on the path that skips the store too
+  auto halo_settle = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < HL; ++i) halo_consume(hv[i]);
   };
   auto halo_store = [&]() {
 #pragma unroll
@@ -242,6 +279,7 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
     for (int k = 0; k < EIT; ++k) {
       const long off = (pix0 + ((tid + k * NTF) >> 3)) * a.ldy + ec;
       if (SL_HALO_KO == 1) continue;
+      // uniform conditions: these loads stay conditional; halo_consume settles them per tile
       if (a.add) ea[k] = ld8(a.add + off);
       if (bnb) bnb_load<false>(a.bn, off, ebn[k]);
     }
@@ -250,6 +288,8 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
     const int next = t + gridDim.x;
     if (next < a.tiles && SL_HALO_KO != 2) halo_load(next);  // lands under this tile's MFMAs
     if constexpr (!DEFER && SL_HALO_EPI_PF) epi_loads(t);    // ... and so do these
+    // unconditional loads would otherwise sink below the k-loop, next to their first use
+    if constexpr (SL_HALO_BRFREE) asm volatile("" ::: "memory");
 
     floatx4_t acc[MF][4];
 #pragma unroll
@@ -339,6 +379,8 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       if (next < a.tiles) {
         halo_store();
         lds_bar();  // halo and Ds visible to the next k-loop
+      } else {
+        halo_settle();
       }
       continue;
     }
@@ -371,10 +413,22 @@ __global__ __launch_bounds__(NTF, 1) void conv3x3_kernel(HaloArgs a) {
       if (bnb) bnb_chunk<false>(a.bn, ebn[k], v, msc, msh, bacc);
       *reinterpret_cast<short8_t*>(a.y + m * a.ldy + c) = v;
     }
+#pragma unroll
+    for (int k = 0; k < EIT; ++k) {
+      // unconditionally (also where the uniform branch skipped the load: the register is
+      // then just read), so no path reaches the next tile with these loads pending
+      halo_consume(ea[k]);
+      if constexpr (BNB) {
+        halo_consume(ebn[k].x);
+        halo_consume(ebn[k].m);
+      }
+    }
     lds_bar();  // staging reads done before the next halo lands
     if (next < a.tiles) {
       halo_store();
       lds_bar();
+    } else {
+      halo_settle();
     }
   }
 
@@ -524,14 +578,28 @@ int sl_conv3x3_bnin_fwd(const uint16_t* x, const uint16_t* w, int N, int H, uint
 // channels ci 16 (w & 3) .. +15 of taps 0-4 (w < 4) or 5-8, i.e. 20 or 16
 // accumulator tiles; the workgroup's partial dW is added with fp32 atomics
 // once at the end (one adder per CU per address).
-// Pixel stride 144 B: the worst tr-read lane half is 2-way (brute-forced); the
-// implicit-GEMM path re-gathered X 9 times through LDS-DMA instead.
+// LDS images (SL_HWG_SWZ = 1): unpadded 128-B pixels, 16-B chunk c of pixel x at
+// position c ^ (g(x) << 1), g(x) = bit 1 | bit 3 << 1 of x.  A tr-read lane half takes
+// pixels {b .. b+3, b+8 .. b+11} x 32 B; g spreads each parity class of those pixels over
+// the four chunk pairs, so every half covers the 64 banks once (brute-forced over all
+// fragments; the stores stay one contiguous 128-B pixel per 8 lanes).  The per-lane
+// address then depends on the fragment's first pixel mod 16: one base VGPR per residue.
+// SL_HWG_SWZ = 0: the round-3 144-B pixel stride, where every tr-read half is 2-way
+// (44 % of the kernel's LDS cycles were conflicts, profiles/r05_pmc_cnn).  The implicit-
+// GEMM path re-gathered X 9 times through LDS-DMA instead.
 // ---------------------------------------------------------------------------
+#ifndef SL_HWG_SWZ
+#define SL_HWG_SWZ 1
+#endif
 namespace {
 constexpr int WNT = 512;                    // threads
-constexpr int WPS = 144;                    // pixel stride (bytes) of both LDS images
-constexpr int WX_BYTES = HR * HCOL * WPS;   // 48,960
-constexpr int WY_BYTES = TPIX * WPS;        // 36,864
+constexpr int WPS = SL_HWG_SWZ ? 128 : 144; // pixel stride (bytes) of both LDS images
+constexpr int WX_BYTES = HR * HCOL * WPS;   // 43,520 (48,960 at 144)
+constexpr int WY_BYTES = TPIX * WPS;        // 32,768 (36,864)
+// byte offset of 16-B chunk c inside pixel x's row
+__host__ __device__ constexpr int wg_chunk_off(int x, int c) {
+  return SL_HWG_SWZ ? ((c ^ ((((x >> 1) & 1) | (((x >> 3) & 1) << 1)) << 1)) << 4) : c << 4;
+}
 constexpr int WX_CHUNKS = HR * HCOL * 8, WY_CHUNKS = TPIX * 8;
 constexpr int WLOADS = (WX_CHUNKS + WY_CHUNKS + WNT - 1) / WNT;  // 10 x 16 B per thread
 }  // namespace
@@ -561,6 +629,34 @@ __device__ __forceinline__ short8_t tr16_frag(uint32_t a) {
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
+#if SL_HWG_SWZ
+// Per-lane bases: xb[r] / yb[r] address the lane's 8 B of a fragment whose first pixel is
+// = r (mod 16), minus that pixel's 16-aligned part (added as the instruction offset).
+// Y chunk pair I enters by XOR on address bits 5-6 (yb[r] holds pair 0; Ys is 128-B aligned).
+using WgBases = uint32_t[16];
+template <int P0>
+__device__ __forceinline__ short4_t wg_tr_at(const WgBases& b) {
+  return tr16_at<(P0 / 16) * 16 * WPS>(b[P0 % 16]);
+}
+template <int S, int T>
+__device__ __forceinline__ short8_t xfrag(const WgBases& xb) {
+  constexpr int P0 = (S + T / 3) * HCOL + T % 3;
+  const short4_t lo = wg_tr_at<P0>(xb), hi = wg_tr_at<P0 + 4>(xb);
+  short8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+template <int S, int I>
+__device__ __forceinline__ short8_t yfrag(const WgBases& yb) {
+  const short4_t lo = tr16_at<S * 32 * WPS>(yb[0] ^ (I << 5)), hi = tr16_at<S * 32 * WPS>(yb[4] ^ (I << 5));
+  short8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+#else
+using WgBases = uint32_t;
 // X fragment for tap T at output row S: halo pixel (S + T / 3, col + T % 3)
 template <int S, int T>
 __device__ __forceinline__ short8_t xfrag(uint32_t xb) {
@@ -570,9 +666,10 @@ template <int S, int I>
 __device__ __forceinline__ short8_t yfrag(uint32_t yb) {
   return tr16_frag<(S * 32) * WPS + 32 * I, (S * 32 + 4) * WPS + 32 * I>(yb);
 }
+#endif
 
 template <int T0, int NTAP>
-__device__ __forceinline__ void wgrad_tile_mfmas(uint32_t xb, uint32_t yb, floatx4_t (&acc)[4][5]) {
+__device__ __forceinline__ void wgrad_tile_mfmas(const WgBases& xb, const WgBases& yb, floatx4_t (&acc)[4][5]) {
   auto kstep = [&](auto s_c) {
     constexpr int S = decltype(s_c)::value;
     short8_t af[4], bf[5];
@@ -652,7 +749,7 @@ __global__ __launch_bounds__(256) void halo_wgrad_reduce_kernel(const float4* __
 
 __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs a) {
   younger_half_prio();
-  __shared__ __attribute__((aligned(16))) uint8_t smem[WX_BYTES + WY_BYTES];
+  __shared__ __attribute__((aligned(128))) uint8_t smem[WX_BYTES + WY_BYTES];
   uint8_t* Xs = smem;
   uint8_t* Ys = smem + WX_BYTES;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -666,13 +763,46 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
   if (bni) bn_coef8(a.bin, HC, (tid & 7) * 8, a.bin_count, a.bin_eps, isc, ish);
 
   uint4 pv[WLOADS];
+  uint4 pvy[WLOADS];  // SL_HALO_BRFREE: Y half of a range that holds X and Y chunks
   unsigned xok = 0;  // bit i: chunk i is an X chunk inside the image
   auto tile_load = [&](int tile) __attribute__((always_inline)) {
     const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TR;
     xok = 0;
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.x) + (long)img * a.H * IW * HC, 0,
+                                                       a.H * IW * HC * 2, 0x00020000);
+    const auto yrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.dy) + (long)tile * TPIX * a.ldy, 0,
+                                                       TPIX * a.ldy * 2, 0x00020000);
 #pragma unroll
     for (int i = 0; i < WLOADS; ++i) {
       const int c = tid + i * WNT;
+      if constexpr (SL_HALO_BRFREE) {
+        // X and Y chunks through two buffer resources; a lane's offset is out of range in the
+        // one it does not use (and in both past the last Y chunk), which loads zeros for free.
+        // Workgroup-uniform i ranges touch one resource only.
+        constexpr int OOB = 0x7ffffff0;
+        const int i0 = i * WNT;
+        int xoff = OOB, yoff = OOB;
+        if (c < WX_CHUNKS) {
+          const int pix = c >> 3, ch = c & 7;
+          const int hr = pix / HCOL, hc = pix - hr * HCOL;
+          const int ih = r0 - 1 + hr, iw = hc - 1;
+          if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)IW) {
+            xoff = ((ih * IW + iw) * HC + ch * 8) * 2;
+            xok |= 1u << i;
+          }
+        } else if (c < WX_CHUNKS + WY_CHUNKS) {
+          const int cc = c - WX_CHUNKS;
+          yoff = ((cc >> 3) * a.ldy + (cc & 7) * 8) * 2;
+        }
+        if (i0 < WX_CHUNKS) pv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff, 0, 0));
+        if (i0 + WNT > WX_CHUNKS && i0 < WX_CHUNKS + WY_CHUNKS) {
+          // a range holding both kinds keeps its Y half apart until tile_store (an OR here
+          // would wait for both loads before the MFMAs)
+          uint4& dst = i0 < WX_CHUNKS ? pvy[i] : pv[i];
+          dst = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrs, yoff, 0, 0));
+        }
+        continue;
+      }
       uint4 v = make_uint4(0, 0, 0, 0);
       if (c < WX_CHUNKS) {
         const int pix = c >> 3, ch = c & 7;
@@ -693,20 +823,38 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
 #pragma unroll
     for (int i = 0; i < WLOADS; ++i) {
       const int c = tid + i * WNT;
+      if constexpr (SL_HALO_BRFREE) {
+        if (i * WNT < WX_CHUNKS && (i + 1) * WNT > WX_CHUNKS) {  // mixed range: one of the two is zeros
+          pv[i].x |= pvy[i].x; pv[i].y |= pvy[i].y; pv[i].z |= pvy[i].z; pv[i].w |= pvy[i].w;
+        }
+      }
       if (c < WX_CHUNKS) {
         uint4 v = pv[i];
         if (bni && ((xok >> i) & 1u)) v = bn_relu_chunk(v, isc, ish);
-        *reinterpret_cast<uint4*>(Xs + (c >> 3) * WPS + (c & 7) * 16) = v;
+        *reinterpret_cast<uint4*>(Xs + (c >> 3) * WPS + wg_chunk_off(c >> 3, c & 7)) = v;
       } else if (c < WX_CHUNKS + WY_CHUNKS) {
         const int cc = c - WX_CHUNKS;
-        *reinterpret_cast<uint4*>(Ys + (cc >> 3) * WPS + (cc & 7) * 16) = pv[i];
+        *reinterpret_cast<uint4*>(Ys + (cc >> 3) * WPS + wg_chunk_off(cc >> 3, cc & 7)) = pv[i];
       }
     }
   };
 
   // tr16 lane addressing: rows = pixels 8 lg + q (+4 for the second read), columns = 4 p .. 4 p + 3
+#if SL_HWG_SWZ
+  static_assert(WX_BYTES % 128 == 0, "Ys must stay 128-B aligned for the chunk-pair XOR");
+  const uint32_t xs0 = (uint32_t)(uintptr_t)(SL_LDS const uint8_t*)Xs;
+  const uint32_t ys0 = (uint32_t)(uintptr_t)(SL_LDS const uint8_t*)Ys;
+  WgBases xb, yb;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int x = r + 8 * lg + q;
+    xb[r] = xs0 + (uint32_t)(x * WPS + wg_chunk_off(x, 2 * cb + (p >> 1)) + (p & 1) * 8);
+    yb[r] = ys0 + (uint32_t)(x * WPS + wg_chunk_off(x, p >> 1) + (p & 1) * 8);
+  }
+#else
   const uint32_t xb = (uint32_t)(uintptr_t)(SL_LDS const uint8_t*)Xs + (uint32_t)((8 * lg + q) * WPS + (16 * cb + 4 * p) * 2);
   const uint32_t yb = (uint32_t)(uintptr_t)(SL_LDS const uint8_t*)Ys + (uint32_t)((8 * lg + q) * WPS + 4 * p * 2);
+#endif
 
   floatx4_t acc[4][5];
 #pragma unroll
@@ -724,11 +872,18 @@ __global__ __launch_bounds__(WNT, 1) void conv3x3_wgrad_c64_kernel(WgradHaloArgs
     for (; tile < a.tiles; tile += gridDim.x) {
       const int next = tile + gridDim.x;
       if (next < a.tiles) tile_load(next);
+      if constexpr (SL_HALO_BRFREE) asm volatile("" ::: "memory");  // keep the prefetch ahead of the MFMAs
       wgrad_tile_mfmas<T0, NTAP>(xb, yb, acc);
       __syncthreads();  // all waves done with this tile's images
       if (next < a.tiles) {
         tile_store();
         __syncthreads();
+      } else {
+#pragma unroll
+        for (int i = 0; i < WLOADS; ++i) {  // as halo_settle
+          halo_consume(pv[i]);
+          if (SL_HALO_BRFREE && i * WNT < WX_CHUNKS && (i + 1) * WNT > WX_CHUNKS) halo_consume(pvy[i]);
+        }
       }
     }
     // acc[i][t]: lane (lg, lr) holds dW[co = 16 i + 4 lg + r][tap T0 + t][ci = 16 cb + lr]
