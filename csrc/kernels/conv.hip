@@ -785,6 +785,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 #endif
 namespace {
 constexpr int S2_BK = 32;
+#ifndef SL_S2_EPI_EARLY
+#define SL_S2_EPI_EARLY 1
+#endif
 #ifndef SL_S2_LAYOUT
 #define SL_S2_LAYOUT 1  // 0: the first cut's swizzle / MFMA orientation / b16 epilogue (A/B)
 #endif
@@ -959,6 +962,25 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
   for (int cls = 0; cls < 4; ++cls) {
     const int ph = cls >> 1, pw = cls & 1;
     const uint16_t* eadd = (add_even && cls) ? nullptr : e.add;
+    long eoff[EIT];
+    short8_t ea[EIT];
+    BnbIn ebn[EIT];
+    // this class's residual / BN operands: SL_S2_EPI_EARLY issues them before the barrier and
+    // the LDS staging (their latency hides under both) instead of after the staging
+    auto epi_loads = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int it = 0; it < EIT; ++it) {
+        const int row = m0 + tid / CPR + it * (256 / CPR);
+        const Pix q = decode_pix(g, row);
+        const bool ok = row < g.M && full;
+        // lanes outside the tensor load element 0 instead (unused): unconditional loads, so
+        // no path leaves them pending for the wait-count pass (cf. conv3x3_halo.hip BRFREE)
+        eoff[it] = ok ? (((long)q.n * g.FH + 2 * q.oh + ph) * g.FW + 2 * q.ow + pw) * e.ldy + col : 0;
+        if (eadd) ea[it] = ld8(eadd + eoff[it]);
+        if (bnb) bnb_load(e.bn, eoff[it], ebn[it]);
+      }
+    };
+    if (SL_S2_EPI_EARLY) epi_loads();
     if (cls) __syncthreads();  // the previous class's staging reads are done
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -978,18 +1000,7 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
         for (int r = 0; r < 4; ++r) Cs[(wm * (BM / 2) + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[cls][i][j][r]);
 #endif
       }
-    long eoff[EIT];
-    short8_t ea[EIT];
-    BnbIn ebn[EIT];
-#pragma unroll
-    for (int it = 0; it < EIT; ++it) {
-      const int row = m0 + tid / CPR + it * (256 / CPR);
-      const Pix q = decode_pix(g, row);
-      eoff[it] = (((long)q.n * g.FH + 2 * q.oh + ph) * g.FW + 2 * q.ow + pw) * e.ldy + col;
-      const bool ok = row < g.M && full;
-      if (ok && eadd) ea[it] = ld8(eadd + eoff[it]);
-      if (ok && bnb) bnb_load(e.bn, eoff[it], ebn[it]);
-    }
+    if (!SL_S2_EPI_EARLY) epi_loads();
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < EIT; ++it) {
@@ -1005,6 +1016,11 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
       }
       if (bnb) bnb_chunk(e.bn, ebn[it], v, msc, msh, bacc);
       *reinterpret_cast<short8_t*>(e.y + eoff[it]) = v;
+    }
+#pragma unroll
+    for (int it = 0; it < EIT; ++it) {  // settle the operand loads on every path (skipped rows too)
+      asm volatile("" ::"v"(ea[it]));
+      asm volatile("" ::"v"(ebn[it].x), "v"(ebn[it].x2), "v"(ebn[it].m));
     }
   }
   if (bnb) {
