@@ -511,6 +511,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #ifndef SL_GEMM_BIG
 #define SL_GEMM_BIG 1  // use conv_gemm_big_kernel where it applies
 #endif
+#ifndef SL_EPI_SPLIT
+#define SL_EPI_SPLIT 1  // big-GEMM epilogue: compute all chunks, then store (see there)
+#endif
 
 template <bool TRANSPOSED>
 __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
@@ -722,14 +725,37 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
       const Pix pq = decode_pix(g, row);
       orow = ((long)pq.n * g.FH + 2 * pq.oh + gph) * g.FW + 2 * pq.ow + gpw;
     }
-    eoff[it] = orow * e.ldy + col;
-    if (row < g.M && eadd) ea[it] = ld8(eadd + eoff[it]);
-    if (row < g.M && bnb) bnb_load(e.bn, eoff[it], ebn[it]);
+    // rows past M load element 0 (unused): unconditional loads, cf. the stride-2 epilogue
+    eoff[it] = row < g.M ? orow * e.ldy + col : 0;
+    if (eadd) ea[it] = ld8(eadd + eoff[it]);
+    if (bnb) bnb_load(e.bn, eoff[it], ebn[it]);
   }
   BnbAcc bacc;
   float msc[8], msh[8];
   if (bnb) bnb_init(e.bn, e.ncols, col, bacc, msc, msh);
   __syncthreads();
+#if SL_EPI_SPLIT
+  // every chunk first, then the stores back to back: stores interleaved with the operand uses
+  // were each preceded by a full vmcnt(0) (the wait for one chunk's operands also waited for
+  // the stores issued since)
+  short8_t vout[EIT];
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int rl = tid / CPR + it * (512 / CPR), row = m0 + rl;
+    short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+    if (eadd) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
+    }
+    if (bnb && row < g.M) bnb_chunk(e.bn, ebn[it], v, msc, msh, bacc);
+    vout[it] = v;
+  }
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int row = m0 + tid / CPR + it * (512 / CPR);
+    if (row < g.M) *reinterpret_cast<short8_t*>(e.y + eoff[it]) = vout[it];
+  }
+#else
 #pragma unroll
   for (int it = 0; it < EIT; ++it) {
     const int rl = tid / CPR + it * (512 / CPR), row = m0 + rl;
@@ -742,6 +768,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
     if (bnb) bnb_chunk(e.bn, ebn[it], v, msc, msh, bacc);
     *reinterpret_cast<short8_t*>(e.y + eoff[it]) = v;
   }
+#endif
   if (bnb) {
     __syncthreads();
     bnb_fold<512, CPR>(e.bn, bacc, reinterpret_cast<float*>(smem), n0, e.ncols);
