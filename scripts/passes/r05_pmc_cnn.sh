@@ -3,7 +3,7 @@
 set -u
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05_pmc_cnn
+O=gpurun_out/${PASS_TAG:-r05_pmc_cnn}
 mkdir -p $O
 i=0
 for pass in "SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_BUSY_CU_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_MFMA SQ_INSTS_LDS" \
@@ -11,7 +11,7 @@ for pass in "SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_BUSY_CU_CYCLES SQ_VALU_MF
             "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $pass --output-format csv -d $O/p$i -o run -- python3 bench.py --model resnet18 --steps 4 --warmup 2 --settle 0 > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $O/p$i.log; exit 1; }
-  python scripts/pmc_table.py $(find $O/p$i -name "*counter_collection.csv") --match conv > $O/p$i.txt || true
+  python scripts/pmc_table.py $(find $O/p$i -name "*counter_collection.csv") --match ${PMC_MATCH:-conv} > $O/p$i.txt || true
   rm -rf $O/p$i
 done
 cat $O/p1.txt
