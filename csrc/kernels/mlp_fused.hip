@@ -138,6 +138,9 @@ constexpr int ROW_STAMPS = 20;
 // 0: off (age decides: the older workgroup wins issue, finishes ~25k cycles earlier and the
 // younger runs its tail alone); 1 (default): the younger raises its priority after layer 1 and
 // the pair ends together (driver form +2.3 %, profiles/r05_prio); 2: after the softmax (neutral).
+#ifndef SL_ROWS_B3PF
+#define SL_ROWS_B3PF 1  // rows kernel: layer-3 bias prefetched with the labels
+#endif
 #ifndef SL_ROWS_PRIO
 #define SL_ROWS_PRIO 1
 #endif
@@ -538,6 +541,11 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
 #pragma unroll
   for (int sp = 0; sp < SPW; ++sp)
     lab4[sp] = a.y ? *reinterpret_cast<const uint32_t*>(a.y + srow0 + (sp * NWV + wave) * 16 + 4 * lg) : 0u;
+#if SL_ROWS_B3PF
+  // layer 3's bias for this lane's logit column, fetched here instead of at the softmax (an
+  // index clamp, not a condition: the load is unconditional, the column mask is applied at use)
+  const float b3pf = a.b3[lr < NC ? lr : NC - 1];
+#endif
 
   {
   zero_acc();
@@ -752,7 +760,11 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
     const int rb = (sp * NWV + wave) * 16;  // this pass's 16 rows
     const floatx4_t z = z3[sp];
     const int c = lr;
+#if SL_ROWS_B3PF
+    const float bias3 = c < NC ? b3pf : 0.f;
+#else
     const float bias3 = c < NC ? a.b3[c] : 0.f;
+#endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = rb + 4 * lg + r;
