@@ -141,6 +141,9 @@ constexpr int ROW_STAMPS = 20;
 #ifndef SL_ROWS_B3PF
 #define SL_ROWS_B3PF 1  // rows kernel: layer-3 bias prefetched with the labels
 #endif
+#ifndef SL_ROWS_PRO_LATE
+#define SL_ROWS_PRO_LATE 1  // rows kernel (128-row tile): bias prologue after the stream's first loads
+#endif
 #ifndef SL_ROWS_PRIO
 #define SL_ROWS_PRIO 1
 #endif
@@ -379,14 +382,21 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       __syncthreads();
     }
   };
-  {  // the epilogues read the biases from LDS (published by layer 1's barriers)
+  // the epilogues read the biases from LDS (published by layer 1's barriers)
+  auto bias_prologue = [&]() __attribute__((always_inline)) {
     static_assert(NT == HID, "one thread per layer-1 feature");
-    if (BIG && tid < HID / 4) reinterpret_cast<float4*>(BS + HID)[tid] = reinterpret_cast<const float4*>(a.b2)[tid];
+    // all loads before any LDS write (one round trip); b2's index clamped, not guarded
+    const float4 b2v = reinterpret_cast<const float4*>(a.b2)[tid < HID / 4 ? tid : 0];
+    const float b1v = a.b1[tid];
     long long rs = 0;
 #pragma unroll
     for (int j = 0; j < R1_BLK; ++j) rs += a.r1p[tid * R1_BLK + j];
-    BS[tid] = a.b1[tid] + (a.xb - 1024.f * a.xa) * (float)((double)rs * (1.0 / R1_FIX));
-  }
+    if (BIG && tid < HID / 4) reinterpret_cast<float4*>(BS + HID)[tid] = b2v;
+    BS[tid] = b1v + (a.xb - 1024.f * a.xa) * (float)((double)rs * (1.0 / R1_FIX));
+  };
+  // SL_ROWS_PRO_LATE (128-row tile): issued after layer 1's first X chunks and weight-ring
+  // stages, so its memory round trip overlaps theirs instead of preceding them
+  if constexpr (!(BIG && SL_ROWS_PRO_LATE)) bias_prologue();
   if (a.stamps && tid == 0) {  // placement: HW_ID (CU / SH / SE) and XCC_ID
     a.stamps[(long)blockIdx.x * ROW_STAMPS + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     a.stamps[(long)blockIdx.x * ROW_STAMPS + 11] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
@@ -637,6 +647,33 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
         for (int m = 0; m < 8; ++m) pk[m] = u8x2_f16_biased(w[m >> 1], m & 1);
       };
       // prologue: chunks 0, 1 converted, 2, 3 waiting in registers
+#if SL_ROWS_PRO_LATE
+      // every prologue load first (X chunks 0-3, the weight ring, then the biases), then one
+      // wait: the bias fold's round trip no longer precedes the stream's, nor chunk 0/1's the ring's
+      uint4 x01[2][XP];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int p = 0; p < XP; ++p) x01[c][p] = xload(c, p);
+#pragma unroll
+      for (int c = 2; c < 4; ++c)
+#pragma unroll
+        for (int p = 0; p < XP; ++p) xq[c & 1][p] = xload(c, p);
+      short8_t r[RING][NF];
+#pragma unroll
+      for (int i = 0; i < RING; ++i)
+#pragma unroll
+        for (int n = 0; n < NF; ++n) r[i][n] = f_w1(n, i, KS1);
+      bias_prologue();
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int p = 0; p < XP; ++p) {
+          uint32_t pk[8];
+          xcvt(x01[c][p], pk);
+          xput(c, p, pk);
+        }
+#else
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -654,6 +691,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
       for (int i = 0; i < RING; ++i)
 #pragma unroll
         for (int n = 0; n < NF; ++n) r[i][n] = f_w1(n, i, KS1);
+#endif
       bar();
       __builtin_amdgcn_sched_barrier(0);
       const int swz = (lr >> 1) & 7;
