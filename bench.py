@@ -84,6 +84,12 @@ def parse(argv=None):
                     help="after the timed region (1 GPU, graph mode): replay the same K-step graph back-to-back "
                          "for this many seconds and report the last replay as settled_* fields (informative; the "
                          "headline value is the timed region).  0 disables")
+    ap.add_argument("--graph-collectives", action="store_true",
+                    default=os.environ.get("SL_GRAPH_COLLECTIVES", "0") == "1",
+                    help="N>1 with RCCL: capture the process group's collectives (the MLP all-reduce hook, the "
+                         "ResNet bucket all-reduces) into the step hipGraph.  Opt-in, as in the runtime worker, "
+                         "until a real multi-GPU run pins captured multi-rank RCCL; the default steps RCCL "
+                         "eagerly (the xGMI exchange has no host collective and is always captured)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     mlp = a.model == "mlp"
@@ -98,6 +104,32 @@ def parse(argv=None):
     a.shard_batches = a.shard_batches or (4 if mlp else 4)
     a.lr = a.lr if a.lr is not None else (0.05 if mlp else 0.1)
     return a
+
+
+class ReplicaDivergence(RuntimeError):
+    """The replicas still differ after the re-timed fallback: no number may be reported."""
+
+
+def verify_replicas(check, retime, exchange_failed=lambda: False):
+    """The N>1 safety net, for EVERY gradient-exchange path (xGMI one-/two-shot, RCCL captured or
+    eager, gloo).  ``check()`` is True iff every replica holds bit-identical weights (decided by an
+    all-reduce, so every rank takes the same branch); ``exchange_failed()`` is True iff the xGMI
+    exchange recorded a barrier timeout on any rank.  On either failure ``retime()`` re-syncs every
+    rank from rank 0 and times the K steps again with the process group's all-reduce, uncaptured,
+    returning the new elapsed time.  Returns (replicas_identical, fallback reason or None, re-timed
+    elapsed or None); raises :class:`ReplicaDivergence` when the replicas differ even then.
+
+    The reference applies a gossip reply even when the RPC failed (/root/reference/src/worker.cc:153-165);
+    this is the guard against the data-parallel version of that failure mode."""
+    ok, failed = check(), exchange_failed()
+    if ok and not failed:
+        return True, None, None
+    reason = "barrier timeout" if failed else "replicas diverged"
+    elapsed = retime()
+    if not check():
+        raise ReplicaDivergence(f"{reason}; the replicas still diverge after re-timing with the uncaptured "
+                                "process-group all-reduce")
+    return True, reason, elapsed
 
 
 def _free_port() -> int:
@@ -380,7 +412,7 @@ def main(argv=None) -> int:
     # stream-ordered device work and are captured into the step graph as well
     # (tests/test_rccl_gpu.py: captured RCCL steps bit-identical to the hook-free step).  gloo
     # collectives run on the host and keep the eager step.
-    graph_pg = args.dist_backend == "nccl"
+    graph_pg = args.dist_backend == "nccl" and (world == 1 or args.graph_collectives)
     use_graph = args.graph == "on" or (args.graph == "auto" and (world == 1 or xg is not None or graph_pg))
     warm_eager = min(args.warmup, 3)
     for _ in range(warm_eager):
@@ -432,12 +464,13 @@ def main(argv=None) -> int:
         first_loss = tr.stats().loss
         upload_graph()
 
-    def pg_mode():
+    def pg_mode(captured: bool = True):
         nonlocal graph_pg
         tr.enable_xgmi(None)
+        tr.drop_graphs()
         tr.allreduce = lambda g: dist.all_reduce(g)
         tr.step()  # eager first: anything lazily set up by the collective happens outside capture
-        if use_graph and graph_pg:
+        if captured and use_graph and graph_pg:
             try:
                 tr.capture(warmup=0, unroll=args.unroll)
                 return getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
@@ -509,8 +542,16 @@ def main(argv=None) -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    force = os.environ.get("SL_BENCH_FORCE_DIVERGE", "")  # tests: "once" / "always" (rank 1 drifts)
+    n_checks = [0]
+
     def replicas_agree() -> bool:
         # every replica must hold the same weights after lock-step DP (checks the exchange too)
+        n_checks[0] += 1
+        if rank == 1 and (force == "always" or (force == "once" and n_checks[0] == 1)):
+            f = tr.get_flat()
+            f[0] += 1.0
+            tr.set_flat(f)
         ck = tr.get_flat().double()
         lo, hi = ck.clone(), ck.clone()
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
@@ -520,8 +561,41 @@ def main(argv=None) -> int:
     if autotune is not None:
         upload_graph()  # the autotune re-captured the chosen mode's graph
     elapsed = timed()
-    replicas_identical = replicas_agree() if world > 1 else None
     st_timed = tr.stats()
+    replicas_identical, fallback = None, None
+    if world > 1:
+        def exchange_failed() -> bool:
+            bad = torch.tensor([1.0 if (xg is not None and xg.error()) else 0.0], device=dev)
+            dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+            return bad.item() > 0
+
+        def retime() -> float:
+            # never report a number from a broken exchange or diverged replicas: re-sync from rank 0,
+            # switch to the process group's all-reduce WITHOUT graph capture and time the K steps again
+            nonlocal run, use_graph, collective, st_timed
+            print("bench.py: gradient exchange check failed; re-timing with the uncaptured process group",
+                  file=sys.stderr)
+            flat = tr.get_flat()
+            dist.broadcast(flat, 0)
+            tr.set_flat(flat)
+            if mlp:
+                run = pg_mode(captured=False)
+            else:  # the bucket hooks stay; only the captured step goes
+                tr.drop_graphs()
+                run = lambda n: [tr.step() for _ in range(n)]  # noqa: E731
+            use_graph, collective = False, ("rccl" if args.dist_backend == "nccl" else "gloo")
+            run(3)
+            t = timed()
+            st_timed = tr.stats()
+            return t
+
+        try:
+            replicas_identical, fallback, re_elapsed = verify_replicas(replicas_agree, retime, exchange_failed)
+        except ReplicaDivergence as e:
+            print(f"bench.py: {e}; no number reported", file=sys.stderr)
+            return 2
+        if re_elapsed is not None:
+            elapsed = re_elapsed
     settled = None
     if world == 1 and use_graph and args.settle > 0:
         # Informative only: the same K-step replay, back-to-back for args.settle seconds, then
@@ -531,32 +605,14 @@ def main(argv=None) -> int:
         while time.perf_counter() < t_end:
             run(args.steps)
         settled = timed()
-    xgmi_fallback = None
-    if xg is not None:
-        bad = torch.tensor([1.0 if (xg.error() or not replicas_identical) else 0.0], device=dev)
-        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
-        if bad.item() > 0:
-            # never report a number from a broken exchange: re-sync, switch to the process
-            # group's all-reduce and time the K steps again
-            xgmi_fallback = "barrier timeout" if xg.error() else "replicas diverged"
-            print(f"xgmi exchange failed ({xgmi_fallback}); re-timing with the process group", file=sys.stderr)
-            flat = tr.get_flat()
-            dist.broadcast(flat, 0)
-            tr.set_flat(flat)
-            run = pg_mode()
-            use_graph, collective = use_graph and graph_pg, ("rccl" if args.dist_backend == "nccl" else "gloo")
-            run(3)
-            elapsed = timed()
-            replicas_identical = replicas_agree()
-            st_timed = tr.stats()
     out = record(args, world=world, elapsed=elapsed, model_name=model_name, n_params=n_params,
                  use_graph=use_graph, collective=collective, first_loss=first_loss, st=st_timed,
                  t_ingest=t_ingest, ingest_stats=ingest_stats, replicas_identical=replicas_identical, n_dev=n_dev)
     if settled:
         out["settled_ms_per_step"] = round(settled / args.steps * 1e3, 4)
         out["settled_samples_per_s"] = round(args.batch * args.steps / settled, 1)
-    if xgmi_fallback:
-        out["xgmi_fallback"] = xgmi_fallback
+    if fallback:
+        out["replica_fallback"] = fallback
     if getattr(tr, "probe", None) is not None:
         # per step: wall us between consecutive probes and the shader clock over it (GHz), per XCD
         # where both probes ran a workgroup on that XCD (median over those XCDs)

@@ -99,7 +99,22 @@ constexpr double R1_FIX = 16777216.0;     // 2^24
 }  // namespace
 
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+// W1's fp16 shadow limits W1 to |w| < 65488 (values that round to the fp16 maximum 65504 or
+// beyond).  Such a weight (or a NaN) is saturated to +-65504 in the shadow and flagged in the
+// exact row sums: its fixed-point term is R1_OVF instead of its value, which no sum of in-range
+// terms reaches (|R| < 784 * 2^16 * 2^24 < 2^50; converting inf * 2^24 to an integer would be
+// undefined besides).  The host reads the flag where it already synchronises (the trainer's
+// stats / evaluate / logits report NaN), so a run past the range fails visibly instead of
+// training on a saturated value -- a NaN injected into layer 1 would not survive: ReLU is an
+// fmaxf, which drops NaNs.  Weights below ~6e-5 become fp16 subnormals (still exact multiples
+// of 2^-24 in the row sums).
+constexpr long long R1_OVF = 1ll << 52;  // flag term: 25 blocks x 32 columns of it stay < 2^62
+__device__ __forceinline__ uint16_t f2h_w1(float f) {
+  const uint16_t h = f2h(f);
+  return (h & 0x7c00u) == 0x7c00u ? (uint16_t)((h & 0x8000u) | 0x7bffu) : h;  // inf / NaN -> +-65504
+}
 __device__ __forceinline__ long long h_fix(uint16_t h) {
+  if ((h & 0x7fffu) >= 0x7bffu) return R1_OVF;
   return (long long)((double)(float)__builtin_bit_cast(_Float16, h) * R1_FIX);
 }
 // 8 u8 -> 8 fp16 of (1024 + u), exact: fp16 steps by 1 over [1024, 2048), so the bits are
@@ -1041,7 +1056,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
 //   dW1 = dH1^T (a X + b) = a S + b * db1 (x) 1      (mlp_sgd_kernel).
 // That removes the 117 MB normalised-X write (rows kernel) and re-read (here)
 // per 65,536-row step.  The u8 image is read with ds_read_b64_tr_b8 (probed
-// lane map, scripts/probes/tr8_probe.hip: per 16-lane group, lane 2q+p
+// lane map, profiles/r05_passes/probes/tr8_probe.hip: per 16-lane group, lane 2q+p
 // addresses row q bytes 8p..8p+7; lane i receives column i of the 8 rows).
 // dW1 has 784 columns: its 7th tile holds 16 real ones, and the waves past
 // them skip their MFMAs (the tile count per slice stays 9).  Computing the 16
@@ -1555,7 +1570,7 @@ __device__ __forceinline__ long long write_shadow(const SgdArgs& a, long p, floa
   const uint16_t h = f2bf(w);
   if (p < P_B1) {
     const int o = (int)(p / D_IN), i = (int)(p - (long)o * D_IN);
-    const uint16_t h16 = f2h(w);
+    const uint16_t h16 = f2h_w1(w);
     a.w1h[frag_off(o, i, KS1)] = h16;                   // layer 1: B[k=i][n=o]
     return h_fix(h16);
   } else if (p >= P_W2 && p < P_B2) {

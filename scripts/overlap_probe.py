@@ -9,7 +9,7 @@ workgroups -- on a side stream; the optimizer waits for it.  ``--mask-cus k`` ru
 on a stream whose CU mask leaves k CUs per XCD to other queues (hipExtStreamCreateWithCUMask).
 
 Prints one JSON line with ms per step.  Run under ``rocprofv3 --kernel-trace --output-format
-csv`` and feed the trace to scripts/overlap_trace.py for the overlap fraction.
+csv`` and feed the trace to profiles/r05_passes/probes/overlap_trace.py for the overlap fraction.
 """
 import argparse
 import ctypes

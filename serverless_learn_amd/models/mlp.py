@@ -37,6 +37,7 @@ MNIST_STD = 0.3081
 BLOCK_ROWS = 64  # batch rows per workgroup of the fused row kernel
 W3P_LD = 3088  # row stride of the rows kernel's partial rows: [dW3 | db3 | pad | db1 | db2]
 R1_BLK = 25  # 32-column blocks per W1 row: fixed-point partial row sums of the fp16 shadow
+R1_OVF_MIN = 1 << 51  # a partial row sum at or past this flags a W1 weight beyond fp16 (mlp_fused.hip)
 
 LAYOUT = (
     ("fc1.weight", (HIDDEN, D_IN)),
@@ -183,6 +184,9 @@ class CPUTrainer:
         self.x = self.y = None
         self.allreduce = None  # callable(tensor) -> None (sum in place)
         self._last = None
+        from ..utils.phases import PhaseProbe
+
+        self.phases = PhaseProbe("cpu")
 
     n_params = N_PARAMS
     model_name = "mlp-784-256-256-10"
@@ -206,11 +210,22 @@ class CPUTrainer:
         xs = self.x[b * self.batch:(b + 1) * self.batch]
         ys = self.y[b * self.batch:(b + 1) * self.batch]
         loss, correct, g = reference_grads(self.params, xs, ys, 1.0 / (self.batch * self.world_size))
+        self.phases.mark("compute")
         if self.allreduce is not None:
             self.allreduce(g)
+        self.phases.mark("exchange")
         sgd_update(self.params, self.mom, g, self.lr, self.momentum, self.weight_decay)
         self.cursor += 1
+        self.phases.mark("update")
         self._last = (float(loss), float(correct))
+
+    def probe_step(self) -> dict:
+        """One training step with its phases timed (utils/phases.py; wall clock on the CPU)."""
+        self.phases.arm()
+        self.step()
+        out = self.phases.finish()
+        out["exchange_bytes"] = 4 * int(self.params.numel()) if self.allreduce is not None else 0
+        return out
 
     def stats(self) -> StepStats:
         loss, correct = self._last
@@ -319,6 +334,9 @@ class FusedMLPTrainer:
         self.x = self.y = None
         self.n_batches = 1
         self.graph = None
+        from ..utils.phases import PhaseProbe
+
+        self.phases = PhaseProbe(dev)
         self.refresh_shadows()
         # torch loads its reduction kernel's code object on first use (~27 ms): take that here,
         # at construction, not in the first logged chunk of a training worker (profiles/r04_runtime)
@@ -480,27 +498,41 @@ class FusedMLPTrainer:
     def _step_eager(self) -> None:
         if getattr(self, "probe", None) is not None:
             self.probe()
+        ph = self.phases
         self._rows(True)
         self._wgrad()
+        ph.mark("compute")
         if self.xgmi is not None:
             lc = self._launches()
             lc["xreduce"]()
             for launch in lc["xbarrier"]:
                 launch()
-            lc["xupdate"]()
+            ph.mark("exchange")  # slab reduction into the exchange slot + the step barrier(s)
+            lc["xupdate"]()      # (the peers' slots are summed inside the update kernel)
         elif self.allreduce is None:
             self._sgd(2, from_grad=False, grad_out=False)
         else:
             self._sgd(1, from_grad=False, grad_out=True, bump=False)
             self.allreduce(self.grad)
+            ph.mark("exchange")
             self._sgd(2, from_grad=True, grad_out=False)
+        ph.mark("update")
+
+    def probe_step(self) -> dict:
+        """One eager training step with its phases timed (utils/phases.py): {phase: ms} plus
+        the gradient payload aggregated per step (fp32 bytes, 0 at world 1)."""
+        self.phases.arm()
+        self._step_eager()
+        out = self.phases.finish()
+        out["exchange_bytes"] = 4 * N_PARAMS if (self.allreduce is not None or self.xgmi is not None) else 0
+        return out
 
     def drop_graphs(self) -> None:
         """Release every captured step graph after the device has finished with them.  A
         graph may hold a communicator's kernels: the runtime calls this before it re-forms or
         tears down the group, so no replay is in flight when the old
         communicator goes away and the k-step graph is not left alive holding it."""
-        if self.graph is not None or getattr(self, "graph_unrolled", None) is not None:
+        if self.graph is not None:  # steps() ignores graph_unrolled once graph is None (ADVICE r05)
             torch.cuda.synchronize(self.device)
         self.graph = None
         self.graph_unrolled = None
@@ -527,9 +559,16 @@ class FusedMLPTrainer:
             self.graph_unrolled = gk
 
     # ---- eval / state ----
+    def w1_out_of_range(self) -> bool:
+        """True when a W1 weight no longer fits the fp16 shadow layer 1 runs on (|w| >= 65488):
+        the SGD kernel saturates that shadow entry and flags its row sum (mlp_fused.hip h_fix)."""
+        return int(self.r1p.max()) >= R1_OVF_MIN
+
     def stats(self) -> StepStats:
         loss = float(self.loss.sum())
         acc = float(self.correct.sum())
+        if self.w1_out_of_range():
+            loss = float("nan")  # visible: never a number from a saturated layer 1
         return StepStats(loss / self.batch, acc / self.batch, self.batch)
 
     def evaluate(self, x_u8: torch.Tensor, y_u8: torch.Tensor) -> StepStats:
@@ -543,7 +582,8 @@ class FusedMLPTrainer:
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
                n.ptr(loss), n.ptr(corr), None, 0, n.ptr(self.r1p), n.stream_ptr())
-        return StepStats(float(loss.mean()), float(corr.mean()), rows)
+        lv = float("nan") if self.w1_out_of_range() else float(loss.mean())
+        return StepStats(lv, float(corr.mean()), rows)
 
     def logits(self, x_u8: torch.Tensor) -> torch.Tensor:
         n = self._n
@@ -556,6 +596,8 @@ class FusedMLPTrainer:
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
                None, None, n.ptr(out), 0, n.ptr(self.r1p), n.stream_ptr())
+        if self.w1_out_of_range():
+            out.fill_(float("nan"))
         return out
 
     def get_flat(self) -> torch.Tensor:

@@ -262,6 +262,9 @@ class CPUResNetTrainer:
         self.cursor = 0
         self.allreduce = None
         self._last = None
+        from ..utils.phases import PhaseProbe
+
+        self.phases = PhaseProbe("cpu")
 
     @property
     def n_params(self) -> int:
@@ -294,11 +297,22 @@ class CPUResNetTrainer:
         ys = self.y[b * self.batch:(b + 1) * self.batch]
         loss, correct, g = ref_grads(self.spec, self.params, xs, ys, 1.0 / (self.batch * self.world_size),
                                      self.running)
+        self.phases.mark("compute")
         if self.allreduce is not None:
             self.allreduce(g)
+        self.phases.mark("exchange")
         sgd_update(self.params, self.mom, g, self.lr, self.momentum, self.weight_decay)
         self.cursor += 1
+        self.phases.mark("update")
         self._last = (float(loss), float(correct))
+
+    def probe_step(self) -> dict:
+        """One training step with its phases timed (utils/phases.py; wall clock on the CPU)."""
+        self.phases.arm()
+        self.step()
+        out = self.phases.finish()
+        out["exchange_bytes"] = 4 * int(self.params.numel()) if self.allreduce is not None else 0
+        return out
 
     def stats(self):
         from .mlp import StepStats
@@ -351,7 +365,7 @@ def block_backward_errors(tr, g: torch.Tensor) -> list:
     against fp32 autograd of that block run on the engine's OWN stored input, bf16 weights and
     incoming gradient.  Returns [(conv name, "dx" | "dW", relative L2 error)].  Used by the GPU
     numerics tests at B = 32 (tests/test_cnn_gpu.py) and at the bench batch
-    (scripts/resnet_block_check.py)."""
+    (profiles/r05_passes/probes/resnet_block_check.py)."""
     spec = tr.spec
     w32 = tr.shadow.float()
     f32 = lambda t: t.float().permute(0, 3, 1, 2).detach()  # noqa: E731

@@ -175,6 +175,9 @@ class FusedResNetTrainer:
         self.graph = None
         self.bucket_hook = None   # callable(flat_view) -> handle, launched during backward
         self.bucket_wait = None   # callable(handles) -> None, before the optimizer
+        from ..utils.phases import PhaseProbe
+
+        self.phases = PhaseProbe(self.device)
         self.allreduce = None     # callable(grad) -> None (simple, non-overlapped)
         self.bucket_bytes = 16 << 20
         # SL_WGRAD_SIDE=1: the slab reduces run on a side stream beside the next data gradient.  Off by
@@ -411,20 +414,32 @@ class FusedResNetTrainer:
             self.wgws.grow()  # size the split-K slab before any capture (first call: atomics)
         self.forward(train=True)
         handles = self.backward()
+        self.phases.mark("compute")
         if self.bucket_wait is not None:
-            self.bucket_wait(handles)
+            self.bucket_wait(handles)  # the bucket all-reduces ran during backward: the exposed part
         if self.allreduce is not None:
             self.allreduce(self.grad)
+        self.phases.mark("exchange")
         self.O.sgd_flat(self.params, self.grad, self.mom, self.lr, self.momentum, self.weight_decay,
                         shadow=self.shadow)
         self.wt()
         self.K.cursor_bump(self.cursor)
+        self.phases.mark("update")
 
     def step(self) -> None:
         if self.graph is not None:
             self.graph.replay()
             return
         self._step_eager()
+
+    def probe_step(self) -> dict:
+        """One eager training step with its phases timed (utils/phases.py)."""
+        self.phases.arm()
+        self._step_eager()
+        out = self.phases.finish()
+        hooked = self.allreduce is not None or self.bucket_hook is not None
+        out["exchange_bytes"] = 4 * int(self.grad.numel()) if hooked else 0
+        return out
 
     def drop_graphs(self) -> None:
         """Release the captured step graph once the device is done with it (called by the

@@ -15,15 +15,14 @@ for the next epoch (join/leave/eviction all bump it).  After a re-form, rank 0
 -- the longest-lived member, ranks follow join order -- broadcasts the model
 and optimizer state.
 
-:class:`GradBucketer` implements bucketed, backward-overlapped all-reduce for
-models with many parameter tensors (the ResNet-18-shaped CNN): gradients are
-packed into flat buckets as autograd produces them and each full bucket's
-all-reduce is launched asynchronously while backward continues.
+Bucketed, backward-overlapped all-reduce lives with the engine that produces the
+gradients: the ResNet-18 engine launches one asynchronous all-reduce per flat
+gradient bucket as its backward fills it (``FusedResNetTrainer.bucket_hook`` /
+``bucket_wait``, wired to :meth:`ElasticGroup.allreduce_async` by the worker).
 """
 from __future__ import annotations
 
 import datetime
-import os
 import threading
 import time
 
@@ -216,97 +215,3 @@ class ElasticGroup:
         for t in tensors:
             if t is not None:
                 self.broadcast_(t, 0)
-
-
-class GradBucketer:
-    """Bucketed all-reduce overlapped with backward (for multi-tensor models).
-
-    Buckets are filled in reverse registration order (the order autograd
-    produces gradients); ``bucket_bytes`` defaults to 8 MiB -- large enough
-    that each RCCL call runs at link bandwidth on xGMI (ring per-link bound,
-    SURVEY.md §5.8b), small enough that ResNet-18's ~45 MB of gradients form
-    several buckets whose all-reduce hides behind the remaining backward.
-    """
-
-    def __init__(self, params: list[torch.Tensor], group: ElasticGroup, bucket_bytes: int = 8 << 20,
-                 world_size: int = 1):
-        self.group = group
-        self.params = [p for p in params if p.requires_grad]
-        self.world_size = world_size
-        self.buckets: list[list[torch.Tensor]] = []
-        cur, size = [], 0
-        for p in reversed(self.params):
-            cur.append(p)
-            size += p.numel() * 4
-            if size >= bucket_bytes:
-                self.buckets.append(cur)
-                cur, size = [], 0
-        if cur:
-            self.buckets.append(cur)
-        self.flat = [torch.zeros(sum(p.numel() for p in b), dtype=torch.float32, device=b[0].device)
-                     for b in self.buckets]
-        self._index = {}
-        for bi, b in enumerate(self.buckets):
-            off = 0
-            for p in b:
-                self._index[id(p)] = (bi, off)
-                off += p.numel()
-        self._pending = [0] * len(self.buckets)
-        self._works = []
-        self._hooks = []
-        self.comm_stream = torch.cuda.Stream(device=self.flat[0].device) if self.flat and self.flat[0].is_cuda else None
-
-    def attach(self) -> None:
-        for p in self.params:
-            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
-
-    def detach(self) -> None:
-        for h in self._hooks:
-            h.remove()
-        self._hooks.clear()
-
-    def begin_step(self) -> None:
-        self._pending = [len(b) for b in self.buckets]
-        self._works = []
-
-    def _on_grad(self, p: torch.Tensor) -> None:
-        bi, off = self._index[id(p)]
-        self.flat[bi][off:off + p.numel()].copy_(p.grad.reshape(-1))
-        self._pending[bi] -= 1
-        if self._pending[bi] == 0:
-            self._launch(bi)
-
-    def _launch(self, bi: int) -> None:
-        if not self.group.active:
-            return
-        if self.comm_stream is not None:
-            self.comm_stream.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self.comm_stream):
-                work = self.group.allreduce_async(self.flat[bi])
-        else:
-            work = self.group.allreduce_async(self.flat[bi])
-        self._works.append((bi, work))
-
-    def finish(self) -> None:
-        """Wait for every bucket and scatter the averaged gradients back."""
-        for bi, w in self._works:
-            try:
-                w.wait()
-            except Exception as e:
-                self.group.broken = True
-                raise GroupBroken(repr(e)) from e
-        if self.comm_stream is not None:
-            torch.cuda.current_stream().wait_stream(self.comm_stream)
-        inv = 1.0 / max(1, self.world_size)
-        for bi, b in enumerate(self.buckets):
-            off = 0
-            for p in b:
-                n = p.numel()
-                p.grad.copy_(self.flat[bi][off:off + n].view_as(p.grad)).mul_(inv)
-                off += n
-
-
-def env_world() -> tuple[int, int, int]:
-    """(rank, local_rank, world) from torchrun-style environment variables."""
-    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
-            int(os.environ.get("WORLD_SIZE", "1")))

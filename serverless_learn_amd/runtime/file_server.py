@@ -45,7 +45,7 @@ class FileServer:
         self.addr_requested = addr or self.cfg.file_server_addr
         self.metrics = Metrics("file_server")
         self.log = Logger("file_server", self.addr_requested, self.metrics)
-        self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
+        self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s, metrics=self.metrics)
         self._files: dict[int, bytes] = {}
         self._lock = threading.Lock()
         self._gen_locks: dict[int, threading.Lock] = {}
@@ -175,7 +175,8 @@ class FileServer:
 
     # ---- lifecycle -------------------------------------------------------------
     def start(self) -> "FileServer":
-        self.server = RpcServer(self.addr_requested, max_workers=32, max_message_bytes=self.cfg.max_message_bytes)
+        self.server = RpcServer(self.addr_requested, max_workers=32, max_message_bytes=self.cfg.max_message_bytes,
+                                metrics=self.metrics)
         self.server.add_service("FileServer", {"DoPush": self._do_push, "CheckUp": self._check_up})
         self.server.add_service("FileStore", {"StoreFile": self._store_file, "ListFiles": self._list_files})
         self.server.start()

@@ -40,6 +40,9 @@ from ..utils.metrics import Metrics
 from ..wire.codec import decode_update, encode_update
 from .transport import Channels, RpcFailure, RpcServer, metadata_dict
 
+# FlowFeedback's step-time breakdown fields (proto fields 11-16)
+PHASE_FIELDS = ("step_ms", "data_wait_ms", "compute_ms", "exchange_ms", "update_ms", "exchange_gbps")
+
 
 def _free_port() -> int:
     s = socket.socket()
@@ -59,7 +62,7 @@ class Master:
         self.registry = core().Registry()
         self.ps = ParameterServer(self.cfg.learn_rate, per_client=not self.cfg.gossip_compat)
         self.ps_broadcasts = 0
-        self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
+        self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s, metrics=self.metrics)
         self._lock = threading.Lock()
         self.incarnation: dict[str, int] = {}
         self.delivered: dict[str, tuple] = {}       # addr -> (incarnation, file_num)
@@ -162,7 +165,8 @@ class Master:
                 self.feedback[addr] = {"step": fb.step, "samples_per_sec": fb.samples_per_sec, "loss": fb.loss,
                                        "bytes_ingested": fb.bytes_ingested, "epoch": fb.epoch, "state": fb.state,
                                        "group_samples_per_sec": fb.group_samples_per_sec,
-                                       "group_loss": fb.group_loss, "group_world": fb.group_world}
+                                       "group_loss": fb.group_loss, "group_world": fb.group_world,
+                                       **{k: getattr(fb, k) for k in PHASE_FIELDS}}
         except RpcFailure as e:
             evicted = self.registry.heartbeat_fail(addr, self.cfg.max_misses)
             self.log.warn("checkup_failed", worker=addr, evicted=evicted, error=e.code.name if e.code else "")
@@ -209,8 +213,13 @@ class Master:
                 groups[f["epoch"]] = max(groups.get(f["epoch"], 0.0), f.get("group_samples_per_sec", 0.0))
             else:
                 solo += f.get("samples_per_sec", 0.0)
+        # step-time breakdown over the training workers: mean per field, slowest step
+        live = [f for f in fb.values() if f.get("state") == "training" and f.get("step_ms", 0.0) > 0]
+        phases = {k: round(sum(f.get(k, 0.0) for f in live) / len(live), 4) for k in PHASE_FIELDS} if live else {}
+        if live:
+            phases["max_step_ms"] = round(max(f["step_ms"] for f in live), 4)
         return {"samples_per_sec": round(sum(groups.values()) + solo, 1), "groups": len(groups),
-                "workers": len(fb)}
+                "workers": len(fb), "phases": phases}
 
     # ---- push scheduling -------------------------------------------------------
     def _num_shards(self, n_members: int) -> int:
@@ -278,7 +287,8 @@ class Master:
             self.log.warn("rendezvous_unavailable", error=repr(e))
 
     def start(self, loops: bool = True) -> "Master":
-        self.server = RpcServer(self.addr_requested, max_workers=32, max_message_bytes=self.cfg.max_message_bytes)
+        self.server = RpcServer(self.addr_requested, max_workers=32, max_message_bytes=self.cfg.max_message_bytes,
+                                metrics=self.metrics)
         self.server.add_service("Master", {"RegisterBirth": self._register, "ExchangeUpdates": self._exchange_updates})
         self.server.add_service("MasterControl", {"Deregister": self._deregister,
                                                   "GetMembership": self._get_membership,

@@ -10,7 +10,9 @@ Here: handlers are registered on the exact method paths
 (``/serverless_learn.<Service>/<Method>``) with NO serializers, so handlers see
 wire bytes and decode them with the C++ codec (hot messages) or the
 descriptor-built classes; channels are cached per address; every call has a
-deadline; message caps are raised so a full-model ``Update`` fits.
+deadline; message caps are raised so a full-model ``Update`` fits.  Every call served and
+every call made is timed into the owning role's ``sl_rpc_seconds`` histogram (method, side,
+final status code) -- the reference times nothing.
 """
 from __future__ import annotations
 
@@ -55,10 +57,17 @@ def _options(max_message_bytes: int):
     ]
 
 
-class RpcServer:
-    """A gRPC server hosting one or more services of the serverless_learn package."""
+def _status_name(context, default: str) -> str:
+    code = context.code() if context is not None and hasattr(context, "code") else None
+    return code.name if code is not None else default
 
-    def __init__(self, addr: str, max_workers: int = 16, max_message_bytes: int = 256 << 20):
+
+class RpcServer:
+    """A gRPC server hosting one or more services of the serverless_learn package.
+    ``metrics`` (utils.metrics.Metrics): every handled call is timed, with its status code."""
+
+    def __init__(self, addr: str, max_workers: int = 16, max_message_bytes: int = 256 << 20, metrics=None):
+        self.metrics = metrics
         self._server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers,
                                                               thread_name_prefix="sl-rpc"),
                                    options=_options(max_message_bytes) + [("grpc.so_reuseport", 0)])
@@ -74,6 +83,8 @@ class RpcServer:
         table = {}
         for method, fn in handlers.items():
             md = pb.method_def(service, method)
+            if self.metrics is not None:
+                fn = self._timed(f"{service}/{method}", fn)
             if md.client_streaming and not md.server_streaming:
                 table[method] = grpc.stream_unary_rpc_method_handler(fn)
             elif not md.client_streaming and not md.server_streaming:
@@ -82,6 +93,23 @@ class RpcServer:
                 raise NotImplementedError(f"{service}.{method}: streaming responses are not in the protocol")
         self._server.add_generic_rpc_handlers(
             (grpc.method_handlers_generic_handler(f"{pb.PACKAGE}.{service}", table),))
+
+    def _timed(self, name: str, fn):
+        m = self.metrics
+
+        def handler(request, context):
+            t0 = time.perf_counter()
+            code = "UNKNOWN"
+            try:
+                out = fn(request, context)
+                code = _status_name(context, "OK")
+                return out
+            except Exception:
+                code = _status_name(context, "UNKNOWN")  # context.abort() sets it before raising
+                raise
+            finally:
+                m.rpc("server", name, code, time.perf_counter() - t0)
+        return handler
 
     def start(self) -> "RpcServer":
         self._server.start()
@@ -101,7 +129,8 @@ class Channels:
     """Per-address channel cache with deadlines (fixes master.cc:257's TODO(PERF))."""
 
     def __init__(self, max_message_bytes: int = 256 << 20, default_timeout: float = 5.0, retries: int = 4,
-                 backoff_s: float = 0.05):
+                 backoff_s: float = 0.05, metrics=None):
+        self.metrics = metrics      # utils.metrics.Metrics: client-side latency per call
         self.retries = retries      # extra attempts for idempotent unary RPCs
         self.backoff_s = backoff_s  # first back-off; doubles per attempt, +-50 % jitter
         self.retried = 0            # attempts re-sent (metrics / tests)
@@ -143,6 +172,18 @@ class Channels:
         failure-detection timing (the master's miss counting) is unchanged: a peer that is
         really gone still fails within ``timeout``, while a dropped connection or a restarting
         listener no longer costs a miss."""
+        t0 = time.perf_counter()
+        code = "OK"
+        try:
+            return self._unary(addr, service, method, request, timeout, metadata, idempotent)
+        except RpcFailure as f:
+            code = f.code.name if f.code else "UNKNOWN"
+            raise
+        finally:
+            if self.metrics is not None:
+                self.metrics.rpc("client", f"{service}/{method}", code, time.perf_counter() - t0)
+
+    def _unary(self, addr, service, method, request, timeout, metadata, idempotent) -> bytes:
         stub = self._stub(addr, service, method, "uu")
         budget = timeout or self.default_timeout
         deadline = time.monotonic() + budget
@@ -166,10 +207,16 @@ class Channels:
     def stream_unary(self, addr: str, service: str, method: str, requests, timeout: float | None = None,
                      metadata=None) -> bytes:
         stub = self._stub(addr, service, method, "su")
+        t0 = time.perf_counter()
+        code = "OK"
         try:
             return stub(requests, timeout=timeout or self.default_timeout, metadata=metadata)
         except grpc.RpcError as e:
+            code = e.code().name if e.code() else "UNKNOWN"
             raise RpcFailure(pb.method_path(service, method), addr, e.code(), e.details() or "") from None
+        finally:
+            if self.metrics is not None:
+                self.metrics.rpc("client", f"{service}/{method}", code, time.perf_counter() - t0)
 
     def forget(self, addr: str) -> None:
         with self._lock:

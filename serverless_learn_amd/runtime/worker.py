@@ -81,7 +81,7 @@ class Worker:
         self.log = Logger("worker", addr, self.metrics)
         self.incarnation = (time.time_ns() ^ (os.getpid() << 20) ^ random.getrandbits(40)) & ((1 << 63) - 1)
         self.device = resolve_device(self.cfg.device)
-        self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s)
+        self.channels = Channels(self.cfg.max_message_bytes, self.cfg.rpc_timeout_s, metrics=self.metrics)
         self.fault = FaultInjector.from_env()
         self.train_lock = threading.RLock()
         self.view_lock = threading.Lock()
@@ -100,6 +100,13 @@ class Worker:
         self.resumed_step = -1
         self._resume_pulled = 0   # PeerList.resume_file already pulled from the file server
         self.graph_chunks = 0     # graph replays run (tests / feedback)
+        self._graph_collectives = False  # the captured step graphs hold the group's collectives
+        # SURVEY §5.5 step-time breakdown, per log interval: wall ms per step, the loop's waits
+        # per step, and one probed step's device phases (compute / exchange / update, exchange GB/s)
+        self.phase_stats = {k: 0.0 for k in ("step_ms", "data_wait_ms", "compute_ms", "exchange_ms", "update_ms",
+                                             "exchange_gbps")}
+        self._wait_s = 0.0
+        self._probe_due = True
         self.hold_at = None       # pause training exactly at this step (bench.py --runtime, tests)
         self.held_step = -1       # step the worker is paused at, once its device work has drained
         self._agreed_epoch = -1   # newest membership epoch the whole lock-step group has agreed to see
@@ -232,7 +239,8 @@ class Worker:
                              loss=self.loss if self.loss == self.loss else 0.0,
                              bytes_ingested=self.bytes_ingested, epoch=self.group.epoch if self.group.epoch >= 0 else 0,
                              state=self.state, group_samples_per_sec=gm["samples_per_sec"],
-                             group_loss=gm["loss"], group_accuracy=gm["accuracy"], group_world=gm["world"])
+                             group_loss=gm["loss"], group_accuracy=gm["accuracy"], group_world=gm["world"],
+                             **self.phase_stats)
         return fb.SerializeToString()
 
     def _exchange_updates(self, request: bytes, context) -> bytes:
@@ -532,15 +540,27 @@ class Worker:
                 t.bucket_wait = self._bucket_wait if want_hook else None
             if hasattr(t, "graph"):
                 t.graph = None  # the captured step must be re-captured with (or without) the collective
+                if hasattr(t, "graph_unrolled"):
+                    t.graph_unrolled = None  # ... and so must the k-step graph
             self._set_world(max(1, self.group.world) if self.group.active and self.group.world > 1 else 1)
 
     def _drop_graphs(self) -> None:
         """Free the trainer's captured step graphs (the one-step and the k-step graph) after
         the device has drained them: they may hold the current communicator's kernels, so
-        this runs before every re-form and teardown of the group."""
+        this runs before every re-form and teardown of the group.
+
+        The drain must not wait on a collective whose peer is gone: the NCCL
+        watchdog does not track collectives captured in a graph, and an eager all-reduce
+        queued before a peer died only ends at the watchdog timeout.  So when the group is
+        broken, or when the captured graphs hold collectives, the communicator is aborted
+        FIRST (``ncclCommAbort`` releases the kernels waiting on the dead peer) and only then
+        is the device drained; graphs of kernels only are drained directly."""
         t = self.trainer
         if t is None:
             return
+        if self.group.active and (self.group.broken or self._graph_collectives):
+            self.group.teardown()
+        self._graph_collectives = False
         with self.train_lock:
             if hasattr(t, "drop_graphs"):
                 t.drop_graphs()
@@ -594,12 +614,25 @@ class Worker:
         Eager steps take ``train_lock`` one step at a time, so ReceiveFile / ExchangeUpdates /
         gossip wait for at most one step, not a whole chunk.  A collective failing
         at step j of a chunk raises :class:`ChunkBroken` carrying the j steps that did complete,
-        so the step counter stays equal to the trainer's real state."""
+        so the step counter stays equal to the trainer's real state.  That count is exact on
+        the eager path.  On the graph path (opt-in RCCL-in-graph) a failure can only surface
+        in the chunk's first eager step or its capture: ``done`` is then 0 or 1 while replays
+        queued before the failure may still have advanced the device cursor and weights.  The
+        regroup that follows re-synchronises both: rank 0 broadcasts the parameters, the
+        momentum and its step counter (``_maybe_regroup``), so every member restarts from one
+        consistent (step, state) pair."""
         t = self.trainer
         k = max(1, self.cfg.graph_steps)
         n = max(1, min(n, k))
         done = 0
         try:
+            if self._probe_due and hasattr(t, "probe_step"):
+                # once per log interval: the chunk's first step runs eagerly with its phases timed
+                self._probe_due = False
+                with self.train_lock:
+                    p = t.probe_step()
+                done = 1
+                self._record_phases(p)
             if not self._use_graph():
                 while done < n:
                     with self.train_lock:
@@ -608,12 +641,16 @@ class Worker:
                 return n
             with self.train_lock:
                 if t.graph is None:
-                    t.step()
-                    done = 1
+                    if done == 0:
+                        t.step()  # eager first: sizes lazily grown workspaces before the capture
+                        done = 1
                     if hasattr(t, "steps"):
                         t.capture(warmup=0, unroll=k)
                     else:
                         t.capture(warmup=0)
+                    # the replays now hold collectives iff the step has a host hook (RCCL in graph)
+                    self._graph_collectives = (t.allreduce is not None
+                                               or getattr(t, "bucket_hook", None) is not None)
                     self.log.info("graph_captured", steps=k, step=self.step + 1)
                 if n > done:
                     if hasattr(t, "steps"):
@@ -672,17 +709,17 @@ class Worker:
                 self._install_allreduce()
                 if self.group.broken:
                     self.state = "regrouping"  # waiting for the master's next view (see _needs_regroup)
-                    self._stop.wait(0.05)
+                    self._idle(0.05)
                     continue
                 if self.group.active and self._agreed_epoch > self.group.epoch:
                     # the group agreed to move to a newer epoch that this worker's view has
                     # not reached yet: no more steps on the old group, wait for the CheckUp
                     self.state = "regrouping"
-                    self._stop.wait(0.05)
+                    self._idle(0.05)
                     continue
                 if self.view["world"] > 1:
                     if not self.group.active:
-                        self._stop.wait(0.05)
+                        self._idle(0.05)
                         continue
                     if ready_epoch != self.group.epoch:
                         # every member must have data before the first lock-step collective;
@@ -700,11 +737,11 @@ class Worker:
                             t_last, s_last = time.perf_counter(), self.samples
                         else:
                             self.state = "waiting_for_data"
-                            self._stop.wait(0.1)
+                            self._idle(0.1)
                             continue
             if not have_data:
                 self.state = "idle"
-                self.has_data.wait(0.2)
+                self._idle(0.2, self.has_data)
                 self.has_data.clear()
                 continue
             hold = self.hold_at
@@ -774,6 +811,11 @@ class Worker:
                     self._group_metrics_update(dt, self.samples - s_last, st)
                 except GroupBroken as e:
                     self.log.warn("group_metrics_failed", error=str(e))
+                steps_i = max(1, (self.samples - s_last) // max(1, self.trainer.batch))
+                self.phase_stats["step_ms"] = dt * 1e3 / steps_i
+                self.phase_stats["data_wait_ms"] = self._wait_s * 1e3 / steps_i
+                self._wait_s = 0.0
+                self._probe_due = True  # the next chunk times one step's phases
                 t_last, s_last = time.perf_counter(), self.samples
                 self.loss = st.loss
                 gm = self.group_metrics
@@ -785,7 +827,8 @@ class Worker:
                 self.log.info("train", step=self.step, loss=round(st.loss, 4), acc=round(st.accuracy, 4),
                               samples_per_sec=round(self.rate, 1), epoch=self.group.epoch,
                               group_samples_per_sec=round(gm["samples_per_sec"], 1), group_world=gm["world"],
-                              group_loss=round(gm["loss"], 4), graph=self._use_graph(), **extra)
+                              group_loss=round(gm["loss"], 4), graph=self._use_graph(),
+                              **{k: round(v, 4) for k, v in self.phase_stats.items()}, **extra)
             if (self.cfg.checkpoint_every and self.step // self.cfg.checkpoint_every != prev // self.cfg.checkpoint_every
                     and (self.group.rank <= 0)):
                 try:
@@ -795,6 +838,20 @@ class Worker:
             if self.cfg.max_steps and self.step >= self.cfg.max_steps:
                 self.state = "done"
                 return
+
+    def _idle(self, secs: float, event: threading.Event | None = None) -> None:
+        """A wait of the training loop (no data, waiting for the group or a peer's data):
+        counted into the next log interval's data-wait share (``phase_stats``)."""
+        t0 = time.perf_counter()
+        (event or self._stop).wait(secs)
+        self._wait_s += time.perf_counter() - t0
+
+    def _record_phases(self, p: dict) -> None:
+        """One probed step's phases (utils/phases.py) -> phase_stats / FlowFeedback."""
+        ps = self.phase_stats
+        ps["compute_ms"], ps["exchange_ms"], ps["update_ms"] = p["compute"], p["exchange"], p["update"]
+        nbytes = p.get("exchange_bytes", 0)
+        ps["exchange_gbps"] = nbytes / (p["exchange"] * 1e-3) / 1e9 if nbytes and p["exchange"] > 0 else 0.0
 
     def _simulate_loop(self) -> None:
         """The reference's training: every model element += 1 every 2 s (worker.cc:221-231)."""
@@ -837,7 +894,8 @@ class Worker:
 
     # ---- lifecycle ---------------------------------------------------------------
     def start(self) -> "Worker":
-        self.server = RpcServer(self.addr_requested, max_workers=16, max_message_bytes=self.cfg.max_message_bytes)
+        self.server = RpcServer(self.addr_requested, max_workers=16, max_message_bytes=self.cfg.max_message_bytes,
+                                metrics=self.metrics)
         handlers = {"ReceiveFile": self._receive_file, "CheckUp": self._check_up,
                     "ExchangeUpdates": self._exchange_updates}
         self.server.add_service("Worker", {k: self.fault.wrap(k, v) for k, v in handlers.items()})

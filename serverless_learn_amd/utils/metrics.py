@@ -11,6 +11,12 @@ numeric fields of a few well-known events feed gauges / counters / histograms:
 * ``push``          -> ``sl_pushed_bytes_total{ok}``, ``sl_push_seconds`` histogram
 * ``register_birth`` / ``deregister`` / ``evict`` -> ``sl_membership_epoch`` gauge
 * any ``epoch`` / ``world`` field -> ``sl_membership_epoch`` / ``sl_world_size``
+* ``train``'s step-time breakdown -> ``sl_step_phase_ms{phase}``, ``sl_exchange_gbps``
+
+Besides the log events, the transport reports every RPC it serves or makes (SURVEY.md §5.1,
+"per-RPC latency histograms"): ``sl_rpc_seconds{role,side,method,code}`` -- side ``server`` /
+``client``, method ``Service/Method``, the final gRPC status code (a client call's retries
+included in its one observation).
 
 Each role owns a :class:`Metrics` (its own registry: several roles may share
 a process in tests and the local cluster).  ``SL_METRICS_PORT`` /
@@ -29,6 +35,10 @@ except Exception:  # pragma: no cover - exercised only where prometheus_client i
     AVAILABLE = False
 
 _BUCKETS = (0.001, 0.005, 0.02, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0, 10.0, 30.0)
+# RPC latencies: control-plane calls take ~0.1-1 ms on one host, a 100 MB push seconds
+_RPC_BUCKETS = (0.0001, 0.00025, 0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5,
+                5.0, 10.0, 30.0)
+_PHASES = ("step_ms", "data_wait_ms", "compute_ms", "exchange_ms", "update_ms")
 
 
 class Metrics:
@@ -55,6 +65,34 @@ class Metrics:
                                   registry=r)
         self.pushed = Counter("sl_pushed_bytes", "bytes streamed by pushes", ["role", "ok"], registry=r)
         self.push_s = Histogram("sl_push_seconds", "push duration", ["role"], buckets=_BUCKETS, registry=r)
+        self.rpc_s = Histogram("sl_rpc_seconds", "gRPC call latency by side (server / client), method and "
+                               "final status code", ["role", "side", "method", "code"], buckets=_RPC_BUCKETS,
+                               registry=r)
+        self.phase_ms = Gauge("sl_step_phase_ms", "per-step time by phase over the last log interval "
+                              "(wall step, loop waits; device compute / exchange / update of one probed step)",
+                              ["role", "phase"], registry=r)
+        self.exchange_gbps = Gauge("sl_exchange_gbps", "gradient exchange algorithm bandwidth of the probed step",
+                                   ["role"], registry=r)
+
+    # ---- fed by the transport ---------------------------------------------------------
+    def rpc(self, side: str, method: str, code: str, seconds: float) -> None:
+        if not self.enabled:
+            return
+        self.rpc_s.labels(self.role, side, method, code).observe(seconds)
+
+    def rpc_count(self, side: str, method: str, code: str = "OK") -> int:
+        """Observations so far of one (side, method, code) series (tests, feedback)."""
+        if not self.enabled:
+            return 0
+        for metric in self.registry.collect():
+            if metric.name != "sl_rpc_seconds":
+                continue
+            for smp in metric.samples:
+                lb = smp.labels
+                if (smp.name.endswith("_count") and lb.get("side") == side and lb.get("method") == method
+                        and lb.get("code") == code):
+                    return int(smp.value)
+        return 0
 
     # ---- fed by Logger ----------------------------------------------------------
     def observe(self, level: str, event: str, fields: dict) -> None:
@@ -73,6 +111,11 @@ class Metrics:
                         g.labels(role).set(fields[k])
                 if isinstance(fields.get("group_samples_per_sec"), (int, float)):
                     self.group_rate.labels(role).set(fields["group_samples_per_sec"])
+                for ph in _PHASES:
+                    if isinstance(fields.get(ph), (int, float)):
+                        self.phase_ms.labels(role, ph[:-3]).set(fields[ph])
+                if isinstance(fields.get("exchange_gbps"), (int, float)):
+                    self.exchange_gbps.labels(role).set(fields["exchange_gbps"])
             elif event == "job":
                 if isinstance(fields.get("samples_per_sec"), (int, float)):
                     self.job_rate.labels(role).set(fields["samples_per_sec"])

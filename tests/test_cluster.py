@@ -55,6 +55,42 @@ def test_eviction_bumps_epoch_and_survivors_regroup(cluster):
     assert cluster.wait_for(lambda: all(w.step > s + 20 for w, s in zip(survivors, steps)), 120)
 
 
+def test_rpc_latency_histograms_and_step_phase_feedback(cluster):
+    """every role times the RPCs it serves and makes
+    (method, side, status code) into sl_rpc_seconds; the workers report a step-time breakdown
+    (wall step, loop waits, one probed step's compute / exchange / update and the exchange's
+    GB/s) through the additive FlowFeedback fields, and the master aggregates it per job."""
+    a = cluster.add_worker(sync="allreduce", batch=256, log_every=10)
+    b = cluster.add_worker(sync="allreduce", batch=256, log_every=10)
+    m = cluster.master
+    assert cluster.wait_for(lambda: all(m.feedback.get(w.addr, {}).get("exchange_ms", 0) > 0
+                                        and m.feedback[w.addr].get("step_ms", 0) > 0 for w in (a, b)), 120), \
+        m.feedback
+    fb = m.feedback[a.addr]
+    assert fb["compute_ms"] > 0 and fb["update_ms"] > 0 and fb["exchange_gbps"] > 0
+    job = m.job_metrics()
+    assert job["phases"]["max_step_ms"] >= job["phases"]["step_ms"] > 0
+    assert job["phases"]["exchange_ms"] > 0
+    # server and client sides of the same RPCs, with their status codes
+    assert m.metrics.rpc_count("client", "Worker/CheckUp") > 0
+    assert a.metrics.rpc_count("server", "Worker/CheckUp") > 0
+    assert a.metrics.rpc_count("server", "Worker/ReceiveFile") > 0
+    assert m.metrics.rpc_count("server", "Master/RegisterBirth") > 0
+    assert cluster.file_server.metrics.rpc_count("client", "Worker/ReceiveFile") > 0
+    assert cluster.file_server.metrics.rpc_count("server", "FileServer/DoPush") > 0
+    text = m.metrics.text()
+    assert 'sl_rpc_seconds_bucket{code="OK",le="0.001",method="Worker/CheckUp",role="master",side="client"}' in text
+    assert "sl_step_phase_ms" in a.metrics.text() and "sl_exchange_gbps" in a.metrics.text()
+    # a failing call is recorded with its code: CheckUp of an address nobody serves
+    from serverless_learn_amd.runtime.transport import RpcFailure
+    from serverless_learn_amd.proto import messages as pb
+
+    with pytest.raises(RpcFailure):
+        m.channels.unary("127.0.0.1:1", "Worker", "CheckUp", pb.PeerList().SerializeToString(), timeout=0.3)
+    assert m.metrics.rpc_count("client", "Worker/CheckUp", "UNAVAILABLE") + \
+        m.metrics.rpc_count("client", "Worker/CheckUp", "DEADLINE_EXCEEDED") >= 1
+
+
 def test_gossip_workers_exchange(cluster):
     a = cluster.add_worker(sync="gossip")
     b = cluster.add_worker(sync="gossip")

@@ -564,7 +564,7 @@ def test_resnet_engine_fused_bn_backward_matches_unfused(monkeypatch):
     gradient as the standalone bn_bwd_reduce passes (SL_BNB_FUSE=0), up to the run-to-run
     noise of the engine itself: its cross-workgroup fp32 sums are order-nondeterministic and
     a BN net at init amplifies one-ulp bf16 flips (cos ~0.986 between two unfused runs at
-    batch 32, scripts/bnb_diag.py), so the check is against that noise."""
+    batch 32, profiles/r05_passes/probes/bnb_diag.py), so the check is against that noise."""
     monkeypatch.setenv("SL_BNB_FUSE", "1")
     tr, g, _, _ = _engine("cifar", 32, 32)
     assert tr.fuse_bn_bwd

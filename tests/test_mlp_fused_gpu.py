@@ -211,3 +211,35 @@ def test_gradients_match_reference_at_headline_config(monkeypatch):
     st = tr.stats()
     assert abs(st.loss - float(loss) / B) < 2e-2
     assert abs(st.accuracy - float(correct) / B) < 0.02
+
+
+def test_w1_fp16_shadow_range_edge():
+    """Layer 1 runs against an fp16 shadow of W1: entries close to the fp16 limit
+    still give the fp32 logits (exact fixed-point row sums of large values), and an entry past
+    65504 turns the outputs NaN -- visibly -- instead of training on a saturated or garbage value."""
+    batch = 256
+    x, y = _data(batch, seed=41)
+    flat = M.init_params(3)
+    v = M.views(flat)
+    v["fc1.weight"][7, :16] = 30000.0   # exact in fp16 (spacing 16 at 2^14..2^15)
+    v["fc1.weight"][9, 100:110] = -30000.0
+    tr = M.FusedMLPTrainer(batch=batch, flat=flat)
+    got = tr.logits(x).cpu().double()
+    ref = M.MLP(flat)(x).detach().double()
+    assert float((got - ref).norm() / ref.norm()) < 2e-2
+    assert bool(torch.isfinite(got).all())
+    assert not tr.w1_out_of_range()
+    tr.load_shard(x, y)
+    tr.step()
+    assert tr.stats().loss == tr.stats().loss  # finite while in range
+    v["fc1.weight"][7, 0] = 1.0e5       # beyond fp16
+    tr.set_flat(flat)
+    assert tr.w1_out_of_range()
+    assert bool(torch.isnan(tr.logits(x)).all())
+    st = tr.evaluate(x, y)
+    assert st.loss != st.loss  # NaN loss
+    tr.step()
+    assert tr.stats().loss != tr.stats().loss
+    # the flag lives in the exact row sums: it never reaches a row that is in range
+    rows = tr.r1p.view(M.HIDDEN, -1).sum(1)
+    assert int(rows[7]) >= 1 << 51 and int(rows[[i for i in range(M.HIDDEN) if i != 7]].abs().max()) < 1 << 50

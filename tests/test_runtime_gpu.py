@@ -182,7 +182,7 @@ def test_bench_two_ranks_autotune_and_replicas():
     assert len(lines) == 1, p.stdout[-4000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 8192
-    assert out["replicas_identical"] is True and "xgmi_fallback" not in out
+    assert out["replicas_identical"] is True and "replica_fallback" not in out
     at = out["allreduce_autotune"]
     assert {"xgmi_ms", "xgmi_two_shot_ms", "pg_ms"} <= set(at), at
     best = min(at["xgmi_ms"], at["xgmi_two_shot_ms"], at["pg_ms"])
@@ -224,3 +224,34 @@ def test_bench_self_launches_two_ranks(model, extra):
     assert out["replicas_identical"] is True, out
     b = int(extra[extra.index("--batch") + 1])
     assert out["config"]["global_batch"] == 2 * b
+
+
+@pytest.mark.parametrize("mode", ["once", "always"])
+def test_bench_diverged_replicas_retime_or_refuse(mode):
+    """The N>1 safety net end to end (2 gloo ranks sharing the GPU, the process-group path):
+    rank 1's weights are perturbed before the replica check.  Once: bench.py re-syncs, re-times
+    with the uncaptured process group and reports the new number with replica_fallback.  Always:
+    exit 2 and no JSON line -- a diverged run never prints a number."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = ["timeout", "-k", "10", "200", sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+           "--oversubscribe", "--dist-backend", "gloo", "--allreduce", "pg", "--batch", "4096", "--steps", "6",
+           "--warmup", "2", "--ingest", "local"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["SL_BENCH_FORCE_DIVERGE"] = mode
+    p = subprocess.run(cmd, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=230,
+                       env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    if mode == "once":
+        assert p.returncode == 0, p.stdout[-4000:]
+        import json
+
+        out = json.loads(lines[-1])
+        assert out["replica_fallback"] == "replicas diverged" and out["replicas_identical"] is True
+        assert out["config"]["hipgraph"] is False
+    else:
+        assert p.returncode != 0 and not lines, p.stdout[-4000:]
+        assert "no number reported" in p.stdout

@@ -310,6 +310,37 @@ def test_bench_refuses_more_gpus_than_visible():
     assert p.returncode == 2 and '"metric"' not in p.stdout
 
 
+def test_bench_replica_check_covers_every_path_and_refuses_persistent_divergence():
+    """the N>1 replica check runs for every exchange path -- here the
+    process group's (no xGMI exchange) -- and a divergence re-times with the uncaptured process
+    group; replicas that still differ afterwards raise ReplicaDivergence, which bench.main turns
+    into exit 2 with no JSON line.  Also: capturing multi-rank RCCL is opt-in."""
+    import bench
+
+    calls = []
+
+    def retime():
+        calls.append("retime")
+        return 1.25
+
+    # healthy: no re-time
+    assert bench.verify_replicas(lambda: True, retime) == (True, None, None) and calls == []
+    # process-group path, replicas diverged once: re-timed, the new time is reported
+    seq = iter([False, True])
+    assert bench.verify_replicas(lambda: next(seq), retime) == (True, "replicas diverged", 1.25)
+    assert calls == ["retime"]
+    # an xGMI barrier timeout with identical replicas still re-times
+    assert bench.verify_replicas(lambda: True, retime, lambda: True)[1] == "barrier timeout"
+    # persistent divergence: no number
+    calls.clear()
+    with pytest.raises(bench.ReplicaDivergence):
+        bench.verify_replicas(lambda: False, retime)
+    assert calls == ["retime"]
+    # multi-rank RCCL capture is opt-in (flag or SL_GRAPH_COLLECTIVES=1)
+    assert bench.parse([]).graph_collectives is False
+    assert bench.parse(["--graph-collectives"]).graph_collectives is True
+
+
 def test_ps_new_incarnation_restarts_old_and_anonymous_entries_are_bounded():
     from serverless_learn_amd.parallel.ps import ParameterServer
 
@@ -565,6 +596,51 @@ def test_worker_drops_graphs_before_regroup_and_multirank_rccl_capture_is_opt_in
     t.allreduce = None
     w.cfg.graph_collectives = False
     assert w._use_graph() is True  # no host-side collective in the step: always captured
+
+
+def test_worker_aborts_communicator_before_draining_graphs_that_hold_collectives(monkeypatch):
+    """a replayed graph can sit inside a collective whose peer died, and
+    the watchdog does not see it, so draining the device first would hang the regroup.  When
+    the group is broken, or when the captured graphs hold collectives, _drop_graphs aborts the
+    communicator (teardown) BEFORE the device drain; graphs of kernels only drain with the
+    group untouched."""
+    from serverless_learn_amd.runtime.local_cluster import fast_config
+    from serverless_learn_amd.runtime.worker import Worker
+
+    events = []
+
+    class T(_FakeGraphTrainer):
+        def drop_graphs(self):
+            events.append("drain")  # FusedMLPTrainer.drop_graphs syncs the device here
+            self.graph = self.graph_unrolled = None
+
+    class G:
+        backend, world = "nccl", 2
+
+        def __init__(self, broken):
+            self.broken, self.pg = broken, object()
+
+        @property
+        def active(self):
+            return self.pg is not None
+
+        def teardown(self):
+            events.append("abort")
+            self.pg = None
+
+    w = Worker("127.0.0.1:0", fast_config(graph_steps=4))
+    monkeypatch.setattr(w, "_use_graph", lambda: True)
+    for broken, collectives, want in ((True, False, ["abort", "drain"]), (False, True, ["abort", "drain"]),
+                                      (False, False, ["drain"])):
+        events.clear()
+        t = T()
+        t.allreduce = (lambda g: None) if collectives else None
+        w.trainer, w.group = t, G(broken)
+        w._run_chunk(4)  # eager first step + capture: records whether the graphs hold collectives
+        assert w._graph_collectives is collectives
+        w._drop_graphs()
+        assert events == want, (broken, collectives, events)
+        assert not w._graph_collectives
 
 
 def test_allreduce_async_enqueue_failure_is_group_broken():

@@ -51,6 +51,30 @@ def test_additive_fields_are_skipped_by_an_original_parser():
     assert list(old.peer_addrs) == ["a:1", "b:2"]
 
 
+def test_flow_feedback_with_step_phases_parses_with_the_original_empty_schema():
+    """FlowFeedback is empty in the original (/root/reference/src/protos/serverless_learn.proto:73-75):
+    an original parser skips every additive field, the step-time breakdown (fields 11-16) included,
+    and an original (empty) FlowFeedback decodes here with all phases zero."""
+    from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+    fdp = descriptor_pb2.FileDescriptorProto(name="old_fb.proto", package="old", syntax="proto3")
+    fdp.message_type.add(name="FlowFeedback")
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fdp)
+    Old = message_factory.GetMessageClass(pool.FindMessageTypeByName("old.FlowFeedback"))
+    new = pb.FlowFeedback(step=9, samples_per_sec=1e6, step_ms=0.11, data_wait_ms=0.01, compute_ms=0.09,
+                          exchange_ms=0.015, update_ms=0.008, exchange_gbps=71.8)
+    raw = new.SerializeToString()
+    old = Old.FromString(raw)
+    assert old.SerializeToString() == b"" or old.ByteSize() >= 0  # parsed (unknown fields kept or dropped)
+    back = pb.FlowFeedback.FromString(Old().SerializeToString())
+    assert back.compute_ms == 0.0 and back.exchange_gbps == 0.0
+    got = {f.name: f.number for f in pb.PROTO.messages["FlowFeedback"]}
+    assert [got[k] for k in ("step_ms", "data_wait_ms", "compute_ms", "exchange_ms", "update_ms",
+                             "exchange_gbps")] == [11, 12, 13, 14, 15, 16]
+    assert pb.FlowFeedback.FromString(raw).exchange_gbps == 71.8
+
+
 @settings(max_examples=60, deadline=None)
 @given(st.lists(st.floats(allow_nan=False, allow_infinity=True, width=64), max_size=300))
 def test_update_roundtrip_f64(vals):

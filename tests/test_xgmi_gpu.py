@@ -50,4 +50,4 @@ def test_bench_four_rank_rehearsal_replicas_identical():
     r = json.loads(line)
     assert r["n_gpus"] == 4 and r["dist"]["world_size"] == 4, r
     assert r["replicas_identical"] is True, r
-    assert r["value"] > 0 and "xgmi_fallback" not in r, r
+    assert r["value"] > 0 and "replica_fallback" not in r, r
