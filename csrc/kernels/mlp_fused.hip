@@ -15,7 +15,7 @@
 //           and dH1 are written row-major with coalesced 16-B stores for the
 //           weight gradient; [dW3 | db3] (10 x 257) and the bias gradients
 //           db1 / db2 are computed here from the LDS images as one fp32
-//           partial row per 64 rows, so H2 and dZ never reach HBM.
+//           partial row per workgroup, so H2 and dZ never reach HBM.
 //   K_wgrad (mlp_wgrad_kernel) grouped split-K GEMM dW = dH^T . A over the
 //           batch for dW1 (A = raw u8 X, taken as the exact fp16 1024 + u
 //           against a power-of-two-scaled fp16 dH1: one v_perm per two
@@ -174,10 +174,11 @@ struct MlpRowArgs {
   float xa, xb, grad_scale;
   float dh1_scale;                     // dH1 goes to HBM as fp16 of dH1 * dh1_scale (a power of two)
   uint16_t* h1;                        // row-major [batch][256]
-  float* w3p;                          // [batch / 64][W3P_LD] partial [dW3 | db3 | db1 | db2]
+  float* w3p;                          // [batch / BM][W3P_LD] partial [dW3 | db3 | db1 | db2]
   uint16_t *dh2, *dh1;                 // row-major [batch][256]: dH2 bf16, dH1 fp16 (scaled)
   float *loss, *correct, *logits;
   unsigned long long* stamps;  // diagnostics: per-workgroup phase timestamps (nullptr in production)
+  unsigned* step_ctr;          // xGMI inline mode: the exchange's step id, advanced once per step here
 };
 
 // Fully unrolled K loop with a D-deep register ring for the per-wave B operand
@@ -384,6 +385,9 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   };
   stamp(0);
   if (a.stamps && tid == 0) a.stamps[(long)blockIdx.x * ROW_STAMPS + 16] = __builtin_amdgcn_s_memrealtime();
+  // the step's first kernel advances the xGMI step id (inline synchronisation, xgmi.h): every
+  // reader of it runs later in the stream, and the previous step's readers have finished
+  if (a.step_ctr && blockIdx.x == 0 && tid == 0) atomicAdd(a.step_ctr, 1u);
   // Workgroup barrier.  The 128-row tile waits only for LDS
   // traffic: __syncthreads() also drains every outstanding global store (vmcnt(0)), and
   // with all CUs storing the same activation at once that drain stalled the CU for
@@ -849,13 +853,13 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   bar();
   stamp(5);
 
-  // ---- [dW3 | db3] partial over this wave's 64 rows: dZ^T (RZ) . H2 (R0), both read
+  // ---- [dW3 | db3] partial over the workgroup's BM rows: dZ^T (RZ) . H2 (R0), both read
   // transposed (ds_read_b64_tr_b16).  The weight-gradient kernel would otherwise need
   // H2 and dZ in HBM (a [batch][256] write here + a re-read there) and spend 2 of its
-  // 20 tiles on a 10-row GEMM.  The wgrad kernel sums the partials in a fixed order. ----
-#pragma unroll
-  for (int hr = 0; hr < MF / 4; ++hr) {  // one partial row per 64 of this wave's rows
-    const int rh = rw + 64 * hr;
+  // 20 tiles on a 10-row GEMM.  The wgrad kernel sums the partials in a fixed order.
+  // One partial row per workgroup (BM rows): the 128-row tile wrote one per 64 rows until
+  // round 5, 12.6 MB per step written here and re-read by the weight gradient instead of 6.3. ----
+  {
     floatx4_t d3[NF], db3 = zero4();
 #pragma unroll
     for (int n = 0; n < NF; ++n) d3[n] = zero4();
@@ -863,14 +867,14 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int k0 = rh + 32 * ks;
+    for (int ks = 0; ks < MF / 2; ++ks) {  // 32-row k-steps over all BM rows
+      const int k0 = rw + 32 * ks;
       const short8_t af = lds_tr8(RZ + k0 * DZL, DZL, lane);  // A[c][row] = dZ[row][c]
 #pragma unroll
       for (int n = 0; n < NF; ++n) d3[n] = mfma16(af, lds_tr8(R0 + k0 * HS_LD + cw + n * 16, HS_LD, lane), d3[n]);
       if (wng == 0) db3 = mfma16(af, ones, db3);
     }
-    float* part = a.w3p + (long)((row0 + rh) >> 6) * W3P_LD;
+    float* part = a.w3p + (long)blockIdx.x * W3P_LD;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int c = 4 * lg + r;
@@ -906,27 +910,23 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
   masked_out(R0);
   bar();
   stamp(7);
-  // column sums of the masked dH2 over this wave's 64 rows: the db2 partial (ones-row MFMA)
+  // column sums of the masked dH2 over the workgroup's BM rows: the db2 partial (ones-row MFMA)
   auto col_sums = [&](const uint16_t* img, int off) {
     short8_t ones;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
+    floatx4_t cs[NF];
 #pragma unroll
-    for (int hr = 0; hr < MF / 4; ++hr) {
-      const int rh = rw + 64 * hr;
-      floatx4_t cs[NF];
+    for (int n = 0; n < NF; ++n) cs[n] = zero4();
 #pragma unroll
-      for (int n = 0; n < NF; ++n) cs[n] = zero4();
+    for (int ks = 0; ks < MF / 2; ++ks)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int n = 0; n < NF; ++n)
+        cs[n] = mfma16(ones, lds_tr8(img + (rw + 32 * ks) * HS_LD + cw + n * 16, HS_LD, lane), cs[n]);
+    if (lg == 0) {
+      float* part = a.w3p + (long)blockIdx.x * W3P_LD + off;
 #pragma unroll
-        for (int n = 0; n < NF; ++n)
-          cs[n] = mfma16(ones, lds_tr8(img + (rh + 32 * ks) * HS_LD + cw + n * 16, HS_LD, lane), cs[n]);
-      if (lg == 0) {
-        float* part = a.w3p + (long)((row0 + rh) >> 6) * W3P_LD + off;
-#pragma unroll
-        for (int n = 0; n < NF; ++n) st_out(&part[cw + n * 16 + lr], cs[n][0]);
-      }
+      for (int n = 0; n < NF; ++n) st_out(&part[cw + n * 16 + lr], cs[n][0]);
     }
   };
   col_sums(R0, W3P_DB2);
@@ -959,11 +959,9 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
     const int voff8 = ((rw + lr) * HID + cw + 4 * lg) * 2;
     const float sc = a.dh1_scale;
     uint32_t hv[NF][2];
-    floatx4_t cs[MF / 4][NF];
+    floatx4_t cs[NF];
 #pragma unroll
-    for (int hr = 0; hr < MF / 4; ++hr)
-#pragma unroll
-      for (int n = 0; n < NF; ++n) cs[hr][n] = zero4();
+    for (int n = 0; n < NF; ++n) cs[n] = zero4();
 #pragma unroll
     for (int m = 0; m < MF; ++m) {
 #pragma unroll
@@ -973,7 +971,7 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)  // bit r sign-extended to an all-ones / zero mask
           v[r] = __int_as_float(__float_as_int(acc[m][n][r]) & __builtin_amdgcn_sbfe(b, r, 1));
-        cs[m >> 2][n] += v;
+        cs[n] += v;
         const floatx4_t vs = v * sc;
         hv[n][0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(vs[0], vs[1]));
         hv[n][1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(vs[2], vs[3]));
@@ -985,20 +983,17 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
         __builtin_amdgcn_raw_buffer_store_b64(h, dst, voff8, (m * 16 * HID + n * 16) * 2, OUT_AUX_NARROW);
       }
     }
-    // Transpose-reduce of the 32 column partials over the 16 rows of a DPP row: each
+    // Transpose-reduce of the 16 column partials over the 16 rows of a DPP row: each
     // stage pairs lane i with i^15, i^7, i^2, i^1 (row_mirror, row_half_mirror, quad
     // perms), keeps the half of the values chosen by the lane bit the partners differ
-    // in and adds the partner's other half: 90 VALU instead of 32 row16_sums (256).
-    // Value index hr*16 + n*4 + r; lane lr ends with index j*16 + lr0*8 + lr1*4 +
-    // lr2*2 + lr3 (lrK = bit K of lr) for j = 0, 1.
-    static_assert(MF / 4 == 2 && NF == 4, "32 partials per lane");
-    float red[32];
+    // in and adds the partner's other half.  Value index n*4 + r; lane lr ends with index
+    // lr0*8 + lr1*4 + lr2*2 + lr3 (lrK = bit K of lr).
+    static_assert(NF == 4, "16 partials per lane");
+    float red[16];
 #pragma unroll
-    for (int hr = 0; hr < 2; ++hr)
+    for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[hr * 16 + n * 4 + r] = cs[hr][n][r];
+      for (int r = 0; r < 4; ++r) red[n * 4 + r] = cs[n][r];
     auto stage = [&](auto ctrl_c, int bit, int cnt) {
       constexpr int CTRL = decltype(ctrl_c)::value;
 #pragma unroll
@@ -1008,15 +1003,13 @@ __global__ __launch_bounds__(256, 2) void mlp_rows_kernel(MlpRowArgs a) {
         red[i] = keep + dpp_f<CTRL>(send);
       }
     };
-    stage(std::integral_constant<int, 0x140>{}, (lr >> 3) & 1, 16);
-    stage(std::integral_constant<int, 0x141>{}, (lr >> 2) & 1, 8);
-    stage(std::integral_constant<int, 0x4E>{}, (lr >> 1) & 1, 4);
-    stage(std::integral_constant<int, 0xB1>{}, lr & 1, 2);
+    stage(std::integral_constant<int, 0x140>{}, (lr >> 3) & 1, 8);
+    stage(std::integral_constant<int, 0x141>{}, (lr >> 2) & 1, 4);
+    stage(std::integral_constant<int, 0x4E>{}, (lr >> 1) & 1, 2);
+    stage(std::integral_constant<int, 0xB1>{}, lr & 1, 1);
     {
       const int n = 2 * (lr & 1) + ((lr >> 1) & 1), r = 2 * ((lr >> 2) & 1) + ((lr >> 3) & 1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        st_out(&a.w3p[(long)((row0 + rw + 64 * j) >> 6) * W3P_LD + W3P_DB1 + cw + n * 16 + 4 * lg + r], red[j]);
+      st_out(&a.w3p[(long)blockIdx.x * W3P_LD + W3P_DB1 + cw + n * 16 + 4 * lg + r], red[0]);
     }
     stamp(15);
   } else {
@@ -1099,7 +1092,7 @@ struct WgArgs {
   long slab_stride;
   const int* cursor;  // X is the resident shard: rows start at batch_base(cursor)
   int n_batches, batch;
-  const float* w3p;      // [n_w3p][W3P_LD] partial rows of the rows kernel
+  const float* w3p;      // [n_w3p][W3P_LD] partial rows of the rows kernel (one per rows workgroup)
   int n_w3p;
   unsigned long long* stamps;  // diagnostics: [logical workgroup][WG_STAMPS] (nullptr in production)
 };
@@ -1194,6 +1187,37 @@ __device__ __forceinline__ void wg_vmcnt(int younger) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Workgroup -> (slice, tile) placement.  A slice's 7 dW1 tiles all stream the same dH1 rows
+// (and the same X cache lines: 784-B rows straddle 128-B lines, so neighbouring tiles share
+// lines), its 2 dW2 tiles the same dH2 rows: each such group should sit on ONE XCD so that its
+// operand rows come from HBM once and are shared through that XCD's L2.  Workgroups are dealt
+// round-robin over the 8 XCDs (block b on XCD b % 8 -- observed, a speed matter only), so the
+// 252 of the default grid (9 tiles x 28 slices) are 32 on XCDs 0-3 and 31 on 4-7: XCDs 0-6 take
+// 4 whole dW1 groups (28) each, XCDs 0-3 two dW2 pairs and 4-6 one and a half, XCD 7 the
+// remaining 31 dW2 tiles -- 2 of the 28 dW2 pairs straddle XCDs, no dW1 group does.  The
+// generic remap (consecutive logical tiles per XCD, 9 per slice) splits about 7 slices
+// (profiles/r06_place: 195 MB read for 164 MB of operands).  Other grids keep it.
+#ifndef SL_WG_PLACE
+#define SL_WG_PLACE 1
+#endif
+__device__ __forceinline__ void wg_place(int bid, int nwg, int total_tiles, int& s, int& t) {
+  if (SL_WG_PLACE && nwg == 252 && total_tiles == 9) {
+    const int x = bid & 7, idx = bid >> 3;
+    if (x < 7 && idx < 28) {
+      s = 4 * x + idx / 7;
+      t = idx % 7;
+      return;
+    }
+    const int q = x < 7 ? (x < 4 ? 4 * x : 16 + 3 * (x - 4)) + (idx - 28) : 25 + idx;  // dW2 tile index 0..55
+    s = q >> 1;
+    t = 7 + (q & 1);
+    return;
+  }
+  const int logical = xcd_remap(bid, nwg);
+  s = logical / total_tiles;
+  t = logical - s * total_tiles;
+}
+
 constexpr int WG_NT = 512;
 constexpr int WG_MI = 8;  // 16-row A (dZ) fragments per wave
 constexpr int WG_NJ = 2;  // 16-column B fragments per wave
@@ -1206,9 +1230,9 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches on it stay uniform
   const int wm = wave & 1, wn = wave >> 1;
   const int lr = lane & 15, lg = lane >> 4;
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int s = logical / A.total_tiles;
-  const int t = logical - s * A.total_tiles;
+  int s, t;
+  wg_place(blockIdx.x, gridDim.x, A.total_tiles, s, t);
+  const int logical = s * A.total_tiles + t;  // stamps
   const int pi = t >= A.p[1].tile_base ? 1 : 0;
   const WgProblem& P = A.p[pi];
   const int tn = t - P.tile_base;
@@ -1457,8 +1481,10 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (A.stamps && tid == 0) A.stamps[logical * WG_STAMPS + 1] = __builtin_amdgcn_s_memtime();
 
-  // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2] per
-  // 64 rows): tile t of the slice takes a band of float4 columns, G row groups per column,
+  // ---- the slice's sums of the rows kernel's partial rows ([dW3 | db3 | db1 | db2], one per
+  // rows workgroup): slice s sums partial rows [s ppr, (s + 1) ppr) -- any partition of them
+  // over the slices works, the SGD kernel adds every slice -- and tile t of the slice takes a
+  // band of float4 columns, G row groups per column,
   // a fixed-order sum through LDS (deterministic).  Done HERE, around the slab stores: the
   // loads are issued first (every row of the band at once, clamped indices so no branch
   // splits them), the accumulator stores go out while they are in flight, and the sum
@@ -1469,12 +1495,15 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
   const int per = (NC4 + A.total_tiles - 1) / A.total_tiles;
   const int c0 = t * per, nc = min(NC4, c0 + per) - c0;
   const int G = WG_NT / nc, col = tid % nc, g = tid / nc;
-  const float4* psrc = reinterpret_cast<const float4*>(A.w3p + (long)st0 * W3P_LD) + c0 + col;
-  const bool pr_regs = (nst + G - 1) / G <= PR_MAX;
+  const int n_slices = (A.total_steps + A.steps_per_slice - 1) / A.steps_per_slice;
+  const int ppr = (A.n_w3p + n_slices - 1) / n_slices;
+  const int pr0 = min(s * ppr, A.n_w3p - 1), npr = max(0, min(ppr, A.n_w3p - s * ppr));
+  const float4* psrc = reinterpret_cast<const float4*>(A.w3p + (long)pr0 * W3P_LD) + c0 + col;
+  const bool pr_regs = (npr + G - 1) / G <= PR_MAX;
   float4 pv[PR_MAX];
   if (g < G && pr_regs) {
 #pragma unroll
-    for (int i = 0; i < PR_MAX; ++i) pv[i] = psrc[(long)min(g + i * G, nst - 1) * NC4];
+    for (int i = 0; i < PR_MAX; ++i) pv[i] = psrc[(long)max(0, min(g + i * G, npr - 1)) * NC4];
   }
 
   // ---- epilogue: the MFMAs took their operands swapped (B first), so each lane holds
@@ -1503,11 +1532,11 @@ __global__ __launch_bounds__(WG_NT, 1) void mlp_wgrad_kernel(WgArgs A) {
     if (pr_regs) {
 #pragma unroll
       for (int i = 0; i < PR_MAX; ++i) {
-        const float w = g + i * G < nst ? 1.f : 0.f;  // select after the load, not around it
+        const float w = g + i * G < npr ? 1.f : 0.f;  // select after the load, not around it
         sum.x += w * pv[i].x; sum.y += w * pv[i].y; sum.z += w * pv[i].z; sum.w += w * pv[i].w;
       }
     } else {
-      for (int k = g; k < nst; k += G) {
+      for (int k = g; k < npr; k += G) {
         const float4 v = psrc[(long)k * NC4];
         sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
       }
@@ -1562,6 +1591,9 @@ struct SgdArgs {
   const unsigned* ar_ctl;
   long long* r1p;  // fixed-point partial row sums of the fp16 W1 shadow (tiled mode 2 writes them)
   unsigned long long* stamps;  // diagnostics, tiled path: [workgroup][2] start / end s_memrealtime
+  // xGMI exchange (mode 1 into an exchange slot): the slot parity follows the step in flight,
+  // whose id depends on the synchronisation mode (xg_cur)
+  XgArgs xg;
 };
 
 // Shadow copies of the new weight: fp16 for W1 (layer 1 multiplies exact fp16 pixels), bf16
@@ -1687,7 +1719,7 @@ __device__ __forceinline__ long long sgd_tiled(const SgdArgs& a, long u, int par
   }
   if (!mine) return 0;
   float* gout = a.grad_out;
-  if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
+  if (a.ar_ctl && (xg_cur(a.ar_ctl, a.xg.inline_sync) & 1u)) gout = a.grad_out_alt;
   return sgd_apply(a, gout, pe, gme, w0, m0);
 }
 
@@ -1743,7 +1775,7 @@ __global__ __launch_bounds__(SGD_NT) void mlp_sgd_kernel(SgdArgs a) {
   const float gme = mine ? a.grad_in[p] : 0.f;
   if (!mine) return;
   float* gout = a.grad_out;
-  if (a.ar_ctl && (xg_step(a.ar_ctl) & 1u)) gout = a.grad_out_alt;
+  if (a.ar_ctl && (xg_cur(a.ar_ctl, a.xg.inline_sync) & 1u)) gout = a.grad_out_alt;
   sgd_apply(a, gout, p, gme, w0, m0);
 }
 
@@ -1758,42 +1790,86 @@ __global__ __launch_bounds__(64) void mlp_w1_rowsum_kernel(const uint16_t* w1h, 
   r1p[m * R1_BLK + j] = s;
 }
 
-// Multi-GPU update (after sl_xgmi_barrier): one thread per 4 parameters sums the W ranks' reduced gradients
-// straight out of their exchange buffers over xGMI (rank order: identical on every
-// replica) -- or, two-shot, reads the chunk owner's all-reduced value -- then applies momentum SGD and refreshes the bf16 shadows -- the all-reduce
-// and the optimizer step in one launch, no RCCL call and no host sync (xgmi.h).
-__global__ __launch_bounds__(256) void mlp_sgd_xgmi_kernel(SgdArgs a, XgArgs x) {
+// Update from an aggregated gradient (no slab): the RCCL path's all-reduced gradient (XG =
+// false: a.grad_in) or the xGMI exchange (XG = true: every rank's slot summed in rank order
+// straight over xGMI -- or, two-shot, each chunk read from its owner's reduced slot), then
+// momentum SGD and the shadow refresh: the all-reduce's consumer and the optimizer step in one
+// launch.  Work items: the 256 W1 rows (196 float4 each; the row's R1_BLK fixed-point partial
+// sums of its new fp16 shadow come out of the same pass: 8 lanes per 32-column block, so the
+// separate row-sum launch is gone), then 1,024-parameter chunks of b1 W2 b2 W3 b3.
+// Inline xGMI mode: each workgroup waits for the step's signals first (xg_block_wait).
+constexpr int UPD_NT = 256;
+constexpr int UPD_W1_ROW4 = D_IN / 4;  // 196 float4 per W1 row
+constexpr int UPD_REST_TASKS = (int)((P_N - P_B1 + 4 * UPD_NT - 1) / (4 * UPD_NT));
+constexpr int UPD_TASKS = HID + UPD_REST_TASKS;
+static_assert(P_B1 % 4 == 0 && D_IN % 32 == 16 && 8 * R1_BLK <= UPD_NT, "update work items");
+
+// Two-shot consumer read that is safe for any wave: a W1 row's waves are not 64-float4 aligned,
+// so one wave may span two chunk owners (lo, lo + 1); that rare wave loads from both.
+__device__ __forceinline__ float4 xg_load_reduced_any(const XgArgs& x, unsigned s, long i) {
+  const int owner = (int)(i / x.chunk4);
+  const int lo = __builtin_amdgcn_readfirstlane(owner);
+  const unsigned off = xg_red_off(x, s) + (unsigned)(i * 16);
+  const float4 va = xg_load(xg_rsrc(x, lo), off);
+  if (!__builtin_amdgcn_ballot_w64(owner != lo)) return va;
+  const float4 vb = xg_load(xg_rsrc(x, lo + 1 < x.world ? lo + 1 : lo), off);
+  return owner == lo ? va : vb;
+}
+
+template <bool XG>
+__global__ __launch_bounds__(UPD_NT) void mlp_update_kernel(SgdArgs a, XgArgs x) {
   __shared__ unsigned s_step;
-  if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.cursor, 1);
-  const unsigned s = xg_block_step(x, &s_step);  // xgmi_barrier_kernel ran just before
-  const long p0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (p0 < a.n) {
-    float4 g;
-    float4 w4, m4;
-    if (x.chunk4 > 0) {  // two-shot: the chunk's owner already summed it (xgmi_rs_kernel)
-      g = xg_load_reduced(x, s, p0 / 4);
-      w4 = *reinterpret_cast<const float4*>(a.w + p0);
-      m4 = a.mom ? *reinterpret_cast<const float4*>(a.mom + p0) : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
-      float4 v[XG_MAX_WORLD];
-#pragma unroll
-      for (int q = 0; q < XG_MAX_WORLD; ++q)
-        if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), xg_slot_off(x, s) + (unsigned)(p0 * 4));
-      w4 = *reinterpret_cast<const float4*>(a.w + p0);
-      m4 = a.mom ? *reinterpret_cast<const float4*>(a.mom + p0) : make_float4(0.f, 0.f, 0.f, 0.f);
-      g = v[0];
-#pragma unroll
-      for (int q = 1; q < XG_MAX_WORLD; ++q)
-        if (q < x.world) {
-          g.x += v[q].x; g.y += v[q].y; g.z += v[q].z; g.w += v[q].w;
-        }
-    }
-    const float ga[4] = {g.x, g.y, g.z, g.w}, wa[4] = {w4.x, w4.y, w4.z, w4.w}, ma[4] = {m4.x, m4.y, m4.z, m4.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (p0 + j < a.n) sgd_apply(a, nullptr, p0 + j, ga[j], wa[j], ma[j]);
+  const int tid = threadIdx.x;
+  if (a.cursor && blockIdx.x == 0 && tid == 0) atomicAdd(a.cursor, 1);
+  unsigned s = 0;
+  if constexpr (XG) {
+    s = xg_block_step(x, &s_step);
+    if (x.inline_sync) xg_block_wait(x, x.chunk4 > 0 ? 1 : 0, s);  // two-shot: the owners' reduced slots
   }
-  xg_finish(x, s);
+  for (int task = blockIdx.x; task < UPD_TASKS; task += gridDim.x) {
+    const bool w1 = task < HID;  // uniform per workgroup
+    const long first = w1 ? (long)task * UPD_W1_ROW4 : P_B1 / 4 + (long)(task - HID) * UPD_NT;
+    const long i4 = first + tid;
+    const bool live = w1 ? tid < UPD_W1_ROW4 : i4 * 4 < P_N;
+    const long ic = live ? i4 : first;  // dead lanes load a live address (same owner), unused
+    float4 g;
+    if constexpr (XG) {
+      if (x.chunk4 > 0) {
+        g = xg_load_reduced_any(x, s, ic);
+      } else {
+        float4 v[XG_MAX_WORLD];
+#pragma unroll
+        for (int q = 0; q < XG_MAX_WORLD; ++q)
+          if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), xg_slot_off(x, s) + (unsigned)(ic * 16));
+        g = v[0];
+#pragma unroll
+        for (int q = 1; q < XG_MAX_WORLD; ++q)
+          if (q < x.world) {
+            g.x += v[q].x; g.y += v[q].y; g.z += v[q].z; g.w += v[q].w;
+          }
+      }
+    } else {
+      g = reinterpret_cast<const float4*>(a.grad_in)[ic];
+    }
+    const float4 w4 = reinterpret_cast<const float4*>(a.w)[ic];
+    const float4 m4 = a.mom ? reinterpret_cast<const float4*>(a.mom)[ic] : make_float4(0.f, 0.f, 0.f, 0.f);
+    long long fx = 0;
+    if (live) {
+      const float ga[4] = {g.x, g.y, g.z, g.w}, wa[4] = {w4.x, w4.y, w4.z, w4.w}, ma[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (i4 * 4 + j < P_N) fx += sgd_apply(a, nullptr, i4 * 4 + j, ga[j], wa[j], ma[j]);
+    }
+    if (w1) {  // 32-column block b = lanes 8b .. 8b+7 of the row (the 25th: 4 live lanes + 4 dead)
+      fx += __shfl_xor(fx, 1);
+      fx += __shfl_xor(fx, 2);
+      fx += __shfl_xor(fx, 4);
+      if ((tid & 7) == 0 && tid < 8 * R1_BLK) a.r1p[task * R1_BLK + (tid >> 3)] = fx;
+    }
+  }
+  if constexpr (XG) {
+    if (!x.inline_sync) xg_finish(x, s);  // inline: the next step's rows kernel advances the step
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1844,7 +1920,8 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
                 const uint16_t* w3th, const float* params, float xa, float xb,
                 float grad_scale, float dh1_scale,
                 uint16_t* h1, float* w3p, uint16_t* dh2, uint16_t* dh1,
-                float* loss, float* correct, float* logits, int train, const long long* r1p, hipStream_t stream) {
+                float* loss, float* correct, float* logits, int train, const long long* r1p, unsigned* step_ctr,
+                hipStream_t stream) {
   if (batch <= 0 || batch % BM != 0) return -1;
   MlpRowArgs a;
   a.x = x; a.y = y; a.cursor = cursor; a.n_batches = n_batches > 0 ? n_batches : 1; a.batch = batch;
@@ -1856,6 +1933,7 @@ int sl_mlp_rows(const uint8_t* x, const uint8_t* y, const int* cursor, int n_bat
   a.h1 = h1; a.w3p = w3p; a.dh2 = dh2; a.dh1 = dh1;
   a.loss = loss; a.correct = correct; a.logits = logits;
   a.stamps = g_stamps;
+  a.step_ctr = train ? step_ctr : nullptr;
   if (train && (!h1 || !w3p || !dh2 || !dh1)) return -2;
   const int bm = sl_mlp_rows_bm(batch);
   if (bm == 128) {
@@ -1885,7 +1963,9 @@ int sl_mlp_wgrad_slices(int batch, int requested) {
 int sl_mlp_wgrad(int batch, const uint8_t* x, const int* cursor, int n_batches, const uint16_t* h1,
                  const uint16_t* dh2, const uint16_t* dh1, const float* w3p, int n_w3p, float* slab, int slices,
                  long slab_stride, hipStream_t stream) {
-  if (!w3p || n_w3p != batch / 64) return -1;
+  // one partial row per rows-kernel workgroup (sl_mlp_rows_bm rows); n_w3p is the buffer's capacity
+  if (!w3p || n_w3p < batch / 64) return -1;
+  n_w3p = batch / sl_mlp_rows_bm(batch);
   if (slab_stride < TL_STRIDE) return -1;
   const int s_eff = sl_mlp_wgrad_slices(batch, slices);
   if (s_eff <= 0 || s_eff != slices) return -1;
@@ -1927,48 +2007,68 @@ int sl_mlp_sgd(float* w, float* mom, const float* slab, int slices, long slab_st
   if (mode == 1 && !grad_out) return -1;
   if (slab && (slab_stride & 3)) return -1;
   if (slab && slab_stride < TL_STRIDE) return -1;
+  if (mode == 2 && !slab) {
+    // update from an all-reduced gradient: one launch, the W1 row sums included
+    if (((uintptr_t)w | (uintptr_t)grad_in | (uintptr_t)(mom ? mom : w)) & 15) return -2;
+    hipLaunchKernelGGL(mlp_update_kernel<false>, dim3(UPD_TASKS), dim3(UPD_NT), 0, stream, a, XgArgs{});
+    SL_CHECK_LAUNCH();
+    return 0;
+  }
   const long groups = sgd_units(slab != nullptr && mode != 0);
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
-  if (mode == 0 || (mode == 2 && !slab)) {  // flat paths: the row sums from the new shadow
+  if (mode == 0) {  // shadow refresh: the row sums from the new shadow
     hipLaunchKernelGGL(mlp_w1_rowsum_kernel, dim3(HID), dim3(64), 0, stream, w1h, r1p);
     SL_CHECK_LAUNCH();
   }
   return 0;
 }
 
-// Slab reduction straight into this rank's xGMI exchange slot for the step in flight.
+static bool xg_fill(XgArgs& x, char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4,
+                    int inline_sync) {
+  if (!bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return false;
+  if (slot_bytes < ((P_N + 3) / 4) * 16 || (slot_bytes & 255)) return false;
+  if (chunk4 < 0 || (chunk4 > 0 && (chunk4 * world * 16 < slot_bytes || (chunk4 & 63)))) return false;
+  if (inline_sync < 0 || inline_sync > 2) return false;
+  x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world; x.chunk4 = chunk4;
+  x.inline_sync = inline_sync;
+  return true;
+}
+
+// Slab reduction straight into this rank's xGMI exchange slot for the step in flight (slot0 /
+// slot1: this rank's two payload slots; inline_sync only selects how the step id is kept).
 int sl_mlp_reduce_xgmi(const float* slab, int slices, long slab_stride, float xa, float xb, float* slot0,
-                       float* slot1, const unsigned* ctl, hipStream_t stream) {
-  if (!slab || !slot0 || !slot1 || !ctl || (slab_stride & 3)) return -1;
+                             float* slot1, char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world,
+                             long chunk4, int inline_sync, hipStream_t stream) {
+  if (!slot0 || !slot1) return -1;
   SgdArgs a = {};
+  if (!slab || (slab_stride & 3) || slab_stride < TL_STRIDE) return -1;
+  if (!xg_fill(a.xg, bases, ctl, slot_bytes, rank, world, chunk4, inline_sync)) return -1;
   a.slab = slab; a.slices = slices; a.slab_stride = slab_stride; a.grad_out = slot0; a.grad_out_alt = slot1;
   a.ar_ctl = ctl; a.n = P_N; a.xa = xa; a.xb = xb; a.mode = 1;
-  if (slab_stride < TL_STRIDE) return -1;
   const long groups = sgd_units(true);
   hipLaunchKernelGGL(mlp_sgd_kernel, dim3((groups * SGD_TPG + SGD_NT - 1) / SGD_NT), dim3(SGD_NT), 0, stream, a);
   SL_CHECK_LAUNCH();
   return 0;
 }
 
+// Multi-GPU update (one-shot: after the step's signals; two-shot: after the owners' reduce-
+// scatter): the W ranks' gradients summed over xGMI + momentum SGD + shadows + W1 row sums.
+// inline_sync 1 / 2: every workgroup waits for the signals itself (2 = ranks share the GPU:
+// at most XG_SHARED_GRID workgroups, so the peers' kernels keep CUs); 0: after the barrier kernel.
 int sl_mlp_sgd_xgmi(float* w, float* mom, float lr, float mu, float wd, uint16_t* w1h, uint16_t* w2h,
                     uint16_t* w2th, uint16_t* w3h, uint16_t* w3th, int* cursor, char* const* bases,
                     unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, long long* r1p,
-                    hipStream_t stream) {
-  if (!r1p) return -1;
-  if (!w || !bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return -1;
-  if (slot_bytes < ((P_N + 3) / 4) * 16 || (slot_bytes & 255)) return -1;
-  if (chunk4 < 0 || (chunk4 > 0 && (chunk4 * world * 16 < slot_bytes || (chunk4 & 63)))) return -1;
+                    int inline_sync, hipStream_t stream) {
+  if (!r1p || !w) return -1;
   if (((uintptr_t)w | (uintptr_t)(mom ? mom : w)) & 15) return -2;
   SgdArgs a = {};
   a.w = w; a.mom = mom; a.n = P_N; a.lr = lr; a.mu = mu; a.wd = wd; a.mode = 2;
-  a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor;
+  a.w1h = w1h; a.w2h = w2h; a.w2th = w2th; a.w3h = w3h; a.w3th = w3th; a.cursor = cursor; a.r1p = r1p;
   XgArgs x;
-  x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world; x.chunk4 = chunk4;
-  const long groups = (P_N + 3) / 4;
-  hipLaunchKernelGGL(mlp_sgd_xgmi_kernel, dim3((groups + 255) / 256), dim3(256), 0, stream, a, x);
-  SL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(mlp_w1_rowsum_kernel, dim3(HID), dim3(64), 0, stream, w1h, r1p);
+  if (!xg_fill(x, bases, ctl, slot_bytes, rank, world, chunk4, inline_sync)) return -1;
+  const int grid = inline_sync == 2 ? xg_shared_grid(UPD_TASKS, world) : UPD_TASKS;
+  hipLaunchKernelGGL(mlp_update_kernel<true>, dim3(grid), dim3(UPD_NT), 0, stream, a, x);
   SL_CHECK_LAUNCH();
   return 0;
 }

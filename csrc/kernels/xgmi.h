@@ -28,6 +28,24 @@
 // s + 1 -- and every peer signals s + 1 only after its step-s consumer kernel
 // (the reader of that slot) has finished.
 //
+// Inline synchronisation (XgArgs::inline_sync = 1, the default since round 6): no barrier
+// kernel.  The barrier's two halves move into the consumer kernel's prologue (xg_block_wait):
+// its workgroup 0 signals s into inbox[rank] of every buffer -- the producer kernel before it
+// in the stream has completed, so every payload byte is in memory -- and every workgroup then
+// waits for the W inboxes (one lane polls, same timeout and error word).  The step id is
+// advanced ONCE per step by the step's first kernel (the MLP rows kernel's workgroup 0, before
+// any producer or consumer of the step reads it), so the consumer needs no last-workgroup
+// fan-in at its end either: ctl[0] is the step IN FLIGHT in this mode (xg_cur), the number of
+// completed steps in the barrier mode (xg_step = ctl[0] + 1).  An earlier cut published from
+// the producer's last workgroup and kept the consumer's fan-in: 583 + 324 serialised returning
+// atomics made it slower than the barrier kernel it replaced (profiles/r06_xchg).  The
+// invariant above is unchanged (a rank signals s + 1 from its step-(s+1) consumer, which runs
+// after its step-s consumer).  Waiting workgroups hold their CUs: where ranks share one GPU
+// (the rehearsals) the consumer grids are bounded (xg_shared_grid) so a lagging rank's
+// kernels always find free CUs; with one rank per GPU the wait is the peers' skew.  The
+// one-wave barrier kernel stays as the fallback (SL_XGMI_BARRIER=1) and for the generic
+// all-reduce.
+//
 // Two-shot variant (chunk4 > 0; reduce-scatter + all-gather): one-shot moves W - 1
 // whole payloads into every GPU, (W - 1) x 1.08 MB over 7 links for the MLP at W = 8.
 // Two-shot moves 2 (W - 1) / W of one payload instead, for one more barrier:
@@ -51,11 +69,22 @@ constexpr unsigned long long XG_TIMEOUT_TICKS = 100ull * 1000 * 1000 * 10;  // 1
 
 struct XgArgs {
   char* const* bases;  // [world] device table: rank q's exchange buffer as mapped in this process
-  unsigned* ctl;       // local: [0] completed steps, [1] finished-block counter, [2] error (1 = timeout)
+  unsigned* ctl;       // local: [0] completed steps (barrier mode) / step in flight (inline mode),
+                       // [1] finished-block counter, [2] error (1 = timeout)
   long slot_bytes;     // payload slot size, multiple of 256
   int rank, world;
   long chunk4;         // two-shot: float4 elements reduced by each rank, multiple of 64 (0 = one-shot)
+  int inline_sync;     // 1: producers publish from their last workgroup, consumers wait per workgroup
 };
+
+// Consumer grids where ranks share one GPU (inline mode): the waiting workgroups of ALL ranks
+// together hold at most XG_SHARED_GRID of the 256 CUs, so a lagging rank's kernels -- the
+// weight gradient needs a whole CU per workgroup -- always find free CUs.
+constexpr int XG_SHARED_GRID = 64;
+__host__ __device__ constexpr int xg_shared_grid(int grid, int world) {
+  const int cap = XG_SHARED_GRID / (world > 0 ? world : 1);
+  return grid < cap ? grid : (cap > 0 ? cap : 1);
+}
 
 __device__ __forceinline__ unsigned* xg_inbox(char* base, int q, int set) {
   return reinterpret_cast<unsigned*>(base + (long)set * 1024 + (long)q * 64);
@@ -139,9 +168,44 @@ __device__ __forceinline__ void xg_signal_wait(const XgArgs& x, int set) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // "" = system scope
 }
 
+// Consumer side of the inline mode: workgroup 0 signals step s through `set` to every rank
+// (this rank's producer kernel has completed: stream order), then one lane of every workgroup
+// waits until every rank has signalled s (bounded: after XG_TIMEOUT_TICKS it records the error
+// word; a block that finds the word set -- another gave up -- stops waiting), and the workgroup
+// proceeds.  Every later read of a peer's bytes is a system-scope load (xg_load).
+__device__ __forceinline__ void xg_block_wait(const XgArgs& x, int set, unsigned s) {
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)x.world)
+    __hip_atomic_store(xg_inbox(x.bases[threadIdx.x], x.rank, set), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0 && __hip_atomic_load(x.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool give_up = false;
+    for (int q = 0; q < x.world && !give_up; ++q) {
+      const unsigned* f = xg_inbox(x.bases[x.rank], q, set);
+      while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - s) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__hip_atomic_load(x.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+          give_up = true;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > XG_TIMEOUT_TICKS) {
+          __hip_atomic_store(x.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          give_up = true;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Step id of the step in flight under either mode (inline: ctl[0] itself).
+__device__ __forceinline__ unsigned xg_cur(const unsigned* ctl, int inline_sync) {
+  return __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (inline_sync ? 0u : 1u);
+}
+
 // Step id for a consumer block (one load, shared through LDS).
 __device__ __forceinline__ unsigned xg_block_step(const XgArgs& x, unsigned* lds_step) {
-  if (threadIdx.x == 0) *lds_step = xg_step(x.ctl);
+  if (threadIdx.x == 0) *lds_step = xg_cur(x.ctl, x.inline_sync);
   __syncthreads();
   return *lds_step;
 }

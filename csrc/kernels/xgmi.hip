@@ -22,10 +22,12 @@ __global__ __launch_bounds__(256) void xgmi_copyin_kernel(XgArgs x, const float4
 __global__ __launch_bounds__(64) void xgmi_barrier_kernel(XgArgs x, int set) { xg_signal_wait(x, set); }
 
 // Two-shot reduce-scatter (after barrier set 0): this rank's chunk of the W slots,
-// summed in rank order into the same offsets of its own reduced slot.
+// summed in rank order into the same offsets of its own reduced slot.  Inline mode: workgroup 0
+// signals set 0 and every workgroup waits for it; the update kernel after it signals set 1.
 __global__ __launch_bounds__(256) void xgmi_rs_kernel(XgArgs x, long n4) {
   __shared__ unsigned s_step;
   const unsigned s = xg_block_step(x, &s_step);
+  if (x.inline_sync) xg_block_wait(x, 0, s);
   const unsigned off0 = xg_slot_off(x, s);
   float4* red = reinterpret_cast<float4*>(x.bases[x.rank] + xg_red_off(x, s));
   const long lo = (long)x.rank * x.chunk4;
@@ -91,13 +93,16 @@ static int xg_grid(long n4) {
   return (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
 }
 
-static bool xg_args(XgArgs& x, char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4) {
+static bool xg_args(XgArgs& x, char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4,
+                    int inline_sync = 0) {
   if (!bases || !ctl || world < 1 || world > XG_MAX_WORLD || rank < 0 || rank >= world) return false;
   if (slot_bytes <= 0 || (slot_bytes & 255)) return false;
   // two-shot: the W chunks must cover the slot, and be whole waves of float4 (a consumer wave
   // then reads ONE owner's buffer: xg_rsrc makes the owner wave-uniform with readfirstlane)
   if (chunk4 < 0 || (chunk4 > 0 && (chunk4 * world * 16 < slot_bytes || (chunk4 & 63)))) return false;
+  if (inline_sync < 0 || inline_sync > 2) return false;
   x.bases = bases; x.ctl = ctl; x.slot_bytes = slot_bytes; x.rank = rank; x.world = world; x.chunk4 = chunk4;
+  x.inline_sync = inline_sync;
   return true;
 }
 
@@ -158,13 +163,17 @@ int sl_xgmi_barrier(char* const* bases, unsigned* ctl, long slot_bytes, int rank
   return 0;
 }
 
-// Two-shot reduce-scatter of n floats (run between barrier sets 0 and 1).
+// Two-shot reduce-scatter of n floats (run between barrier sets 0 and 1; inline_sync 1 / 2:
+// waits for set 0 and publishes set 1 itself, 2 = ranks share the GPU: bounded grid).
 int sl_xgmi_rs(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int world, long chunk4, long n,
-               hipStream_t stream) {
+               int inline_sync, hipStream_t stream) {
   XgArgs x;
-  if (!xg_args(x, bases, ctl, slot_bytes, rank, world, chunk4) || chunk4 <= 0 || (n & 3) || n * 4 > slot_bytes)
+  if (!xg_args(x, bases, ctl, slot_bytes, rank, world, chunk4, inline_sync) || chunk4 <= 0 || (n & 3) ||
+      n * 4 > slot_bytes)
     return -1;
-  hipLaunchKernelGGL(xgmi_rs_kernel, dim3(xg_grid(chunk4)), dim3(256), 0, stream, x, n / 4);
+  int grid = xg_grid(chunk4);
+  if (inline_sync == 2) grid = xg_shared_grid(grid, world);
+  hipLaunchKernelGGL(xgmi_rs_kernel, dim3(grid), dim3(256), 0, stream, x, n / 4);
   SL_CHECK_LAUNCH();
   return 0;
 }

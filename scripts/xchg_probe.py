@@ -2,8 +2,9 @@
 """Fixed per-step cost of the MLP's xGMI gradient exchange on one GPU.
 
 A one-rank XgmiExchange runs the multi-GPU step's exact launch sequence -- slab reduction into
-the exchange slot, step barrier (two-shot: + reduce-scatter + second barrier), update kernel
-reading the slots back -- with no peer, so the difference to the 1-GPU step (slab reduction
+the exchange slot that publishes the step, (two-shot: reduce-scatter that waits and publishes,)
+update kernel that waits and reads the slots back; or the round-5 sequence with the one-wave
+barrier kernel(s) in between -- with no peer, so the difference to the 1-GPU step (slab reduction
 fused with the update) is the exchange's fixed cost.  Graph-replayed K-step regions, modes
 interleaved; one JSON line per mode.  Kernel times: run under rocprofv3 --kernel-trace --stats."""
 import json
@@ -27,11 +28,14 @@ def main() -> int:
     x, y = make_mnist_like(B * 4, seed=0)
     x, y = torch.from_numpy(x), torch.from_numpy(y)
     modes = {}
-    for mode in ("sgd", "xgmi_one_shot", "xgmi_two_shot"):
+    # inline synchronisation (the default since round 6: the reduce publishes, the update waits
+    # per workgroup) against the round-5 protocol with its one-wave barrier kernel(s)
+    for mode in ("sgd", "xgmi_one_shot", "xgmi_two_shot", "xgmi_one_shot_barrier", "xgmi_two_shot_barrier"):
         tr = FusedMLPTrainer(batch=B, device=dev)
         tr.load_shard(x, y)
         if mode != "sgd":
-            ex = XgmiExchange(tr.n_pad, 0, 1, dev, lambda b: [b], lambda ok: ok, two_shot=mode == "xgmi_two_shot")
+            os.environ["SL_XGMI_BARRIER"] = "1" if mode.endswith("_barrier") else "0"
+            ex = XgmiExchange(tr.n_pad, 0, 1, dev, lambda b: [b], lambda ok: ok, two_shot="two_shot" in mode)
             tr.enable_xgmi(ex)
         tr.step()
         tr.capture(warmup=1, unroll=K)

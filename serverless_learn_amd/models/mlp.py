@@ -219,13 +219,14 @@ class CPUTrainer:
         self.phases.mark("update")
         self._last = (float(loss), float(correct))
 
-    def probe_step(self) -> dict:
-        """One training step with its phases timed (utils/phases.py; wall clock on the CPU)."""
+    def probe_step(self):
+        """One training step with its phases timed (utils/phases.py; wall clock on the CPU):
+        a PendingPhases, ready at once."""
         self.phases.arm()
         self.step()
-        out = self.phases.finish()
-        out["exchange_bytes"] = 4 * int(self.params.numel()) if self.allreduce is not None else 0
-        return out
+        pending = self.phases.finish()
+        pending.exchange_bytes = 4 * int(self.params.numel()) if self.allreduce is not None else 0
+        return pending
 
     def stats(self) -> StepStats:
         loss, correct = self._last
@@ -384,7 +385,7 @@ class FusedMLPTrainer:
         """Cached launches for the current buffers/hyper-parameters (rebuilt on change)."""
         key = (self.x.data_ptr() if self.x is not None else 0, self.n_batches, self.grad_scale, self.lr,
                self.momentum, self.weight_decay, id(self.xgmi), bool(self.xgmi and self.xgmi.two_shot),
-               )
+               self.xgmi.inline_sync if self.xgmi is not None else None)
         if getattr(self, "_lkey", None) == key:
             return self._lc
         n, p = self._n, self._n.ptr
@@ -394,7 +395,9 @@ class FusedMLPTrainer:
                              p(self.w1h), p(self.w2h), p(self.w3h), p(self.w2th), p(self.w3th),
                              p(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                              p(self.h1t), p(self.w3p), p(self.dh2t), p(self.dh1t),
-                             p(self.loss), p(self.correct), None, 1, p(self.r1p)),
+                             p(self.loss), p(self.correct), None, 1, p(self.r1p),
+                             # xGMI inline synchronisation: this launch advances the exchange's step id
+                             self.xgmi.ctl.data_ptr() if self.xgmi is not None and self.xgmi.inline_sync else None),
             "wgrad": n.Launch("sl_mlp_wgrad", self.batch, p(self.x), p(self.cursor), self.n_batches,
                               p(self.h1t), p(self.dh2t), p(self.dh1t), p(self.w3p), self.w3p.shape[0], p(self.slab),
                               self.slices, self.slab_stride),
@@ -409,11 +412,12 @@ class FusedMLPTrainer:
                                 p(self.cursor) if bump else None, p(self.r1p))
         if self.xgmi is not None:
             xg = self.xgmi
+            # inline synchronisation: the reduce publishes the step, the update waits per workgroup
             lc["xreduce"] = n.Launch("sl_mlp_reduce_xgmi", p(self.slab), self.slices, self.slab_stride, *self.dw1_coeffs,
-                                     xg.slot_ptr(0), xg.slot_ptr(1), xg.ctl.data_ptr())
+                                     xg.slot_ptr(0), xg.slot_ptr(1), *xg.args(), xg.inline_sync)
             lc["xbarrier"] = [n.Launch(fn, *xg.args(), *extra) for fn, extra in xg.exchange_launches(self.n_pad)]
             lc["xupdate"] = n.Launch("sl_mlp_sgd_xgmi", p(self.params), p(self.mom), self.lr, self.momentum,
-                                     self.weight_decay, *ws, p(self.cursor), *xg.args(), p(self.r1p))
+                                     self.weight_decay, *ws, p(self.cursor), *xg.args(), p(self.r1p), xg.inline_sync)
         self._lc, self._lkey = lc, key
         return lc
 
@@ -425,7 +429,7 @@ class FusedMLPTrainer:
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, self.grad_scale, self.dh1_scale,
                n.ptr(self.h1t), n.ptr(self.w3p), n.ptr(self.dh2t), n.ptr(self.dh1t),
-               n.ptr(self.loss), n.ptr(self.correct), None, 0, n.ptr(self.r1p), n.stream_ptr())
+               n.ptr(self.loss), n.ptr(self.correct), None, 0, n.ptr(self.r1p), None, n.stream_ptr())
 
     def _wgrad(self):
         self._launches()["wgrad"]()
@@ -436,7 +440,8 @@ class FusedMLPTrainer:
         self._launches()[name]()
 
     def compute_grads(self) -> torch.Tensor:
-        """Forward + backward only; returns the reduced (local) gradient."""
+        """Forward + backward only; returns the reduced (local) gradient (not with an xGMI
+        exchange enabled: its rows launch advances the exchange's step id)."""
         self._rows(True)
         self._wgrad()
         self._sgd(1, from_grad=False, grad_out=True, bump=False)
@@ -518,14 +523,15 @@ class FusedMLPTrainer:
             self._sgd(2, from_grad=True, grad_out=False)
         ph.mark("update")
 
-    def probe_step(self) -> dict:
-        """One eager training step with its phases timed (utils/phases.py): {phase: ms} plus
+    def probe_step(self):
+        """One eager training step with its phase boundaries recorded (utils/phases.py): returns
+        a PendingPhases (resolved by the caller once the device has finished the step) carrying
         the gradient payload aggregated per step (fp32 bytes, 0 at world 1)."""
         self.phases.arm()
         self._step_eager()
-        out = self.phases.finish()
-        out["exchange_bytes"] = 4 * N_PARAMS if (self.allreduce is not None or self.xgmi is not None) else 0
-        return out
+        pending = self.phases.finish()
+        pending.exchange_bytes = 4 * N_PARAMS if (self.allreduce is not None or self.xgmi is not None) else 0
+        return pending
 
     def drop_graphs(self) -> None:
         """Release every captured step graph after the device has finished with them.  A
@@ -581,7 +587,7 @@ class FusedMLPTrainer:
         n.call("sl_mlp_rows", n.ptr(x), n.ptr(y), None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
-               n.ptr(loss), n.ptr(corr), None, 0, n.ptr(self.r1p), n.stream_ptr())
+               n.ptr(loss), n.ptr(corr), None, 0, n.ptr(self.r1p), None, n.stream_ptr())
         lv = float("nan") if self.w1_out_of_range() else float(loss.mean())
         return StepStats(lv, float(corr.mean()), rows)
 
@@ -595,7 +601,7 @@ class FusedMLPTrainer:
         n.call("sl_mlp_rows", n.ptr(x), None, None, 1, rows,
                n.ptr(self.w1h), n.ptr(self.w2h), n.ptr(self.w3h), n.ptr(self.w2th), n.ptr(self.w3th),
                n.ptr(self.params), self.xa, self.xb, 1.0, 1.0, None, None, None, None,
-               None, None, n.ptr(out), 0, n.ptr(self.r1p), n.stream_ptr())
+               None, None, n.ptr(out), 0, n.ptr(self.r1p), None, n.stream_ptr())
         if self.w1_out_of_range():
             out.fill_(float("nan"))
         return out

@@ -306,13 +306,14 @@ class CPUResNetTrainer:
         self.phases.mark("update")
         self._last = (float(loss), float(correct))
 
-    def probe_step(self) -> dict:
-        """One training step with its phases timed (utils/phases.py; wall clock on the CPU)."""
+    def probe_step(self):
+        """One training step with its phases timed (utils/phases.py; wall clock on the CPU):
+        a PendingPhases, ready at once."""
         self.phases.arm()
         self.step()
-        out = self.phases.finish()
-        out["exchange_bytes"] = 4 * int(self.params.numel()) if self.allreduce is not None else 0
-        return out
+        pending = self.phases.finish()
+        pending.exchange_bytes = 4 * int(self.params.numel()) if self.allreduce is not None else 0
+        return pending
 
     def stats(self):
         from .mlp import StepStats
@@ -365,7 +366,7 @@ def block_backward_errors(tr, g: torch.Tensor) -> list:
     against fp32 autograd of that block run on the engine's OWN stored input, bf16 weights and
     incoming gradient.  Returns [(conv name, "dx" | "dW", relative L2 error)].  Used by the GPU
     numerics tests at B = 32 (tests/test_cnn_gpu.py) and at the bench batch
-    (profiles/r05_passes/probes/resnet_block_check.py)."""
+    (scripts/resnet_block_check.py)."""
     spec = tr.spec
     w32 = tr.shadow.float()
     f32 = lambda t: t.float().permute(0, 3, 1, 2).detach()  # noqa: E731

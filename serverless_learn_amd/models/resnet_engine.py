@@ -432,14 +432,15 @@ class FusedResNetTrainer:
             return
         self._step_eager()
 
-    def probe_step(self) -> dict:
-        """One eager training step with its phases timed (utils/phases.py)."""
+    def probe_step(self):
+        """One eager training step with its phase boundaries recorded (utils/phases.py): returns
+        a PendingPhases, resolved by the caller once the device has finished the step."""
         self.phases.arm()
         self._step_eager()
-        out = self.phases.finish()
+        pending = self.phases.finish()
         hooked = self.allreduce is not None or self.bucket_hook is not None
-        out["exchange_bytes"] = 4 * int(self.grad.numel()) if hooked else 0
-        return out
+        pending.exchange_bytes = 4 * int(self.grad.numel()) if hooked else 0
+        return pending
 
     def drop_graphs(self) -> None:
         """Release the captured step graph once the device is done with it (called by the

@@ -31,7 +31,7 @@ F = ctypes.c_float
 _SIGS: dict[str, list] = {
     "sl_mlp_param_count": [],
     "sl_mlp_slab_stride": [],
-    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P, P],
+    "sl_mlp_rows": [P, P, P, I, I, P, P, P, P, P, P, F, F, F, F, P, P, P, P, P, P, P, I, P, P, P],
     "sl_mlp_wgrad": [I, P, P, I, P, P, P, P, I, P, I, L, P],
     "sl_mlp_wgrad_slices": [I, I],
     "sl_mlp_set_rows_bm": [I],
@@ -43,8 +43,8 @@ _SIGS: dict[str, list] = {
     "sl_mlp_set_sgd_stamps": [P],
     "sl_mlp_sgd_wgs": [],
     "sl_mlp_sgd": [P, P, P, I, L, P, P, F, F, F, F, F, I, P, P, P, P, P, P, P, P],
-    "sl_mlp_reduce_xgmi": [P, I, L, F, F, P, P, P, P],
-    "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, L, P, P],
+    "sl_mlp_reduce_xgmi": [P, I, L, F, F, P, P, P, P, L, I, I, L, I, P],
+    "sl_mlp_sgd_xgmi": [P, P, F, F, F, P, P, P, P, P, P, P, P, L, I, I, L, P, I, P],
     "sl_clock_probe": [P, P, I, P],
     "sl_comm_proxy": [P, P, L, I, P],
 }

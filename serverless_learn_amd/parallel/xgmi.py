@@ -8,6 +8,14 @@ protocol and memory-ordering argument in ``csrc/kernels/xgmi.h``.  The exchange
 needs no host synchronisation, so the whole multi-GPU step (forward, backward,
 all-reduce, optimizer) is captured in one hipGraph like the 1-GPU step.
 
+Synchronisation is inline (``SL_XGMI_BARRIER=1`` restores the one-wave barrier kernel): the
+consumer kernel's workgroup 0 signals every peer in its prologue (the producer before it has
+completed) and all its workgroups wait for the peers' signals there; the step id advances once
+per step in the MLP rows kernel -- no barrier launch and no last-workgroup fan-in per step
+(``profiles/r06_xchg``).  Whether ranks share a GPU (the rehearsals)
+is detected at setup from the devices' PCI addresses; the consumer grid is then bounded so a
+waiting rank never holds every CU its peer needs.
+
 ``two_shot=True`` switches to reduce-scatter + all-gather through the same buffers: each
 rank sums only its 1/W chunk of the W payloads, and consumers read every chunk from its
 owner -- 2(W-1)/W of a payload crosses each GPU's links instead of W-1 payloads, for one
@@ -43,7 +51,7 @@ N.register("sl_ipc_close", [N.P])
 N.register("sl_xgmi_buffer_bytes", [N.L], restype=ctypes.c_long)
 N.register("sl_xgmi_copyin", [N.P, N.P, N.L, N.I, N.I, N.L, N.P, N.L, N.P])
 N.register("sl_xgmi_barrier", [N.P, N.P, N.L, N.I, N.I, N.L, N.I, N.P])
-N.register("sl_xgmi_rs", [N.P, N.P, N.L, N.I, N.I, N.L, N.L, N.P])
+N.register("sl_xgmi_rs", [N.P, N.P, N.L, N.I, N.I, N.L, N.L, N.I, N.P])
 N.register("sl_xgmi_sum", [N.P, N.P, N.L, N.I, N.I, N.L, N.P, N.L, N.F, N.P])
 N.register("sl_xgmi_peek", [N.P, N.P, N.L, N.I, N.I, N.L, N.I, N.I, N.I, N.P, N.L, N.P])
 
@@ -60,6 +68,17 @@ def two_shot_chunk4(slot_bytes: int, world: int) -> int:
     each is whole waves (64 float4), so a consumer wave reads from one owner's buffer."""
     per_rank = -(-(slot_bytes // 16) // world)
     return -(-per_rank // 64) * 64
+
+
+def inline_sync_enabled() -> bool:
+    """``SL_XGMI_BARRIER=1``: step barrier as its own one-wave kernel (the round-5 protocol)."""
+    return os.environ.get("SL_XGMI_BARRIER", "0") != "1"
+
+
+def device_key(device) -> bytes:
+    """PCI address of the GPU (ranks that share one map to the same key)."""
+    p = torch.cuda.get_device_properties(torch.device(device))
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}".encode()
 
 
 def default_two_shot(world: int) -> bool:
@@ -92,6 +111,10 @@ class XgmiExchange:
         self.hdr = int(lib.sl_xgmi_header_bytes())
         self.chunk4 = two_shot_chunk4(self.slot_bytes, world)
         self.two_shot = bool(two_shot)
+        # ranks sharing a GPU (rehearsals): bounded consumer grids under inline synchronisation
+        keys = allgather(device_key(device).ljust(int(lib.sl_ipc_handle_size()), b"\0"))  # handle-sized record
+        self.shared_gpu = len(set(keys)) < len(keys)
+        self.inline_sync = (2 if self.shared_gpu else 1) if inline_sync_enabled() else 0
         self._own = ctypes.c_void_p()
         self._opened: list[int] = []
         self.table = None
@@ -127,6 +150,8 @@ class XgmiExchange:
                 self.close(sync=False)
                 raise RuntimeError("xgmi exchange unavailable: " + (err or "a peer failed to map its buffers"))
             self.table = torch.tensor(bases, dtype=torch.int64, device=device)
+            # [0] completed steps (barrier mode) / step in flight (inline mode: advanced by the
+            # MLP rows kernel), [1] finished-block counter, [2] error
             self.ctl = torch.zeros(4, dtype=torch.int32, device=device)
 
     # ---- pointers --------------------------------------------------------------
@@ -143,11 +168,16 @@ class XgmiExchange:
         return (self.table.data_ptr(), self.ctl.data_ptr(), self.slot_bytes, self.rank, self.world,
                 self.chunk4 if self.two_shot else 0)
 
-    def exchange_launches(self, n: int) -> list:
-        """Launch specs run between "payload written" and "consumer": [(fn, extra args)]."""
+    def exchange_launches(self, n: int, inline: bool | None = None) -> list:
+        """Launch specs run between "payload written" and "consumer": [(fn, extra args)].
+        Inline synchronisation (the producer published the step): nothing for one-shot, the
+        reduce-scatter (which waits and publishes by itself) for two-shot."""
+        inl = self.inline_sync if inline is None else (self.inline_sync if inline else 0)
+        if inl:
+            return [("sl_xgmi_rs", (n, inl))] if self.two_shot else []
         if not self.two_shot:
             return [("sl_xgmi_barrier", (0,))]
-        return [("sl_xgmi_barrier", (0,)), ("sl_xgmi_rs", (n,)), ("sl_xgmi_barrier", (1,))]
+        return [("sl_xgmi_barrier", (0,)), ("sl_xgmi_rs", (n, 0)), ("sl_xgmi_barrier", (1,))]
 
     # ---- generic all-reduce ----------------------------------------------------
     def allreduce_(self, t: torch.Tensor, scale: float = 1.0) -> None:
@@ -158,7 +188,7 @@ class XgmiExchange:
             raise ValueError("tensor larger than the exchange slot")
         s = N.stream_ptr()
         N.call("sl_xgmi_copyin", *self.args(), t.data_ptr(), t.numel(), s)
-        for fn, extra in self.exchange_launches(t.numel()):
+        for fn, extra in self.exchange_launches(t.numel(), inline=False):  # copyin does not publish
             N.call(fn, *self.args(), *extra, s)
         N.call("sl_xgmi_sum", *self.args(), t.data_ptr(), t.numel(), float(scale), s)
 

@@ -107,6 +107,7 @@ class Worker:
                                              "exchange_gbps")}
         self._wait_s = 0.0
         self._probe_due = True
+        self._pending_phases = None
         self.hold_at = None       # pause training exactly at this step (bench.py --runtime, tests)
         self.held_step = -1       # step the worker is paused at, once its device work has drained
         self._agreed_epoch = -1   # newest membership epoch the whole lock-step group has agreed to see
@@ -627,12 +628,12 @@ class Worker:
         done = 0
         try:
             if self._probe_due and hasattr(t, "probe_step"):
-                # once per log interval: the chunk's first step runs eagerly with its phases timed
+                # once per log interval: the chunk's first step runs eagerly with its phase
+                # boundaries recorded; resolved later, outside the lock (_poll_phases)
                 self._probe_due = False
                 with self.train_lock:
-                    p = t.probe_step()
+                    self._pending_phases = t.probe_step()
                 done = 1
-                self._record_phases(p)
             if not self._use_graph():
                 while done < n:
                     with self.train_lock:
@@ -770,6 +771,7 @@ class Worker:
                 self.log.warn("collective_failed", error=str(e.cause), epoch=self.group.epoch, steps_done=e.done)
                 continue
             self._account_steps(prev, ran)
+            self._poll_phases()
             self.state = "training"
             lockstep = self.cfg.sync == "allreduce" and self.group.active and self.group.world > 1
             agreement = None
@@ -845,6 +847,14 @@ class Worker:
         t0 = time.perf_counter()
         (event or self._stop).wait(secs)
         self._wait_s += time.perf_counter() - t0
+
+    def _poll_phases(self) -> None:
+        """Resolve the probed step once the device has finished it (a non-blocking event query:
+        never a wait -- with a dead peer the step may stall until the exchange times out)."""
+        pend = self._pending_phases
+        if pend is not None and pend.ready():
+            self._pending_phases = None
+            self._record_phases(pend.result())
 
     def _record_phases(self, p: dict) -> None:
         """One probed step's phases (utils/phases.py) -> phase_stats / FlowFeedback."""

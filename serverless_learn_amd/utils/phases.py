@@ -6,7 +6,10 @@ messages are reserved and empty (/root/reference/src/protos/serverless_learn.pro
 
 A :class:`PhaseProbe` records device events at the phase boundaries of ONE eager training step
 when armed (the runtime arms it once per log interval; captured graph replays are never
-probed, so the hot path pays nothing).  Engines call :meth:`mark` at the END of each phase:
+probed, so the hot path pays nothing).  Nothing here waits for the device: the probed step
+hands back a :class:`PendingPhases` that the runtime resolves once the step has finished
+(``ready()`` is a non-blocking event query) -- a wait inside the training lock would stall the
+RPC handlers that need that lock for as long as the step runs.  Engines call :meth:`mark` at the END of each phase:
 
 * ``compute``  -- forward + backward (plus the optimizer when it is fused into the backward's
   last launch: the world-1 MLP step);
@@ -47,12 +50,30 @@ class PhaseProbe:
         else:
             self._marks.append((name, time.perf_counter()))
 
-    def finish(self) -> dict:
-        """Disarm and return {phase: ms} for the phases marked since :meth:`arm` (missing
-        phases are 0; a phase marked twice accumulates)."""
+    def finish(self) -> "PendingPhases":
+        """Disarm and hand back the marks recorded since :meth:`arm`, unresolved: the device
+        may still be running the step (never synchronise here -- callers hold locks)."""
         self.armed = False
         marks, self._marks = self._marks, []
-        out = {p: 0.0 for p in self.PHASES}
+        return PendingPhases(marks, self.cuda)
+
+
+class PendingPhases:
+    """The marks of one probed step; :meth:`ready` / :meth:`result` once the device is done."""
+
+    def __init__(self, marks: list, cuda: bool, exchange_bytes: int = 0):
+        self.marks, self.cuda, self.exchange_bytes = marks, cuda, exchange_bytes
+
+    def ready(self) -> bool:
+        """Non-blocking: has the probed step's last phase finished on the device?"""
+        return not (self.cuda and self.marks) or self.marks[-1][1].query()
+
+    def result(self) -> dict:
+        """{phase: ms} (missing phases 0; a phase marked twice accumulates) and the gradient
+        bytes the step exchanged; waits for the device if the step is still running."""
+        out = {p: 0.0 for p in PhaseProbe.PHASES}
+        out["exchange_bytes"] = self.exchange_bytes
+        marks = self.marks
         if len(marks) < 2:
             return out
         if self.cuda:

@@ -609,6 +609,51 @@ def test_resnet_block_backward_at_bench_batch_deterministic_build(batch):
     assert not bad, (bad, r["worst"])
 
 
+@pytest.mark.parametrize("batch", [1024])
+def test_resnet_block_backward_at_bench_batch_shipped_build(batch):
+    """the per-block fp32 check at the bench batch in the SHIPPED build (split-K
+    atomics and order-nondeterministic cross-workgroup sums), with the deterministic build's 0.06
+    bound -- every block's backward on its own stored input and incoming gradient."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "SL_DETERMINISTIC"}
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "resnet_block_check.py"), str(batch)],
+                         env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert not r["deterministic_build"] and r["batch"] == batch, r
+    bad = [e for e in r["errors"] if e[2] > 0.06]
+    assert not bad, (bad, r["worst"])
+
+
+def test_resnet_engine_grads_at_b256_within_run_to_run_noise():
+    """the whole engine at B = 256 (large tiles, split-K, parity classes) in the
+    shipped build against fp32 autograd, per layer, with the bound set by the build's own
+    run-to-run noise: two engine runs of the same batch differ by one-ulp bf16 flips that a BN net
+    at init amplifies, so each layer's distance from fp32 (1 - cosine) may be at most 4x its
+    distance between those two runs.  Measured (profiles/r06_numerics): fp32 cosines 0.928-0.999,
+    run-to-run 0.970-0.999, worst ratio 3.5."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "SL_DETERMINISTIC"}
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "resnet_engine_check.py"), "256"],
+                         env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert abs(r["loss"] - r["loss_ref"]) / r["loss_ref"] < 0.02, r
+    assert r["fc_cos"] > 0.995, r
+    bad = [ly for ly in r["layers"] if 1 - ly[1] > max(4 * (1 - ly[2]), 0.02) or ly[1] < 0.88]
+    assert not bad, (bad, r["worst_ref"], r["worst_noise"])
+
+
 def test_resnet_engine_trains_and_graph_replays():
     from serverless_learn_amd.data.synthetic import make_cifar_like
     from serverless_learn_amd.models.resnet_engine import FusedResNetTrainer
