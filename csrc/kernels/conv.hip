@@ -222,6 +222,12 @@ __device__ __forceinline__ short8_t ds_b128(uint32_t a) {
   return r;
 }
 template <int OFF>
+__device__ __forceinline__ short8_t ds_b128o(uint32_t a) {
+  short8_t r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+template <int OFF>
 __device__ __forceinline__ short4_t ds_tr16(uint32_t a) {
   short4_t r;
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
@@ -511,6 +517,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #ifndef SL_GEMM_BIG
 #define SL_GEMM_BIG 1  // use conv_gemm_big_kernel where it applies
 #endif
+#ifndef SL_GEMM_LEAN
+#define SL_GEMM_LEAN 1  // big-GEMM k-loop: buffer-resource DMA + tap masks, LDS-read offsets (see there)
+#endif
 #ifndef SL_EPI_SPLIT
 #define SL_EPI_SPLIT 1  // big-GEMM epilogue: compute all chunks, then store (see there)
 #endif
@@ -575,22 +584,61 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
     boffs[j] = col * g.wld + swz64(lane & 7, row) * 8;
   }
   const int cps_shift = g.c_shift - 6;  // log2(stages per tap)
-  auto issue = [&](int kt) {
-    uint16_t* As = smem + (kt % NSLOT) * SLOT;
-    uint16_t* Bs = As + BM * BK;
-    const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
-    int dh, dw, kb;
+  // workgroup-uniform gather shift (dh, dw) of a tap
+  auto tap_shift = [&](int tap, int& dh, int& dw) {
     if (phase) {
       dh = g.dh[tap0 + tap];
       dw = g.dw[tap0 + tap];
-      kb = g.tapw[tap0 + tap] * g.SC + ch0;
     } else {
       const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
       dh = TRANSPOSED ? -kh : kh;
       dw = TRANSPOSED ? -kw : kw;
-      kb = kt * BK;
     }
+  };
+#if SL_GEMM_LEAN
+  // Buffer-resource DMA: a padding piece gets an out-of-range offset and lands as zeros, and
+  // each piece's in-image test for every tap is one bit of a per-lane mask computed here once,
+  // so a piece costs an add, a bit test and a select per stage (was ~10 VALU with 64-bit
+  // addresses and the zero-page select).  The host keeps both operands under 2 GB (plan_gemm).
+  const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(g.src), 0,
+                                                      (int)((long)g.N * g.SH * g.SW * g.SC * 2), 0x00020000);
+  const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(e.w), 0, (int)((long)e.ncols * g.wld * 2),
+                                                      0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  unsigned tmask[PA] = {};
+#pragma unroll 1
+  for (int tap = 0; tap < (gK / BK) >> cps_shift; ++tap) {
+    int dh, dw;
+    tap_shift(tap, dh, dw);
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const bool v = rok[j] && (unsigned)(rih[j] + dh) < (unsigned)g.SH && (unsigned)(riw[j] + dw) < (unsigned)g.SW;
+      tmask[j] |= (unsigned)v << tap;
+    }
+  }
+  unsigned bbyte[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) bbyte[j] = bok[j] ? (unsigned)boffs[j] * 2u : OOB;  // + kb * 2 < 2 GB stays out
+#endif
+  auto issue = [&](int kt) {
+    uint16_t* As = smem + (kt % NSLOT) * SLOT;
+    uint16_t* Bs = As + BM * BK;
+    const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
+    int dh, dw;
+    tap_shift(tap, dh, dw);
+    const int kb = phase ? g.tapw[tap0 + tap] * g.SC + ch0 : kt * BK;
     const int soff = (dh * g.SW + dw) * g.SC + ch0;  // workgroup-uniform
+#if SL_GEMM_LEAN
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const unsigned off = (tmask[j] >> tap) & 1u ? (unsigned)(rbase[j] + soff) * 2u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a, (SL_LDS void*)(As + (wave * PA + j) * 8 * BK), 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_b, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK), 16,
+                                               bbyte[j] + (unsigned)kb * 2u, 0, 0, 0);
+#else
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const bool v = rok[j] && (unsigned)(rih[j] + dh) < (unsigned)g.SH && (unsigned)(riw[j] + dw) < (unsigned)g.SW;
@@ -599,6 +647,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 #pragma unroll
     for (int j = 0; j < PB; ++j)
       glds16(bok[j] ? e.w + (boffs[j] + kb) : g_conv_zero, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK));
+#endif
   };
 
   uint32_t aoff[MT][2], boff[NT][2];
@@ -634,10 +683,25 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
     short8_t af[2][MT], bf[2][NT];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+#if SL_GEMM_LEAN
+      // fragment i / j sits i * 16 rows past fragment 0 with the same swizzle (swz64 reads row
+      // bits 1-3): one base per operand and half, the rest as instruction offsets
+      static_assert(MT == 4 && NT == 4, "offset list");
+      const uint32_t a = sb + aoff[0][h], b = sb + boff[0][h];
+      af[h][0] = ds_b128o<0>(a);
+      af[h][1] = ds_b128o<16 * BK * 2>(a);
+      af[h][2] = ds_b128o<32 * BK * 2>(a);
+      af[h][3] = ds_b128o<48 * BK * 2>(a);
+      bf[h][0] = ds_b128o<0>(b);
+      bf[h][1] = ds_b128o<16 * BK * 2>(b);
+      bf[h][2] = ds_b128o<32 * BK * 2>(b);
+      bf[h][3] = ds_b128o<48 * BK * 2>(b);
+#else
 #pragma unroll
       for (int i = 0; i < MT; ++i) af[h][i] = ds_b128(sb + aoff[i][h]);
 #pragma unroll
       for (int j = 0; j < NT; ++j) bf[h][j] = ds_b128(sb + boff[j][h]);
+#endif
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1355,6 +1419,11 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
 #ifndef SL_WGRAD_BIG
 #define SL_WGRAD_BIG 1
 #endif
+// LEAN (host: SL_GEMM_LEAN, OH*OW divides 64, M % 64 == 0, operands under 1 GB): a 64-pixel
+// stage is whole images (or a whole image's part at a fixed offset), so every DMA piece's source
+// is a per-lane constant plus a workgroup-uniform stage offset -- buffer-resource DMA, padding
+// pieces at an out-of-range offset (zeros), no per-stage pixel decode or bounds test.
+template <bool LEAN>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
   younger_half_prio();
   constexpr int BMO = 256, BNO = 128, NSLOT = 3, WGM = 64;
@@ -1392,6 +1461,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
     abase[j] = a.dy + (long)(mbeg + arow[j]) * a.ldy + co;
   }
   // B (im2col) pieces: the lane's k chunk (tap, channels) is fixed for the workgroup
+  const unsigned bimg0 = LEAN ? (unsigned)(mbeg >> g.hw_shift << a.img_shift) * 2u : 0u;
   int brow[PB], bkh[PB], bkw[PB], bch[PB];
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
@@ -1402,10 +1472,40 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
     bkw[j] = tap - bkh[j] * g.KW;
     bch[j] = kk & (g.SC - 1);
   }
+  constexpr unsigned OOB = 0x80000000u;
+  unsigned abyte[PA], bbyte[PB];
+  const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.dy), 0, (int)((long)g.M * a.ldy * 2), 0x00020000);
+  const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(g.src), 0,
+                                                      (int)((long)g.N * g.SH * g.SW * g.SC * 2), 0x00020000);
+  if constexpr (LEAN) {
+#pragma unroll
+    for (int j = 0; j < PA; ++j) abyte[j] = (unsigned)((abase[j] - a.dy) * 2);
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {  // row brow[j] of every stage: image brow >> hw_shift of the stage, same pixel
+      const int nl = brow[j] >> g.hw_shift, r = brow[j] & ((1 << g.hw_shift) - 1);
+      const int oh = r >> g.w_shift, ow = r & ((1 << g.w_shift) - 1);
+      const int ih = (oh << g.s_shift) - g.pad + bkh[j], iw = (ow << g.s_shift) - g.pad + bkw[j];
+      const bool ok = (unsigned)ih < (unsigned)g.SH && (unsigned)iw < (unsigned)g.SW;
+      bbyte[j] = ok ? (unsigned)((nl << a.img_shift) + (((ih << a.sw_shift) + iw) << g.c_shift) + bch[j]) * 2u : OOB;
+    }
+  }
   auto issue = [&](int st) {
     uint16_t* Ai = smem + (st % NSLOT) * SLOT;
     uint16_t* Bi = Ai + IMG_A;
     const int mb = mbeg + st * WGM;
+    if constexpr (LEAN) {
+      const unsigned astep = (unsigned)(st * WGM * a.ldy) * 2u;       // < 1 GB (host)
+      const unsigned bstep = (unsigned)((mb - mbeg) >> g.hw_shift << a.img_shift) * 2u;
+#pragma unroll
+      for (int j = 0; j < PA; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a, (SL_LDS void*)(Ai + (wave * PA + j) * RA * BMO), 16, abyte[j] + astep,
+                                                 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < PB; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_b, (SL_LDS void*)(Bi + (wave * PB + j) * RB * BNO), 16,
+                                                 bbyte[j] + bstep + bimg0, 0, 0, 0);
+      return;
+    }
     const long astep = (long)st * WGM * a.ldy;
 #pragma unroll
     for (int j = 0; j < PA; ++j)
@@ -1598,7 +1698,8 @@ static GemmPlan plan_gemm(const ConvGeom& g, const ConvEpi& e, int mult = 1) {
   // tiles for every CU; transposed gathers only in phase mode or at stride 1
   const long big_tiles = (long)((g.M + 255) / 256) * (e.ncols / 128);
   if (gemm_big_enabled() && (g.SC & 63) == 0 && (g.K & 63) == 0 && (e.ncols & 127) == 0 && big_tiles * mult >= 256 &&
-      (!T || g.ph >= 0 || g.stride == 1) && (g.wld & 7) == 0 && (!e.y || (e.ldy & 7) == 0)) {
+      (!T || g.ph >= 0 || g.stride == 1) && (g.wld & 7) == 0 && (!e.y || (e.ldy & 7) == 0) &&
+      (!SL_GEMM_LEAN || ((long)g.N * g.SH * g.SW * g.SC < (1L << 30) && (long)e.ncols * g.wld < (1L << 30)))) {
     p.big = 1; p.BM = 256; p.BN = 128; p.tiles_n = e.ncols / 128; p.grid = big_tiles;
     return p;
   }
@@ -2040,7 +2141,10 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
     const bool slab = wgrad_use_slab(a, ws, ws_floats);
     if (SL_DETERMINISTIC && a.slices > 1 && !slab) return SL_NEED_WS;  // no order-dependent atomics
     if (slab) sl_wgrad_slab_acquire(ws, stream);
-    hipLaunchKernelGGL(conv_wgrad_big_kernel, dim3(tiles * a.slices), dim3(512), 0, stream, a);
+    const bool lean = SL_GEMM_LEAN && a.g.hw_shift <= 6 && (a.g.M & 63) == 0 &&
+                      (long)a.g.M * ldy < (1L << 29) && (long)N * H * W * C < (1L << 29);
+    if (lean) hipLaunchKernelGGL(conv_wgrad_big_kernel<true>, dim3(tiles * a.slices), dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL(conv_wgrad_big_kernel<false>, dim3(tiles * a.slices), dim3(512), 0, stream, a);
     SL_CHECK_LAUNCH();
     return wgrad_finish(a, ws, ws_floats, stream, slab);
   }

@@ -36,6 +36,7 @@ CONV_CASES = [
     (1024, 16, 128, 256, 3, 2, 1),  # forward + phase-mode dgrad (parity classes of 65,536 rows)
     (256, 8, 256, 512, 3, 1, 1),    # stage-4 shape forward; large-tile weight gradient (cout 512)
     (64, 16, 128, 256, 3, 1, 1),    # large-tile weight gradient, cout 256, K 1152
+    (64, 16, 128, 256, 1, 2, 0),    # stage-3 1x1 / stride-2 shortcut: large-tile wgrad, buffer-DMA form
     (1024, 32, 64, 128, 3, 2, 1),   # ResNet-18 stage 2 at B = 1024: phase-mode dgrad into 64 channels
     (1024, 32, 64, 128, 1, 2, 0),   # ... and its 1x1 / stride-2 shortcut
 ]
