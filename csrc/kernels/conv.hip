@@ -206,6 +206,11 @@ __device__ __forceinline__ void glds16(const void* src, SL_LDS void* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, dst, 16, 0, 0);
 }
 
+// 16 B per lane into LDS through a buffer resource: an offset past the resource's size loads
+// zeros (the SL_GEMM_LEAN forms' padding).  A plain function so template kernels can call it.
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rs, SL_LDS void* dst, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, off, 0, 0, 0);
+}
 template <int N>
 __device__ __forceinline__ void vmcnt_stages(int stages_after) {
   // this wave's DMA pieces of the stage about to be read have landed once at
@@ -632,12 +637,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const unsigned off = (tmask[j] >> tap) & 1u ? (unsigned)(rbase[j] + soff) * 2u : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a, (SL_LDS void*)(As + (wave * PA + j) * 8 * BK), 16, off, 0, 0, 0);
+      blds16(rs_a, (SL_LDS void*)(As + (wave * PA + j) * 8 * BK), off);
     }
 #pragma unroll
     for (int j = 0; j < PB; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_b, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK), 16,
-                                               bbyte[j] + (unsigned)kb * 2u, 0, 0, 0);
+      blds16(rs_b, (SL_LDS void*)(Bs + (wave * PB + j) * 8 * BK), bbyte[j] + (unsigned)kb * 2u);
 #else
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
@@ -1169,6 +1173,37 @@ struct WgradArgs {
   float* ws;
 };
 
+// Lean weight-gradient DMA (SL_GEMM_LEAN; host: wgrad_lean_ok).  With OH*OW and OW powers of
+// two, OW dividing the WGM-row stage and M % WGM == 0, a stage is whole images (OH*OW <= WGM) or
+// whole output rows of one image, so a lane's pixel inside the stage never changes: only the
+// image and the output-row base move, as workgroup-uniform scalars.  A piece then costs an add,
+// a row test and a select per stage, through a buffer resource whose out-of-range offsets load
+// zeros (the padding), instead of a pixel decode, three bounds tests and a 64-bit address.
+constexpr unsigned WG_OOB = 0x80000000u;
+struct WgLeanB {
+  unsigned cst;  // byte offset at stage base 0 (modular: only used when the row is in range)
+  int ihl;       // input row at stage output-row base 0; -2^20 when the column / k is out of range
+  __device__ __forceinline__ void init(const WgradArgs& a, int lw, int brow, int kh, int kw, int ch) {
+    const ConvGeom& g = a.g;
+    const bool whole = g.hw_shift <= lw;  // stage = whole images
+    const int nl = whole ? brow >> g.hw_shift : 0, r = whole ? brow & ((1 << g.hw_shift) - 1) : brow;
+    const int oh = r >> g.w_shift, ow = r & ((1 << g.w_shift) - 1);
+    const int iw = (ow << g.s_shift) - g.pad + kw;
+    ihl = (unsigned)iw < (unsigned)g.SW ? (oh << g.s_shift) - g.pad + kh : -(1 << 20);
+    cst = (((unsigned)nl << a.img_shift) + ((((unsigned)ihl << a.sw_shift) + (unsigned)iw) << g.c_shift) + (unsigned)ch) * 2u;
+  }
+  __device__ __forceinline__ unsigned off(const ConvGeom& g, int ihs, unsigned scal) const {
+    return (unsigned)(ihl + ihs) < (unsigned)g.SH ? cst + scal : WG_OOB;
+  }
+};
+// workgroup-uniform part of a stage starting at row mb: input-row shift and byte offset
+__device__ __forceinline__ void wg_lean_stage(const WgradArgs& a, int mb, int& ihs, unsigned& scal) {
+  const ConvGeom& g = a.g;
+  const int n = mb >> g.hw_shift, ohb = (mb & ((1 << g.hw_shift) - 1)) >> g.w_shift;
+  ihs = ohb << g.s_shift;
+  scal = (((unsigned)n << a.img_shift) + (((unsigned)ihs << a.sw_shift) << g.c_shift)) * 2u;
+}
+
 __device__ __forceinline__ void wgrad_out(const WgradArgs& a, int s, int co, int k, float v) {
   if (a.ws) a.ws[((long)s * a.cout + co) * a.g.K + k] = v;
   else if (a.slices > 1) atomicAdd(a.dw + (long)co * a.g.K + k, v);
@@ -1240,7 +1275,7 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float4* __
 
 // KS = 2: 8 waves, waves 4-7 take the second 32 pixels of every 64-pixel stage
 // (two waves per SIMD inside one workgroup); the k-halves are summed through LDS.
-template <int BMO, int NSLOT, int KS, int WGM = WG_M>
+template <int BMO, int NSLOT, int KS, int WGM = WG_M, bool LEAN = false>
 __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
   constexpr int BNO = 128;
   constexpr int WA = BMO / 8, WB = BNO / 8;       // 16-B chunks per image row
@@ -1297,10 +1332,34 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
   const uint16_t* abase[PA];
 #pragma unroll
   for (int j = 0; j < PA; ++j) abase[j] = acol[j] ? acol[j] + (long)(mbeg + arow[j]) * a.ldy : nullptr;
+  const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.dy), 0, (int)((long)g.M * a.ldy * 2), 0x00020000);
+  const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(g.src), 0,
+                                                      (int)((long)g.N * g.SH * g.SW * g.SC * 2), 0x00020000);
+  unsigned abyte[PA];
+  WgLeanB lb[PB];
+  if constexpr (LEAN) {
+#pragma unroll
+    for (int j = 0; j < PA; ++j) abyte[j] = abase[j] ? (unsigned)((abase[j] - a.dy) * 2) : WG_OOB;
+#pragma unroll
+    for (int j = 0; j < PB; ++j) lb[j].init(a, WGM == 64 ? 6 : WGM == 32 ? 5 : 4, brow[j], bkh[j], bkw[j], bch[j]);
+  }
   auto issue = [&](int st) {
     uint16_t* Ai = smem + (st % NSLOT) * SLOT;
     uint16_t* Bi = Ai + IMG_A;
     const int mb = mbeg + st * WGM;
+    if constexpr (LEAN) {
+      const unsigned astep = (unsigned)(st * WGM * a.ldy) * 2u;
+      int ihs;
+      unsigned scal;
+      wg_lean_stage(a, mb, ihs, scal);
+#pragma unroll
+      for (int j = 0; j < PA; ++j)
+        blds16(rs_a, (SL_LDS void*)(Ai + (wave * PA + j) * RA * BMO), abyte[j] + astep);
+#pragma unroll
+      for (int j = 0; j < PB; ++j)
+        blds16(rs_b, (SL_LDS void*)(Bi + (wave * PB + j) * RB * BNO), lb[j].off(g, ihs, scal));
+      return;
+    }
     if (shift_path) {
       const long astep = (long)st * WGM * a.ldy;
 #pragma unroll
@@ -1419,10 +1478,7 @@ __global__ __launch_bounds__(256 * KS, KS == 1 ? 2 : 1) void conv_wgrad_kernel(W
 #ifndef SL_WGRAD_BIG
 #define SL_WGRAD_BIG 1
 #endif
-// LEAN (host: SL_GEMM_LEAN, OH*OW divides 64, M % 64 == 0, operands under 1 GB): a 64-pixel
-// stage is whole images (or a whole image's part at a fixed offset), so every DMA piece's source
-// is a per-lane constant plus a workgroup-uniform stage offset -- buffer-resource DMA, padding
-// pieces at an out-of-range offset (zeros), no per-stage pixel decode or bounds test.
+// LEAN: buffer-resource DMA with lane-constant sources (WgLeanB; host: wgrad_lean_ok)
 template <bool LEAN>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
   younger_half_prio();
@@ -1461,7 +1517,6 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
     abase[j] = a.dy + (long)(mbeg + arow[j]) * a.ldy + co;
   }
   // B (im2col) pieces: the lane's k chunk (tap, channels) is fixed for the workgroup
-  const unsigned bimg0 = LEAN ? (unsigned)(mbeg >> g.hw_shift << a.img_shift) * 2u : 0u;
   int brow[PB], bkh[PB], bkw[PB], bch[PB];
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
@@ -1472,38 +1527,32 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_big_kernel(WgradArgs a) {
     bkw[j] = tap - bkh[j] * g.KW;
     bch[j] = kk & (g.SC - 1);
   }
-  constexpr unsigned OOB = 0x80000000u;
-  unsigned abyte[PA], bbyte[PB];
+  unsigned abyte[PA];
+  WgLeanB lb[PB];
   const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.dy), 0, (int)((long)g.M * a.ldy * 2), 0x00020000);
   const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(g.src), 0,
                                                       (int)((long)g.N * g.SH * g.SW * g.SC * 2), 0x00020000);
-  if constexpr (LEAN) {
+  if constexpr (LEAN) {  // (conv_wgrad_kernel's LEAN form)
 #pragma unroll
     for (int j = 0; j < PA; ++j) abyte[j] = (unsigned)((abase[j] - a.dy) * 2);
 #pragma unroll
-    for (int j = 0; j < PB; ++j) {  // row brow[j] of every stage: image brow >> hw_shift of the stage, same pixel
-      const int nl = brow[j] >> g.hw_shift, r = brow[j] & ((1 << g.hw_shift) - 1);
-      const int oh = r >> g.w_shift, ow = r & ((1 << g.w_shift) - 1);
-      const int ih = (oh << g.s_shift) - g.pad + bkh[j], iw = (ow << g.s_shift) - g.pad + bkw[j];
-      const bool ok = (unsigned)ih < (unsigned)g.SH && (unsigned)iw < (unsigned)g.SW;
-      bbyte[j] = ok ? (unsigned)((nl << a.img_shift) + (((ih << a.sw_shift) + iw) << g.c_shift) + bch[j]) * 2u : OOB;
-    }
+    for (int j = 0; j < PB; ++j) lb[j].init(a, 6, brow[j], bkh[j], bkw[j], bch[j]);
   }
   auto issue = [&](int st) {
     uint16_t* Ai = smem + (st % NSLOT) * SLOT;
     uint16_t* Bi = Ai + IMG_A;
     const int mb = mbeg + st * WGM;
     if constexpr (LEAN) {
-      const unsigned astep = (unsigned)(st * WGM * a.ldy) * 2u;       // < 1 GB (host)
-      const unsigned bstep = (unsigned)((mb - mbeg) >> g.hw_shift << a.img_shift) * 2u;
+      const unsigned astep = (unsigned)(st * WGM * a.ldy) * 2u;
+      int ihs;
+      unsigned scal;
+      wg_lean_stage(a, mb, ihs, scal);
 #pragma unroll
       for (int j = 0; j < PA; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a, (SL_LDS void*)(Ai + (wave * PA + j) * RA * BMO), 16, abyte[j] + astep,
-                                                 0, 0, 0);
+        blds16(rs_a, (SL_LDS void*)(Ai + (wave * PA + j) * RA * BMO), abyte[j] + astep);
 #pragma unroll
       for (int j = 0; j < PB; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_b, (SL_LDS void*)(Bi + (wave * PB + j) * RB * BNO), 16,
-                                                 bbyte[j] + bstep + bimg0, 0, 0, 0);
+        blds16(rs_b, (SL_LDS void*)(Bi + (wave * PB + j) * RB * BNO), lb[j].off(g, ihs, scal));
       return;
     }
     const long astep = (long)st * WGM * a.ldy;
@@ -2107,6 +2156,16 @@ static bool wgrad_use_slab(WgradArgs& a, float* ws, long ws_floats) {
   return true;
 }
 
+// The lean DMA form's preconditions (WgLeanB): power-of-two shapes on the shift path, OW dividing
+// the stage, whole stages, operands under 1 GB so that an out-of-range offset plus a stage offset
+// stays out of range.
+static bool wgrad_lean_ok(const WgradArgs& a, int wgm, int ldy) {
+  const ConvGeom& g = a.g;
+  return SL_GEMM_LEAN && a.img_shift >= 0 && a.sw_shift >= 0 && g.hw_shift >= 0 && g.w_shift >= 0 &&
+         (1 << g.w_shift) <= wgm && (g.hw_shift <= ilog2(wgm) || (1 << g.hw_shift) % wgm == 0) && g.M % wgm == 0 &&
+         (long)g.M * ldy < (1L << 29) && (long)g.N * g.SH * g.SW * g.SC < (1L << 29);
+}
+
 int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t* dy, int ldy, int cout, int KH,
                   int KW, int stride, int pad, int OH, int OW, float* dw, int target_wgs, float* ws, long ws_floats,
                   hipStream_t stream) {
@@ -2141,9 +2200,7 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
     const bool slab = wgrad_use_slab(a, ws, ws_floats);
     if (SL_DETERMINISTIC && a.slices > 1 && !slab) return SL_NEED_WS;  // no order-dependent atomics
     if (slab) sl_wgrad_slab_acquire(ws, stream);
-    const bool lean = SL_GEMM_LEAN && a.g.hw_shift <= 6 && (a.g.M & 63) == 0 &&
-                      (long)a.g.M * ldy < (1L << 29) && (long)N * H * W * C < (1L << 29);
-    if (lean) hipLaunchKernelGGL(conv_wgrad_big_kernel<true>, dim3(tiles * a.slices), dim3(512), 0, stream, a);
+    if (wgrad_lean_ok(a, 64, ldy)) hipLaunchKernelGGL(conv_wgrad_big_kernel<true>, dim3(tiles * a.slices), dim3(512), 0, stream, a);
     else hipLaunchKernelGGL(conv_wgrad_big_kernel<false>, dim3(tiles * a.slices), dim3(512), 0, stream, a);
     SL_CHECK_LAUNCH();
     return wgrad_finish(a, ws, ws_floats, stream, slab);
@@ -2164,10 +2221,18 @@ int sl_conv_wgrad(const uint16_t* x, int N, int H, int W, int C, const uint16_t*
   const bool slab = wgrad_use_slab(a, ws, ws_floats);
   if (SL_DETERMINISTIC && a.slices > 1 && !slab) return SL_NEED_WS;
   if (slab) sl_wgrad_slab_acquire(ws, stream);
-  if (BMO == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3, 1>), grid, dim3(256), 0, stream, a);
-  else if (SL_WGRAD128_KS == 2)
-    hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_KS2_SLOTS, 2>), grid, dim3(512), 0, stream, a);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS, 1, SL_WGRAD128_WGM>), grid, dim3(256), 0, stream, a);
+  const bool lean = wgrad_lean_ok(a, wgm, ldy);
+  if (BMO == 64) {
+    if (lean) hipLaunchKernelGGL((conv_wgrad_kernel<64, 3, 1, WG_M, true>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<64, 3, 1>), grid, dim3(256), 0, stream, a);
+  } else if (SL_WGRAD128_KS == 2) {
+    if (lean) hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_KS2_SLOTS, 2, WG_M, true>), grid, dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_KS2_SLOTS, 2>), grid, dim3(512), 0, stream, a);
+  } else {
+    if (lean)
+      hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS, 1, SL_WGRAD128_WGM, true>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<128, SL_WGRAD128_SLOTS, 1, SL_WGRAD128_WGM>), grid, dim3(256), 0, stream, a);
+  }
   SL_CHECK_LAUNCH();
   return wgrad_finish(a, ws, ws_floats, stream, slab);
 }

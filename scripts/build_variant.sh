@@ -13,4 +13,7 @@ for f in csrc/kernels/*.hip; do
 done
 wait
 hipcc --offload-arch=gfx950 -shared -fPIC $objs -o $out/libslkernels_$tag.so
+if nm -D --undefined-only $out/libslkernels_$tag.so | grep -q __device_stub__; then
+  echo "undefined kernel launch stubs in $out/libslkernels_$tag.so" >&2; exit 1
+fi
 echo $out/libslkernels_$tag.so

@@ -99,8 +99,22 @@ def build_kernels(force: bool = False, jobs: int = 8, deterministic: bool = Fals
             raise RuntimeError("hipcc failed on " + src)
     tmp = so_path + ".tmp"
     _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", tmp])
+    _check_stubs(tmp)
     os.replace(tmp, so_path)
     return so_path
+
+
+def _check_stubs(so: str) -> None:
+    """Refuse a kernel library with an undefined launch stub.  A template kernel whose body
+    names a device-only builtin in a type-dependent expression fails host-side instantiation
+    silently: its launch stub is left undefined and the library only fails at dlopen, on the
+    GPU box (csrc/kernels/conv.hip `blds16` is the wrapper that avoids this)."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    proc = subprocess.run([nm, "-D", "--undefined-only", so], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                          text=True)
+    missing = [ln.split()[-1] for ln in proc.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        raise RuntimeError("undefined kernel launch stubs in %s: %s" % (so, ", ".join(missing)))
 
 
 def build_core(force: bool = False) -> str:
