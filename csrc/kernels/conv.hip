@@ -522,6 +522,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGeom g, ConvEpi e
 #ifndef SL_GEMM_BIG
 #define SL_GEMM_BIG 1  // use conv_gemm_big_kernel where it applies
 #endif
+#ifndef SL_GEMM_KO
+// timing knockouts of conv_gemm_big_kernel (results wrong; A/B builds only): 1 no DMA after
+// the two prologue stages, 2 every stage's DMA re-reads stage 0's bytes, 3 no epilogue, 4 = 1 + 3
+#define SL_GEMM_KO 0
+#endif
 #ifndef SL_GEMM_LEAN
 #define SL_GEMM_LEAN 1  // big-GEMM k-loop: buffer-resource DMA + tap masks, LDS-read offsets (see there)
 #endif
@@ -628,6 +633,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
   auto issue = [&](int kt) {
     uint16_t* As = smem + (kt % NSLOT) * SLOT;
     uint16_t* Bs = As + BM * BK;
+    if ((SL_GEMM_KO == 1 || SL_GEMM_KO == 4) && kt >= NSLOT - 1) return;  // knockout: no DMA after the prologue
+    if (SL_GEMM_KO == 2) kt = 0;                      // knockout: every stage re-reads stage 0 (L2-hot)
     const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * 64;
     int dh, dw;
     tap_shift(tap, dh, dw);
@@ -723,6 +730,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (SL_GEMM_KO >= 3) {  // knockout: no epilogue (one store keeps the accumulators live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1234.5f) e.y[tid] = 0;
+    return;
+  }
 
   // ---- epilogue (as conv_gemm_kernel, 8 waves) ----
   if (e.stats) {
@@ -840,6 +856,278 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
   if (bnb) {
     __syncthreads();
     bnb_fold<512, CPR>(e.bn, bacc, reinterpret_cast<float*>(smem), n0, e.ncols);
+  }
+  rsum_arrive(e.fold);
+}
+
+// ---------------------------------------------------------------------------
+// conv_gemm_wide_kernel: the 256 x 128 tile of conv_gemm_big_kernel with TWO workgroups per
+// CU, so one workgroup's epilogue (the data gradient's residual, BN input, mask and output
+// streams: ~250 KB per tile, profiles/r06_ko: 40-46 % of the big kernel's time at 512-1024
+// tiles, with every CU in its epilogue at the same moment and the matrix cores idle) runs
+// beside the other's k-loop.  For that a workgroup gets half the CU: 4 waves of 128 x 64
+// (8 x 4 MFMA tiles, 128 accumulator registers) and a 72 KB ring of three 32-deep stages
+// (24 KB: 256 + 128 rows of 64 B, chunk c of row r at c ^ g((r >> 2) & 3), g = {0, 2, 3, 1}:
+// conflict-free ds_read_b128 lane groups, as the stride-2 kernel).  Per stage a wave issues
+// 6 DMA pieces (16 rows x 64 B), reads 12 fragments at instruction offsets from two bases,
+// and runs 32 MFMAs -- 25 % fewer LDS bytes per MFMA than the big kernel's 64 x 64 waves.
+// Operand sourcing is the SL_GEMM_LEAN form (buffer resources, per-tap lane masks).  Used for
+// >= 512 tiles (SL_GEMM_WIDE); at 256 tiles a CU would hold one 4-wave workgroup.
+// ---------------------------------------------------------------------------
+#ifndef SL_GEMM_WIDE
+#define SL_GEMM_WIDE 1
+#endif
+__device__ __forceinline__ int swz32(int c, int r) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }
+
+template <bool TRANSPOSED>
+__global__ __launch_bounds__(256, 2) void conv_gemm_wide_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
+  constexpr int BM = 256, BN = 128, WBK = 32, NSLOT = 3, NTHR = 256;
+  constexpr int MT = 8, NT = 4;          // 16 x 16 MFMA tiles per wave (128 x 64)
+  constexpr int PA = 4, PB = 2;          // DMA pieces (16 rows x 32 k, 1 KB) per wave per stage
+  constexpr int PS = PA + PB;
+  constexpr int SLOT = (BM + BN) * WBK;  // elements: 24 KB
+  constexpr int CS_LD = BN + 8;
+  static_assert(BM * CS_LD <= NSLOT * SLOT, "epilogue tile must fit the ring");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSLOT * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int logical0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_cls = (int)gridDim.x / g.ncls;
+  const int cls = g.ncls > 1 ? logical0 / per_cls : 0;
+  const int logical = logical0 - cls * per_cls;
+  const int gK = g.cls_K[cls], gph = g.cls_ph[cls], gpw = g.cls_pw[cls], tap0 = g.cls_tap0[cls];
+  const uint16_t* eadd = (g.add_cls0_only && cls) ? nullptr : e.add;
+  const int tm = logical / tiles_n, tn = logical - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wm = wave >> 1, wn = wave & 1;
+  const bool phase = TRANSPOSED && g.ph >= 0;
+
+  // A rows of this lane: piece j covers rows 16 (wave * PA + j) .. +15 -> row + lane / 4,
+  // LDS chunk lane % 4 <- source chunk swz32(lane % 4, row)
+  int rbase[PA], rih[PA], riw[PA];
+  bool rok[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int row = 16 * (wave * PA + j) + (lane >> 2);
+    const Pix p = decode_pix(g, m0 + row);
+    int ih0, iw0;
+    if (!TRANSPOSED) {
+      ih0 = p.oh * g.stride - g.pad;
+      iw0 = p.ow * g.stride - g.pad;
+    } else if (phase) {
+      ih0 = p.oh;
+      iw0 = p.ow;
+    } else {
+      ih0 = p.oh + g.pad;
+      iw0 = p.ow + g.pad;
+    }
+    rih[j] = ih0;
+    riw[j] = iw0;
+    rok[j] = p.ok;
+    rbase[j] = ((p.n * g.SH + ih0) * g.SW + iw0) * g.SC + swz32(lane & 3, row) * 8;
+  }
+  constexpr unsigned OOB = 0x80000000u;
+  unsigned bbyte[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    const int row = 16 * (wave * PB + j) + (lane >> 2);
+    const int col = n0 + row;
+    bbyte[j] = col < e.ncols ? (unsigned)(col * g.wld + swz32(lane & 3, row) * 8) * 2u : OOB;
+  }
+  const int cps_shift = g.c_shift - 5;  // log2(stages per tap)
+  auto tap_shift = [&](int tap, int& dh, int& dw) {
+    if (phase) {
+      dh = g.dh[tap0 + tap];
+      dw = g.dw[tap0 + tap];
+    } else {
+      const int kh = (tap * g.kw_magic) >> 16, kw = tap - kh * g.KW;
+      dh = TRANSPOSED ? -kh : kh;
+      dw = TRANSPOSED ? -kw : kw;
+    }
+  };
+  const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(g.src), 0,
+                                                      (int)((long)g.N * g.SH * g.SW * g.SC * 2), 0x00020000);
+  const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(e.w), 0, (int)((long)e.ncols * g.wld * 2),
+                                                      0x00020000);
+  unsigned tmask[PA] = {};
+#pragma unroll 1
+  for (int tap = 0; tap < (gK / WBK) >> cps_shift; ++tap) {
+    int dh, dw;
+    tap_shift(tap, dh, dw);
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const bool v = rok[j] && (unsigned)(rih[j] + dh) < (unsigned)g.SH && (unsigned)(riw[j] + dw) < (unsigned)g.SW;
+      tmask[j] |= (unsigned)v << tap;
+    }
+  }
+  auto issue = [&](int kt) {
+    uint16_t* As = smem + (kt % NSLOT) * SLOT;
+    uint16_t* Bs = As + BM * WBK;
+    const int tap = kt >> cps_shift, ch0 = (kt & ((1 << cps_shift) - 1)) * WBK;
+    int dh, dw;
+    tap_shift(tap, dh, dw);
+    const int kb = phase ? g.tapw[tap0 + tap] * g.SC + ch0 : kt * WBK;
+    const int soff = (dh * g.SW + dw) * g.SC + ch0;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const unsigned off = (tmask[j] >> tap) & 1u ? (unsigned)(rbase[j] + soff) * 2u : OOB;
+      blds16(rs_a, (SL_LDS void*)(As + (wave * PA + j) * 16 * WBK), off);
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j)
+      blds16(rs_b, (SL_LDS void*)(Bs + (wave * PB + j) * 16 * WBK), bbyte[j] + (unsigned)kb * 2u);
+  };
+
+  // fragment i / j of a wave: row + 16 i, same swizzle (rows differ in bits >= 4): one base each
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
+  const int ra = wm * 128 + lr, rb = wn * 64 + lr;
+  const uint32_t aoff = (uint32_t)((ra * WBK + swz32(lg, ra) * 8) * 2);
+  const uint32_t boff = (uint32_t)(((BM + rb) * WBK + swz32(lg, rb) * 8) * 2);
+
+  floatx4_t acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = zero4();
+
+  const int nk = gK / WBK;
+  for (int kt = 0; kt < NSLOT - 1 && kt < nk; ++kt) issue(kt);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading slot (kt - 1) % 3
+    if (kt + NSLOT - 1 < nk) issue(kt + NSLOT - 1);
+    const uint32_t sb = lds0 + (uint32_t)((kt % NSLOT) * SLOT * 2);
+    const uint32_t a = sb + aoff, b = sb + boff;
+    short8_t af[MT], bf[NT];
+    bf[0] = ds_b128o<0>(b);
+    bf[1] = ds_b128o<16 * WBK * 2>(b);
+    bf[2] = ds_b128o<32 * WBK * 2>(b);
+    bf[3] = ds_b128o<48 * WBK * 2>(b);
+    af[0] = ds_b128o<0>(a);
+    af[1] = ds_b128o<16 * WBK * 2>(a);
+    af[2] = ds_b128o<32 * WBK * 2>(a);
+    af[3] = ds_b128o<48 * WBK * 2>(a);
+    af[4] = ds_b128o<64 * WBK * 2>(a);
+    af[5] = ds_b128o<80 * WBK * 2>(a);
+    af[6] = ds_b128o<96 * WBK * 2>(a);
+    af[7] = ds_b128o<112 * WBK * 2>(a);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (h == 0) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // B and A 0-3 landed
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 4 * h; i < 4 * h + 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue (conv_gemm_big_kernel's, 4 waves; operands in two passes of 8 chunks) ----
+  if (e.stats) {
+    float* rep = rsum_replica(e.stats, 2 * e.ncols);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r];
+          s += v;
+          q += v * v;
+        }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      const int col = n0 + wn * 64 + j * 16 + lr;
+      if (lg == 0 && col < e.ncols) {
+        rsum_add(rep, col, s);
+        rsum_add(rep, e.ncols + col, q);
+      }
+    }
+  }
+  if (e.yf) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + lr;
+        if (col >= e.ncols) continue;
+        const float bb = e.bias ? e.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * 128 + i * 16 + 4 * lg + r;
+          if (row < g.M) e.yf[(long)row * e.ncols + col] = acc[i][j][r] + bb;
+        }
+      }
+  }
+  if (!e.y) {
+    rsum_arrive(e.fold);
+    return;
+  }
+  uint16_t* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int cl = wn * 64 + j * 16 + lr;
+      const float bb = (e.bias && n0 + cl < e.ncols) ? e.bias[n0 + cl] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cs[(wm * 128 + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[i][j][r] + bb);
+    }
+  constexpr int CPR = BN / 8, EIT = BM * CPR / NTHR, EP = 8;  // 16 chunks per thread, 2 passes
+  const int cc = (tid % CPR) * 8, col = n0 + cc;
+  const bool bnb = TRANSPOSED && e.bn.x;
+  BnbAcc bacc;
+  float msc[8], msh[8];
+  if (bnb) bnb_init(e.bn, e.ncols, col, bacc, msc, msh);
+  __syncthreads();
+#pragma unroll
+  for (int p0 = 0; p0 < EIT; p0 += EP) {
+    long eoff[EP];
+    short8_t ea[EP];
+    BnbIn ebn[EP];
+#pragma unroll
+    for (int it = 0; it < EP; ++it) {
+      const int row = m0 + tid / CPR + (p0 + it) * (NTHR / CPR);
+      long orow = row;
+      if (phase) {
+        const Pix pq = decode_pix(g, row);
+        orow = ((long)pq.n * g.FH + 2 * pq.oh + gph) * g.FW + 2 * pq.ow + gpw;
+      }
+      eoff[it] = row < g.M ? orow * e.ldy + col : 0;
+      if (eadd) ea[it] = ld8(eadd + eoff[it]);
+      if (bnb) bnb_load(e.bn, eoff[it], ebn[it]);
+    }
+    short8_t vout[EP];
+#pragma unroll
+    for (int it = 0; it < EP; ++it) {
+      const int rl = tid / CPR + (p0 + it) * (NTHR / CPR), row = m0 + rl;
+      short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
+      if (eadd) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
+      }
+      if (bnb && row < g.M) bnb_chunk(e.bn, ebn[it], v, msc, msh, bacc);
+      vout[it] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < EP; ++it) {
+      const int row = m0 + tid / CPR + (p0 + it) * (NTHR / CPR);
+      if (row < g.M) *reinterpret_cast<short8_t*>(e.y + eoff[it]) = vout[it];
+    }
+  }
+  if (bnb) {
+    __syncthreads();
+    bnb_fold<NTHR, CPR>(e.bn, bacc, reinterpret_cast<float*>(smem), n0, e.ncols);
   }
   rsum_arrive(e.fold);
 }
@@ -1732,6 +2020,15 @@ static int gemm_big_enabled() {
   return v;
 }
 
+static int gemm_wide_enabled() {  // SL_GEMM_WIDE env override (A/B runs, tests)
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("SL_GEMM_WIDE");
+    v = s ? atoi(s) : SL_GEMM_WIDE;
+  }
+  return v;
+}
+
 // Kernel choice for one implicit GEMM: 0 = 256 x 128 large tile, else the 128/64 tile shape.
 struct GemmPlan {
   int big, BM, BN, tiles_n;
@@ -1769,6 +2066,11 @@ static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) 
   const GemmPlan p = plan_gemm<T>(g, e, g.ncls);
   dim3 grid((unsigned)(p.grid * g.ncls));
   if (p.big) {
+    if (SL_GEMM_LEAN && gemm_wide_enabled() && (long)grid.x >= 512) {
+      hipLaunchKernelGGL((conv_gemm_wide_kernel<T>), grid, dim3(256), 0, stream, g, e, p.tiles_n);
+      SL_CHECK_LAUNCH();
+      return 0;
+    }
     hipLaunchKernelGGL((conv_gemm_big_kernel<T>), grid, dim3(512), 0, stream, g, e, p.tiles_n);
     SL_CHECK_LAUNCH();
     return 0;

@@ -33,6 +33,7 @@ CONV_CASES = [
     (3, 7, 64, 64, 3, 2, 1),     # stride-2 dgrad by parity classes, odd extent (4 + 3 rows)
     # >= 256 tiles of 256 x 128: the large-tile kernel (conv_gemm_big_kernel)
     (256, 16, 128, 128, 3, 1, 1),   # forward + stride-1 transposed dgrad
+    (512, 16, 128, 128, 3, 1, 1),   # ... at 512 tiles: the two-per-CU kernel (conv_gemm_wide_kernel)
     (1024, 16, 128, 256, 3, 2, 1),  # forward + phase-mode dgrad (parity classes of 65,536 rows)
     (256, 8, 256, 512, 3, 1, 1),    # stage-4 shape forward; large-tile weight gradient (cout 512)
     (64, 16, 128, 256, 3, 1, 1),    # large-tile weight gradient, cout 256, K 1152
