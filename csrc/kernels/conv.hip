@@ -879,11 +879,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_big_kernel(ConvGeom g, ConvE
 #endif
 __device__ __forceinline__ int swz32(int c, int r) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }
 
-template <bool TRANSPOSED>
+// BM = 128 (grids of 256 big tiles, ResNet-18 stage 4): 128 x 128 tiles, waves of 64 x 64, a
+// 48 KB ring (two workgroups per CU: three would spill the data gradient).
+template <bool TRANSPOSED, int BM>
 __global__ __launch_bounds__(256, 2) void conv_gemm_wide_kernel(ConvGeom g, ConvEpi e, int tiles_n) {
-  constexpr int BM = 256, BN = 128, WBK = 32, NSLOT = 3, NTHR = 256;
-  constexpr int MT = 8, NT = 4;          // 16 x 16 MFMA tiles per wave (128 x 64)
-  constexpr int PA = 4, PB = 2;          // DMA pieces (16 rows x 32 k, 1 KB) per wave per stage
+  constexpr int BN = 128, WBK = 32, NSLOT = 3, NTHR = 256;
+  constexpr int MT = BM / 32, NT = 4;    // 16 x 16 MFMA tiles per wave (BM / 2 x 64)
+  constexpr int PA = BM / 64, PB = 2;    // DMA pieces (16 rows x 32 k, 1 KB) per wave per stage
   constexpr int PS = PA + PB;
   constexpr int SLOT = (BM + BN) * WBK;  // elements: 24 KB
   constexpr int CS_LD = BN + 8;
@@ -982,7 +984,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_wide_kernel(ConvGeom g, Conv
 
   // fragment i / j of a wave: row + 16 i, same swizzle (rows differ in bits >= 4): one base each
   const uint32_t lds0 = (uint32_t)(uintptr_t)(SL_LDS const uint16_t*)smem;
-  const int ra = wm * 128 + lr, rb = wn * 64 + lr;
+  const int ra = wm * (BM / 2) + lr, rb = wn * 64 + lr;
   const uint32_t aoff = (uint32_t)((ra * WBK + swz32(lg, ra) * 8) * 2);
   const uint32_t boff = (uint32_t)(((BM + rb) * WBK + swz32(lg, rb) * 8) * 2);
 
@@ -1010,14 +1012,16 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_wide_kernel(ConvGeom g, Conv
     af[1] = ds_b128o<16 * WBK * 2>(a);
     af[2] = ds_b128o<32 * WBK * 2>(a);
     af[3] = ds_b128o<48 * WBK * 2>(a);
-    af[4] = ds_b128o<64 * WBK * 2>(a);
-    af[5] = ds_b128o<80 * WBK * 2>(a);
-    af[6] = ds_b128o<96 * WBK * 2>(a);
-    af[7] = ds_b128o<112 * WBK * 2>(a);
+    if constexpr (MT == 8) {
+      af[4] = ds_b128o<64 * WBK * 2>(a);
+      af[5] = ds_b128o<80 * WBK * 2>(a);
+      af[6] = ds_b128o<96 * WBK * 2>(a);
+      af[7] = ds_b128o<112 * WBK * 2>(a);
+    }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < MT / 4; ++h) {
       __builtin_amdgcn_sched_barrier(0);
-      if (h == 0) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // B and A 0-3 landed
+      if (h == 0 && MT == 8) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // B and A 0-3 landed
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1064,7 +1068,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_wide_kernel(ConvGeom g, Conv
         const float bb = e.bias ? e.bias[col] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * 128 + i * 16 + 4 * lg + r;
+          const int row = m0 + wm * (BM / 2) + i * 16 + 4 * lg + r;
           if (row < g.M) e.yf[(long)row * e.ncols + col] = acc[i][j][r] + bb;
         }
       }
@@ -1081,9 +1085,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_wide_kernel(ConvGeom g, Conv
       const int cl = wn * 64 + j * 16 + lr;
       const float bb = (e.bias && n0 + cl < e.ncols) ? e.bias[n0 + cl] : 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Cs[(wm * 128 + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[i][j][r] + bb);
+      for (int r = 0; r < 4; ++r) Cs[(wm * (BM / 2) + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[i][j][r] + bb);
     }
-  constexpr int CPR = BN / 8, EIT = BM * CPR / NTHR, EP = 8;  // 16 chunks per thread, 2 passes
+  constexpr int CPR = BN / 8, EIT = BM * CPR / NTHR, EP = 8;  // 16 (8) chunks per thread, 2 (1) passes
   const int cc = (tid % CPR) * 8, col = n0 + cc;
   const bool bnb = TRANSPOSED && e.bn.x;
   BnbAcc bacc;
@@ -2067,7 +2071,14 @@ static int launch_gemm(const ConvGeom& g, const ConvEpi& e, hipStream_t stream) 
   dim3 grid((unsigned)(p.grid * g.ncls));
   if (p.big) {
     if (SL_GEMM_LEAN && gemm_wide_enabled() && (long)grid.x >= 512) {
-      hipLaunchKernelGGL((conv_gemm_wide_kernel<T>), grid, dim3(256), 0, stream, g, e, p.tiles_n);
+      hipLaunchKernelGGL((conv_gemm_wide_kernel<T, 256>), grid, dim3(256), 0, stream, g, e, p.tiles_n);
+      SL_CHECK_LAUNCH();
+      return 0;
+    }
+    if (SL_GEMM_LEAN && gemm_wide_enabled() >= 2) {  // 128-row tiles, twice the grid (A/B: SL_GEMM_WIDE=2)
+      const int tiles_m = (g.M + 127) / 128;
+      dim3 grid128((unsigned)((long)tiles_m * p.tiles_n * g.ncls));
+      hipLaunchKernelGGL((conv_gemm_wide_kernel<T, 128>), grid128, dim3(256), 0, stream, g, e, p.tiles_n);
       SL_CHECK_LAUNCH();
       return 0;
     }
