@@ -251,14 +251,14 @@ __device__ __forceinline__ void rsum_fold_row(float* buf, int n, int tid, int nt
 // `lds` (SL_RSUM_LDS floats); workgroup 0 also stores them to the result row.  Every thread
 // calls it (it ends with a workgroup barrier); res null or on == 0 (the launcher ran outside a
 // deferral: res is a folded row, or any plain array of n values): returns res.
-__device__ __forceinline__ const float* rsum_consume(const float* res, int n, float* lds, int on) {
-  if (!SL_RSUM_CONSUMER || !on || !res || n > SL_RSUM_LDS) return res;
-  const float* buf = res - (long)SL_REP * n;
+// The replicas of an rsum buffer summed into lds[0..n) by the whole workgroup (publish: also
+// stored to the result row with plain stores).  Ends before the final barrier of its callers.
+__device__ __forceinline__ void rsum_consume_fold(const float* buf, int n, float* lds, bool publish) {
 #if SL_DETERMINISTIC
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const float acc = (float)fix_value(reinterpret_cast<const unsigned long long*>(buf) + 2 * i);
     lds[i] = acc;
-    if (blockIdx.x == 0) const_cast<float*>(res)[i] = acc;
+    if (publish) const_cast<float*>(buf + (long)SL_REP * n)[i] = acc;
   }
 #else
   // every thread issues its (at most 16) replica loads at once: R * n <= 4096 values over the
@@ -281,7 +281,7 @@ __device__ __forceinline__ const float* rsum_consume(const float* res, int n, fl
       float t = lds[tid];
       for (int q = 1; q < tpe; ++q) t += lds[q * n + tid];
       lds[tid] = t;
-      if (blockIdx.x == 0) const_cast<float*>(res)[tid] = t;
+      if (publish) const_cast<float*>(buf + (long)SL_REP * n)[tid] = t;
     }
   } else {  // n = 512 / 1024: R <= 8, at most 4 values per thread
     float v[4][8];
@@ -300,11 +300,15 @@ __device__ __forceinline__ const float* rsum_consume(const float* res, int n, fl
       for (int r = 0; r < 8; ++r) t += v[j][r];
       if (e < n) {
         lds[e] = t;
-        if (blockIdx.x == 0) const_cast<float*>(res)[e] = t;
+        if (publish) const_cast<float*>(buf + (long)SL_REP * n)[e] = t;
       }
     }
   }
 #endif
+}
+__device__ __forceinline__ const float* rsum_consume(const float* res, int n, float* lds, int on) {
+  if (!SL_RSUM_CONSUMER || !on || !res || n > SL_RSUM_LDS) return res;
+  rsum_consume_fold(res - (long)SL_REP * n, n, lds, blockIdx.x == 0);
   __syncthreads();
   return lds;
 }
