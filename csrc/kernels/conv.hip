@@ -1175,6 +1175,9 @@ constexpr int S2_BK = 32;
 #ifndef SL_S2_EPI_EARLY
 #define SL_S2_EPI_EARLY 1
 #endif
+#ifndef SL_S2_LEAN
+#define SL_S2_LEAN SL_GEMM_LEAN  // the lean DMA / LDS-offset form in conv_dgrad_s2_kernel (A/B: 0)
+#endif
 #ifndef SL_S2_LAYOUT
 #define SL_S2_LAYOUT 1  // 0: the first cut's swizzle / MFMA orientation / b16 epilogue (A/B)
 #endif
@@ -1237,12 +1240,45 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
     bok[j] = col < e.ncols;
     bbase[j] = col * g.wld + s2_swz(lane & 3, row) * 8;
   }
+#if SL_S2_LEAN
+  // buffer-resource DMA (conv_gemm_big_kernel's lean form): per window, the lane's source byte
+  // offset at channel chunk 0, or an out-of-range offset (zeros) where the window leaves dY
+  const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(g.src), 0,
+                                                      (int)((long)g.N * g.SH * g.SW * g.SC * 2), 0x00020000);
+  const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(e.w), 0, (int)((long)e.ncols * g.wld * 2),
+                                                      0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  unsigned awin[4][PA], bbyte[PBQ];
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const int dh = w >> 1, dw = w & 1;
+      const bool v = aok[j] && ai[j] + dh < g.SH && aj[j] + dw < g.SW;
+      awin[w][j] = v ? (unsigned)(abase[j] + (dh * g.SW + dw) * g.SC) * 2u : OOB;
+    }
+#pragma unroll
+  for (int j = 0; j < PBQ; ++j) bbyte[j] = bok[j] ? (unsigned)bbase[j] * 2u : OOB;
+#endif
   // stage s = 4 * chunk + window
   auto issue = [&](int s, auto wc) __attribute__((always_inline)) {
     constexpr int W = decltype(wc)::value;
     constexpr int DH = W >> 1, DW = W & 1;
     uint16_t* As = smem + (s % NSLOT) * SLOT;
     const int ch0 = (s >> 2) * S2_BK;
+#if SL_S2_LEAN
+#pragma unroll
+    for (int j = 0; j < PA; ++j)
+      blds16(rs_a, (SL_LDS void*)(As + (wave * PA + j) * 16 * S2_BK), awin[W][j] + (unsigned)ch0 * 2u);
+#pragma unroll
+    for (int q = 0; q < s2_npairs(W); ++q) {
+      uint16_t* Bs = As + A_EL + q * B_EL;
+      const unsigned kb2 = (unsigned)(s2_tap(W, q) * g.SC + ch0) * 2u;
+#pragma unroll
+      for (int j = 0; j < PBQ; ++j) blds16(rs_b, (SL_LDS void*)(Bs + (wave * PBQ + j) * 16 * S2_BK), bbyte[j] + kb2);
+    }
+    return;
+#endif
     const int soff = (DH * g.SW + DW) * g.SC + ch0;
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
@@ -1305,12 +1341,24 @@ __global__ __launch_bounds__(256, OCC) void conv_dgrad_s2_kernel(ConvGeom g, Con
     if (s + AHEAD < nk) issue(s + AHEAD, std::integral_constant<int, WNA>{});
     const uint32_t sb = lds0 + (uint32_t)((s % NSLOT) * SLOT * 2);
     short8_t af[MT], bf[4][NT];
+#if SL_S2_LEAN
+    // fragment i / j sits 16 rows past fragment 0 with the same swizzle (s2_swz reads row bits
+    // 2-3): one base per operand, the rest as instruction offsets
+    const uint32_t a0 = sb + aoff[0], b0 = sb + boff[0];
+    static_for<0, MT>([&](auto ic) { af[ic.value] = ds_b128o<ic.value * 16 * S2_BK * 2>(a0); });
+    static_for<0, s2_npairs(W)>([&](auto qc) {
+      static_for<0, NT>([&](auto jc) {
+        bf[qc.value][jc.value] = ds_b128o<(A_EL + qc.value * B_EL) * 2 + jc.value * 16 * S2_BK * 2>(b0);
+      });
+    });
+#else
 #pragma unroll
     for (int i = 0; i < MT; ++i) af[i] = ds_b128(sb + aoff[i]);
 #pragma unroll
     for (int q = 0; q < s2_npairs(W); ++q)
 #pragma unroll
       for (int j = 0; j < NT; ++j) bf[q][j] = ds_b128(sb + (uint32_t)((A_EL + q * B_EL) * 2) + boff[j]);
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -2221,7 +2269,8 @@ static int dgrad_launch(const ConvGeom& g, const uint16_t* dy, int N, int OH, in
                         (ldd & 63) == 0;
   if ((add_even || even_only) && !phase_ok) return -5;
   if (SL_CONV_S2_FUSED && s2_enabled() && phase_ok && KH == 3 && !even_only && g_conv_phase && !(H & 1) && !(W & 1) &&
-      (ldd % S2_BK) == 0 && (cin & 7) == 0 && g.SH * 2 == H && g.SW * 2 == W) {
+      (ldd % S2_BK) == 0 && (cin & 7) == 0 && g.SH * 2 == H && g.SW * 2 == W &&
+      (!SL_S2_LEAN || ((long)g.N * g.SH * g.SW * g.SC < (1L << 29) && (long)cin * KH * KW * ldd < (1L << 29)))) {
     // all four parity classes in one workgroup (conv_dgrad_s2_kernel)
     ConvGeom q = g;
     q.OH = H / 2; q.OW = W / 2; q.hw_shift = ilog2(q.OH * q.OW); q.w_shift = ilog2(q.OW);
