@@ -1077,6 +1077,31 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_wide_kernel(ConvGeom g, Conv
     rsum_arrive(e.fold);
     return;
   }
+  constexpr int CPR = BN / 8, EIT = BM * CPR / NTHR, EP = 8;  // 16 (8) chunks per thread, 2 (1) passes
+  const int cc = (tid % CPR) * 8, col = n0 + cc;
+  const bool bnb = TRANSPOSED && e.bn.x;
+  // a pass's residual / BN operands: pass 0's go out before the staging barrier, pass 1's
+  // before pass 0's stores (their latency hides under the barrier / the stores)
+  struct EpiIn {
+    long off[EP];
+    short8_t a[EP];
+    BnbIn bn[EP];
+  };
+  auto epi_load = [&](int p0, EpiIn& in) __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < EP; ++it) {
+      const int row = m0 + tid / CPR + (p0 + it) * (NTHR / CPR);
+      long orow = row;
+      if (phase) {
+        const Pix pq = decode_pix(g, row);
+        orow = ((long)pq.n * g.FH + 2 * pq.oh + gph) * g.FW + 2 * pq.ow + gpw;
+      }
+      in.off[it] = row < g.M ? orow * e.ldy + col : 0;
+      if (eadd) in.a[it] = ld8(eadd + in.off[it]);
+      if (bnb) bnb_load(e.bn, in.off[it], in.bn[it]);
+    }
+  };
+  EpiIn in0, in1;
   uint16_t* Cs = smem;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -1087,47 +1112,39 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_wide_kernel(ConvGeom g, Conv
 #pragma unroll
       for (int r = 0; r < 4; ++r) Cs[(wm * (BM / 2) + i * 16 + 4 * lg + r) * CS_LD + cl] = f2bf(acc[i][j][r] + bb);
     }
-  constexpr int CPR = BN / 8, EIT = BM * CPR / NTHR, EP = 8;  // 16 (8) chunks per thread, 2 (1) passes
-  const int cc = (tid % CPR) * 8, col = n0 + cc;
-  const bool bnb = TRANSPOSED && e.bn.x;
   BnbAcc bacc;
   float msc[8], msh[8];
   if (bnb) bnb_init(e.bn, e.ncols, col, bacc, msc, msh);
+  epi_load(0, in0);  // in flight under the staging barrier (the accumulators are dead here)
   __syncthreads();
-#pragma unroll
-  for (int p0 = 0; p0 < EIT; p0 += EP) {
-    long eoff[EP];
-    short8_t ea[EP];
-    BnbIn ebn[EP];
-#pragma unroll
-    for (int it = 0; it < EP; ++it) {
-      const int row = m0 + tid / CPR + (p0 + it) * (NTHR / CPR);
-      long orow = row;
-      if (phase) {
-        const Pix pq = decode_pix(g, row);
-        orow = ((long)pq.n * g.FH + 2 * pq.oh + gph) * g.FW + 2 * pq.ow + gpw;
-      }
-      eoff[it] = row < g.M ? orow * e.ldy + col : 0;
-      if (eadd) ea[it] = ld8(eadd + eoff[it]);
-      if (bnb) bnb_load(e.bn, eoff[it], ebn[it]);
-    }
-    short8_t vout[EP];
+  auto epi_pass = [&](int p0, const EpiIn& in, short8_t (&vout)[EP]) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < EP; ++it) {
       const int rl = tid / CPR + (p0 + it) * (NTHR / CPR), row = m0 + rl;
       short8_t v = *reinterpret_cast<const short8_t*>(Cs + rl * CS_LD + cc);
       if (eadd) {
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)ea[it][t]));
+        for (int t = 0; t < 8; ++t) v[t] = (short)f2bf(bf2f((uint16_t)v[t]) + bf2f((uint16_t)in.a[it][t]));
       }
-      if (bnb && row < g.M) bnb_chunk(e.bn, ebn[it], v, msc, msh, bacc);
+      if (bnb && row < g.M) bnb_chunk(e.bn, in.bn[it], v, msc, msh, bacc);
       vout[it] = v;
     }
+  };
+  auto epi_store = [&](int p0, const EpiIn& in, const short8_t (&vout)[EP]) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < EP; ++it) {
       const int row = m0 + tid / CPR + (p0 + it) * (NTHR / CPR);
-      if (row < g.M) *reinterpret_cast<short8_t*>(e.y + eoff[it]) = vout[it];
+      if (row < g.M) *reinterpret_cast<short8_t*>(e.y + in.off[it]) = vout[it];
     }
+  };
+  short8_t vout[EP];
+  epi_pass(0, in0, vout);
+  if constexpr (EIT > EP) epi_load(EP, in1);
+  epi_store(0, in0, vout);
+  if constexpr (EIT > EP) {
+    static_assert(EIT == 2 * EP, "two passes");
+    epi_pass(EP, in1, vout);
+    epi_store(EP, in1, vout);
   }
   if (bnb) {
     __syncthreads();
