@@ -110,6 +110,16 @@ class ReplicaDivergence(RuntimeError):
     """The replicas still differ after the re-timed fallback: no number may be reported."""
 
 
+_T0 = time.perf_counter()
+
+
+def _progress(msg: str) -> None:
+    """SL_BENCH_PROGRESS=1: one stderr line per phase (diagnosing slow or stuck multi-rank runs)."""
+    if os.environ.get("SL_BENCH_PROGRESS") == "1":
+        print(f"[bench rank {os.environ.get('RANK', '0')} +{time.perf_counter() - _T0:.1f}s] {msg}",
+              file=sys.stderr, flush=True)
+
+
 def verify_replicas(check, retime, exchange_failed=lambda: False):
     """The N>1 safety net, for EVERY gradient-exchange path (xGMI one-/two-shot, RCCL captured or
     eager, gloo).  ``check()`` is True iff every replica holds bit-identical weights (decided by an
@@ -178,6 +188,10 @@ def launch_ranks(args, argv) -> int:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
     env["SL_BENCH_LAUNCHED"] = "1"
+    # ranks sharing a GPU (rehearsal): keep their hardware queues within the GPU's budget
+    from serverless_learn_amd.utils.gpu_share import share_gpu_env
+
+    share_gpu_env(env, -(-args.gpus // max(n_dev, 1)))
     p = subprocess.run(cmd, env=env)
     return p.returncode
 
@@ -365,6 +379,7 @@ def main(argv=None) -> int:
         y = torch.from_numpy(labels.copy()).pin_memory().to(dev, non_blocking=True)
     torch.cuda.synchronize()
     t_ingest = time.perf_counter() - t_ingest
+    _progress(f"shard ready ({n_records} records)")
 
     # ---- 2. engine ----------------------------------------------------------
     if mlp:
@@ -406,6 +421,7 @@ def main(argv=None) -> int:
             tr.bucket_hook = lambda view: dist.all_reduce(view, async_op=True)
             tr.bucket_wait = lambda handles: [h.wait() for h in handles]
     tr.load_shard(x, y)
+    _progress("engine ready")
 
     # the xGMI exchange needs no host sync, so the N>1 MLP step is graph-captured like N=1; RCCL
     # collectives (the MLP all-reduce hook, the ResNet bucket all-reduces and their waits) are
@@ -415,8 +431,9 @@ def main(argv=None) -> int:
     graph_pg = args.dist_backend == "nccl" and (world == 1 or args.graph_collectives)
     use_graph = args.graph == "on" or (args.graph == "auto" and (world == 1 or xg is not None or graph_pg))
     warm_eager = min(args.warmup, 3)
-    for _ in range(warm_eager):
+    for i in range(warm_eager):
         tr.step()
+        _progress(f"eager warm-up step {i + 1}")
     run = getattr(tr, "steps", None) or (lambda n: [tr.step() for _ in range(n)])
     if use_graph:
         try:
@@ -459,6 +476,7 @@ def main(argv=None) -> int:
         first_loss = tr.stats().loss  # after the eager warm-up steps
         upload_graph()
     run(args.warmup - warm_eager)
+    _progress("warm-up done")
     if not preload:
         torch.cuda.synchronize()
         first_loss = tr.stats().loss
@@ -560,7 +578,17 @@ def main(argv=None) -> int:
 
     if autotune is not None:
         upload_graph()  # the autotune re-captured the chosen mode's graph
+    _progress("timed region starts")
+    if os.environ.get("SL_BENCH_PROGRESS") == "1" and not (use_graph and mlp):
+        run_inner = run
+
+        def run(n):  # diagnostics only: one synchronised step at a time, one line each
+            for i in range(n):
+                run_inner(1)
+                torch.cuda.synchronize()
+                _progress(f"step {i + 1} of {n}")
     elapsed = timed()
+    _progress(f"timed region done ({elapsed:.3f} s)")
     st_timed = tr.stats()
     replicas_identical, fallback = None, None
     if world > 1:

@@ -659,3 +659,18 @@ def test_allreduce_async_enqueue_failure_is_group_broken():
         with pytest.raises(GroupBroken):
             g.allreduce_async(torch.zeros(2), op)
         assert g.broken
+
+
+def test_share_gpu_env_caps_hardware_queues_only_when_processes_share_a_gpu():
+    """Several processes on one GPU: GPU_MAX_HW_QUEUES is capped so their queues stay within the
+    GPU's budget (4+ processes at HIP's 4 each were time-sliced, profiles/r06_ranks); one or two
+    processes keep the default, and a lower value already set is kept."""
+    from serverless_learn_amd.utils.gpu_share import QUEUE_BUDGET, share_gpu_env
+
+    assert share_gpu_env({}, 1) == {}
+    assert share_gpu_env({"GPU_MAX_HW_QUEUES": "4"}, 2) == {"GPU_MAX_HW_QUEUES": "4"}
+    assert share_gpu_env({"GPU_MAX_HW_QUEUES": "4"}, 4) == {"GPU_MAX_HW_QUEUES": "2"}
+    assert share_gpu_env({}, 8) == {"GPU_MAX_HW_QUEUES": "1"}
+    assert share_gpu_env({"GPU_MAX_HW_QUEUES": "1"}, 3) == {"GPU_MAX_HW_QUEUES": "1"}
+    for n in range(3, 17):
+        assert n * int(share_gpu_env({}, n)["GPU_MAX_HW_QUEUES"]) <= max(QUEUE_BUDGET, n)

@@ -30,7 +30,11 @@ def test_xgmi_exchange_ranks_on_one_gpu(world, two_shot):
     cmd = ["timeout", "-k", "10", str(limit), sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "scripts", "xgmi_check.py"), "--same-device"] + (["--two-shot"] if two_shot else [])
-    p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=limit + 15)
+    from serverless_learn_amd.utils.gpu_share import share_gpu_env
+
+    env = share_gpu_env(dict(os.environ), world)
+    p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=limit + 15,
+                       env=env)
     assert p.returncode == 0, p.stdout[-4000:]
     assert p.stdout.count("XGMI_CHECK_OK") == world, p.stdout[-4000:]
 
