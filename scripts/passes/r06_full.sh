@@ -1,10 +1,12 @@
 #!/bin/bash
-# Round 6: full validation at HEAD -- every GPU test, driver-form benches (MLP x3, ResNet-18 x2),
+# Round 6: full validation at HEAD -- smoke(), every GPU test, driver-form benches (MLP x3, ResNet-18 x2),
 # 2-rank rehearsals, kernel tables of both models.
 set -u
 cd "$(dirname "$0")/../.."
 export TMPDIR=/tmp
 O=gpurun_out/${PASS_TAG:-r06_full}; mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > $O/smoke.log 2>&1 || exit 2
+tail -1 $O/smoke.log
 timeout -k 10 1500 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu \
   > $O/pytest_gpu.log 2>&1; rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 for i in 1 2 3; do
