@@ -1799,6 +1799,9 @@ __global__ __launch_bounds__(64) void mlp_w1_rowsum_kernel(const uint16_t* w1h, 
 // separate row-sum launch is gone), then 1,024-parameter chunks of b1 W2 b2 W3 b3.
 // Inline xGMI mode: each workgroup waits for the step's signals first (xg_block_wait).
 constexpr int UPD_NT = 256;
+#ifndef SL_UPD_HOIST
+#define SL_UPD_HOIST 1
+#endif
 constexpr int UPD_W1_ROW4 = D_IN / 4;  // 196 float4 per W1 row
 constexpr int UPD_REST_TASKS = (int)((P_N - P_B1 + 4 * UPD_NT - 1) / (4 * UPD_NT));
 constexpr int UPD_TASKS = HID + UPD_REST_TASKS;
@@ -1821,26 +1824,50 @@ __global__ __launch_bounds__(UPD_NT) void mlp_update_kernel(SgdArgs a, XgArgs x)
   __shared__ unsigned s_step;
   const int tid = threadIdx.x;
   if (a.cursor && blockIdx.x == 0 && tid == 0) atomicAdd(a.cursor, 1);
+  // SL_UPD_HOIST: the first work item's weight / momentum loads go out before the peer wait
+  // (they do not depend on the peers), so their latency overlaps the wait
+  auto item = [&](int task, long& i4, long& ic, bool& live) __attribute__((always_inline)) {
+    const bool w1 = task < HID;
+    const long first = w1 ? (long)task * UPD_W1_ROW4 : P_B1 / 4 + (long)(task - HID) * UPD_NT;
+    i4 = first + tid;
+    live = w1 ? tid < UPD_W1_ROW4 : i4 * 4 < P_N;
+    ic = live ? i4 : first;  // dead lanes load a live address (same owner), unused
+  };
+  long i4 = 0, ic = 0;
+  bool live = false;
+  float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f), m4 = w4;
+  if (SL_UPD_HOIST && (int)blockIdx.x < UPD_TASKS) {
+    item(blockIdx.x, i4, ic, live);
+    w4 = reinterpret_cast<const float4*>(a.w)[ic];
+    if (a.mom) m4 = reinterpret_cast<const float4*>(a.mom)[ic];
+  }
   unsigned s = 0;
+  float4 own = make_float4(0.f, 0.f, 0.f, 0.f);  // one-shot: this rank's own slot, first work item
   if constexpr (XG) {
     s = xg_block_step(x, &s_step);
+    // this rank's slot was written by the launch before this one: no peer wait needed for it
+    if (SL_UPD_HOIST && x.chunk4 == 0 && (int)blockIdx.x < UPD_TASKS)
+      own = xg_load(xg_rsrc(x, x.rank), xg_slot_off(x, s) + (unsigned)(ic * 16));
     if (x.inline_sync) xg_block_wait(x, x.chunk4 > 0 ? 1 : 0, s);  // two-shot: the owners' reduced slots
   }
   for (int task = blockIdx.x; task < UPD_TASKS; task += gridDim.x) {
     const bool w1 = task < HID;  // uniform per workgroup
-    const long first = w1 ? (long)task * UPD_W1_ROW4 : P_B1 / 4 + (long)(task - HID) * UPD_NT;
-    const long i4 = first + tid;
-    const bool live = w1 ? tid < UPD_W1_ROW4 : i4 * 4 < P_N;
-    const long ic = live ? i4 : first;  // dead lanes load a live address (same owner), unused
+    if (!SL_UPD_HOIST || task != (int)blockIdx.x) {
+      item(task, i4, ic, live);
+      w4 = reinterpret_cast<const float4*>(a.w)[ic];
+      m4 = a.mom ? reinterpret_cast<const float4*>(a.mom)[ic] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float4 g;
     if constexpr (XG) {
       if (x.chunk4 > 0) {
         g = xg_load_reduced_any(x, s, ic);
       } else {
         float4 v[XG_MAX_WORLD];
+        const bool own_ready = SL_UPD_HOIST && task == (int)blockIdx.x;
 #pragma unroll
         for (int q = 0; q < XG_MAX_WORLD; ++q)
-          if (q < x.world) v[q] = xg_load(xg_rsrc(x, q), xg_slot_off(x, s) + (unsigned)(ic * 16));
+          if (q < x.world)
+            v[q] = own_ready && q == x.rank ? own : xg_load(xg_rsrc(x, q), xg_slot_off(x, s) + (unsigned)(ic * 16));
         g = v[0];
 #pragma unroll
         for (int q = 1; q < XG_MAX_WORLD; ++q)
@@ -1851,8 +1878,6 @@ __global__ __launch_bounds__(UPD_NT) void mlp_update_kernel(SgdArgs a, XgArgs x)
     } else {
       g = reinterpret_cast<const float4*>(a.grad_in)[ic];
     }
-    const float4 w4 = reinterpret_cast<const float4*>(a.w)[ic];
-    const float4 m4 = a.mom ? reinterpret_cast<const float4*>(a.mom)[ic] : make_float4(0.f, 0.f, 0.f, 0.f);
     long long fx = 0;
     if (live) {
       const float ga[4] = {g.x, g.y, g.z, g.w}, wa[4] = {w4.x, w4.y, w4.z, w4.w}, ma[4] = {m4.x, m4.y, m4.z, m4.w};
