@@ -143,13 +143,9 @@ def verify_replicas(check, retime, exchange_failed=lambda: False):
 
 
 def _free_port() -> int:
-    import socket
+    from serverless_learn_amd.utils.ports import reserve_port
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    return reserve_port()
 
 
 def visible_devices() -> int:

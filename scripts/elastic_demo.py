@@ -28,7 +28,6 @@ import argparse
 import json
 import os
 import signal
-import socket
 import subprocess
 import sys
 import tempfile
@@ -41,11 +40,9 @@ from serverless_learn_amd.utils.gpu_share import share_gpu_env  # noqa: E402
 
 
 def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from serverless_learn_amd.utils.ports import reserve_port
+
+    return reserve_port()
 
 
 def read_events(path: str) -> list[dict]:

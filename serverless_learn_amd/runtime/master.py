@@ -25,7 +25,6 @@ broadcast loop implements the dead ``periodically_send_updates``.
 from __future__ import annotations
 
 import random
-import socket
 import threading
 import time
 from concurrent import futures
@@ -45,11 +44,9 @@ PHASE_FIELDS = ("step_ms", "data_wait_ms", "compute_ms", "exchange_ms", "update_
 
 
 def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    from ..utils.ports import reserve_port
+
+    return reserve_port()
 
 
 class Master:

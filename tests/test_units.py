@@ -674,3 +674,18 @@ def test_share_gpu_env_caps_hardware_queues_only_when_processes_share_a_gpu():
     assert share_gpu_env({"GPU_MAX_HW_QUEUES": "1"}, 3) == {"GPU_MAX_HW_QUEUES": "1"}
     for n in range(3, 17):
         assert n * int(share_gpu_env({}, n)["GPU_MAX_HW_QUEUES"]) <= max(QUEUE_BUDGET, n)
+
+
+def test_reserve_port_stays_below_the_ephemeral_range_and_binds():
+    """Ports handed to processes that bind them later come from below the kernel's ephemeral
+    range (outgoing connections never take them) and are distinct within a process."""
+    import socket
+
+    from serverless_learn_amd.utils.ports import _ephemeral_low, reserve_port
+
+    ports = [reserve_port() for _ in range(32)]
+    assert len(set(ports)) == len(ports)
+    assert all(10000 <= p < max(10001, _ephemeral_low()) for p in ports)
+    s = socket.socket()
+    s.bind(("127.0.0.1", ports[0]))
+    s.close()

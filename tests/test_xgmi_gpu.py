@@ -2,7 +2,6 @@
 exchange buffers over IPC and run the generic all-reduce and the MLP step with the
 all-reduce fused into its update kernel (scripts/xgmi_check.py does the checking)."""
 import os
-import socket
 import subprocess
 import sys
 
@@ -13,11 +12,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from serverless_learn_amd.utils.ports import reserve_port
+
+    return reserve_port()
 
 
 @pytest.mark.parametrize("world,two_shot", [(2, False), (3, False), (2, True), (3, True),
