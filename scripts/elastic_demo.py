@@ -36,8 +36,6 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from serverless_learn_amd.utils.gpu_share import share_gpu_env  # noqa: E402
-
 
 def free_port() -> int:
     from serverless_learn_amd.utils.ports import reserve_port
@@ -102,8 +100,6 @@ def main(argv=None) -> int:
         if args.xgmi_gloo:
             env["SL_XGMI_GLOO"] = "1"
         env.setdefault("OMP_NUM_THREADS", "2")
-        if args.device.startswith("cuda"):  # the workers share one GPU: cap their hardware queues
-            share_gpu_env(env, args.workers)
         procs[name] = subprocess.Popen([sys.executable, "-m", "serverless_learn_amd.cli", *role_args, *common],
                                        env=env, stdout=subprocess.DEVNULL, stderr=open(path + ".err", "w"))
         logs[name] = path

@@ -5,6 +5,12 @@ on one GPU hold more queues than the GPU can keep mapped, the scheduler time-sli
 4-rank same-GPU MLP rehearsal ran at 16.9 M samples/s with 4 queues per process and at 452 M
 with 2 (profiles/r06_ranks), and a 4-rank ResNet-18 step took ~45 s instead of ~0.03 s.  One
 process per GPU, the deployment shape, is unaffected.
+
+Not used for the elastic workers (scripts/elastic_demo.py). With 2 queues each, a surviving
+worker stopped answering CheckUp while its update kernel spun for the dead peer until the
+exchange's 10 s timeout. The likely cause is a graph replay blocking on a full queue while it
+holds the GIL. The master then evicted that healthy worker (r06_full5). With HIP's 4 queues
+the same test passes.
 """
 from __future__ import annotations
 
