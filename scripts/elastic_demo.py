@@ -96,7 +96,7 @@ def main(argv=None) -> int:
 
     def spawn(name, role_args):
         path = os.path.join(logdir, name + ".log")
-        env = dict(os.environ, SL_LOG_FILE=path, PYTHONPATH=ROOT, SL_LOG_PARAM_SUM="1")
+        env = dict(os.environ, SL_LOG_FILE=path, PYTHONPATH=ROOT, SL_LOG_PARAM_SUM="1", SL_STALL_DUMP_S="3")
         if args.xgmi_gloo:
             env["SL_XGMI_GLOO"] = "1"
         env.setdefault("OMP_NUM_THREADS", "2")

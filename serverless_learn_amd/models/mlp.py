@@ -28,6 +28,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..utils.graphs import GraphSlots
+
 D_IN = 784
 D_IN_PAD = 832  # w1h row stride: layer-1 K in 13 chunks of 64 (mlp_fused.hip)
 HIDDEN = 256
@@ -269,7 +271,7 @@ def default_slices(batch: int) -> int:
     return int(_native.lib().sl_mlp_wgrad_slices(batch, 0))
 
 
-class FusedMLPTrainer:
+class FusedMLPTrainer(GraphSlots):
     """MI355X training engine for the MLP: 3 HIP launches per step.
 
     Buffers are allocated once for a fixed per-GPU batch; the data shard stays
@@ -538,14 +540,17 @@ class FusedMLPTrainer:
         graph may hold a communicator's kernels: the runtime calls this before it re-forms or
         tears down the group, so no replay is in flight when the old
         communicator goes away and the k-step graph is not left alive holding it."""
-        if self.graph is not None:  # steps() ignores graph_unrolled once graph is None (ADVICE r05)
+        if self.graph is not None or self.retired_graphs:  # steps() ignores graph_unrolled once graph is None (ADVICE r05)
             torch.cuda.synchronize(self.device)
         self.graph = None
         self.graph_unrolled = None
+        self.reap_graphs(sync=False)
 
     def capture(self, warmup: int = 2, unroll: int = 1) -> None:
         """Capture one step into a hipGraph (kernels only, or kernels + RCCL);
-        ``unroll > 1`` also captures a k-step graph used by :meth:`steps`."""
+        ``unroll > 1`` also captures a k-step graph used by :meth:`steps`.  Graphs replaced
+        since the last capture are freed first, after a device sync (utils/graphs.py)."""
+        self.reap_graphs()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

@@ -34,6 +34,7 @@ from __future__ import annotations
 import os
 import torch
 
+from ..utils.graphs import GraphSlots
 from .mlp import StepStats
 from .resnet import CIFAR_MEAN, CIFAR_STD, BlockSpec, BNSpec, ConvSpec, init_params, resnet18_spec
 
@@ -73,7 +74,7 @@ class _Conv:
         self.wt = torch.zeros(spec.cin * spec.k * spec.k * self.ldt, dtype=torch.bfloat16, device=dev)
 
 
-class FusedResNetTrainer:
+class FusedResNetTrainer(GraphSlots):
     def __init__(self, batch: int, device="cuda", lr: float = 0.05, momentum: float = 0.9,
                  weight_decay: float = 5e-4, seed: int = 0, world_size: int = 1, stem: str = "cifar",
                  classes: int = 10, flat: torch.Tensor | None = None, bn_momentum: float = 0.1,
@@ -445,11 +446,13 @@ class FusedResNetTrainer:
     def drop_graphs(self) -> None:
         """Release the captured step graph once the device is done with it (called by the
         runtime before it re-forms or tears down a group whose collectives the graph holds)."""
-        if self.graph is not None:
+        if self.graph is not None or self.retired_graphs:
             torch.cuda.synchronize(self.device)
         self.graph = None
+        self.reap_graphs(sync=False)
 
     def capture(self, warmup: int = 2) -> None:
+        self.reap_graphs()  # graphs replaced since the last capture, freed after a sync (utils/graphs.py)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

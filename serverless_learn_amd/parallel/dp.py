@@ -36,6 +36,10 @@ class GroupBroken(RuntimeError):
     pass
 
 
+class GroupCancelled(RuntimeError):
+    """A rendezvous abandoned because the membership it was for is no longer current."""
+
+
 class ElasticGroup:
     """A re-formable process group object (not torch's global default group).
 
@@ -79,31 +83,52 @@ class ElasticGroup:
             except Exception as e:
                 self.log.warn("abort_failed", error=repr(e))
 
-    def _open_round(self, ep_store, epoch: int, rank: int) -> int:
-        """Agree on a fresh rendezvous round for this epoch.
+    def _open_round(self, ep_store, epoch: int, rank: int, world: int, cancelled=None) -> int:
+        """Agree on a fresh rendezvous round for this epoch, with every rank checked in.
 
-        Rank 0 opens round r+1 on every attempt; the other ranks join the first
-        round newer than the last one they tried.  A failed or half-formed
-        attempt therefore never leaves stale keys under the next attempt's
-        prefix (which would make gloo/RCCL connect to dead endpoints).
+        Rank 0 opens round r+1 on every attempt; the other ranks check in to the newest
+        round rank 0 has opened (``in<r>``) and wait for its go (``go<r>``), which rank 0
+        posts once all ``world - 1`` of them are in.  Only then does anyone build the
+        backend group, so a failed or half-formed attempt never leaves stale keys under the
+        next attempt's prefix (gloo/RCCL would connect to dead endpoints).
+
+        A rank that checked in to a round rank 0 has just given up on (its wait timed out as
+        the rank arrived) moves to the next round as soon as rank 0 opens it.  Before the
+        check-in, a late rank could join the abandoned round and wait out a whole timeout
+        there while rank 0 waited in the next one (the r06_full7 elastic failure).
+        ``cancelled()`` turning true (the worker's view moved past ``epoch``) ends the wait.
         """
-        need = self._rounds.get(epoch, 0) + 1
+        deadline = time.monotonic() + self.timeout.total_seconds()
+
+        def tick(what: str) -> None:
+            if cancelled is not None and cancelled():
+                raise GroupCancelled(f"epoch {epoch} superseded while {what}")
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"epoch {epoch}: timed out while {what}")
+            time.sleep(0.02)
+
         if rank == 0:
             rnd = int(ep_store.add("round", 1))
+            while int(ep_store.add(f"in{rnd}", 0)) < world - 1:
+                tick(f"waiting for {world - 1} ranks to check in to round {rnd}")
+            ep_store.add(f"go{rnd}", 1)
         else:
-            deadline = time.monotonic() + self.timeout.total_seconds()
+            need = self._rounds.get(epoch, 0) + 1
+            rnd = 0
             while True:
-                rnd = int(ep_store.add("round", 0))
-                if rnd >= need:
+                cur = int(ep_store.add("round", 0))
+                if cur >= need and cur != rnd:
+                    ep_store.add(f"in{cur}", 1)  # the newest round rank 0 opened
+                    rnd = cur
+                if rnd and int(ep_store.add(f"go{rnd}", 0)) > 0:
                     break
-                if time.monotonic() > deadline:
-                    raise TimeoutError(f"rank 0 opened no round >= {need} for epoch {epoch}")
-                time.sleep(0.05)
+                tick(f"waiting for rank 0's go (round {rnd or '-'}, need >= {need})")
         self._rounds[epoch] = rnd
         return rnd
 
-    def reform(self, epoch: int, rank: int, world: int, rendezvous: str) -> bool:
-        """Join the group for ``epoch``. Returns True when the group is usable."""
+    def reform(self, epoch: int, rank: int, world: int, rendezvous: str, cancelled=None) -> bool:
+        """Join the group for ``epoch``. Returns True when the group is usable.
+        ``cancelled``: optional predicate polled during the rendezvous; True abandons it."""
         with self.lock:
             self.teardown()
             self.epoch, self.rank, self.world = epoch, rank, world
@@ -112,7 +137,7 @@ class ElasticGroup:
                 return True  # single worker: nothing to reduce
             try:
                 base = self._store(rendezvous)
-                rnd = self._open_round(dist.PrefixStore(f"sl/e{epoch}", base), epoch, rank)
+                rnd = self._open_round(dist.PrefixStore(f"sl/e{epoch}", base), epoch, rank, world, cancelled)
                 store = dist.PrefixStore(f"sl/e{epoch}/r{rnd}", base)
                 if self.backend == "nccl":
                     opts = dist.ProcessGroupNCCL.Options()
@@ -126,7 +151,8 @@ class ElasticGroup:
                 return True
             except Exception as e:
                 self.broken = True
-                self.log.warn("group_form_failed", epoch=epoch, rank=rank, world=world, error=repr(e))
+                event = "group_form_cancelled" if isinstance(e, GroupCancelled) else "group_form_failed"
+                self.log.warn(event, epoch=epoch, rank=rank, world=world, error=repr(e))
                 self.teardown()
                 return False
 

@@ -29,6 +29,7 @@ from __future__ import annotations
 import os
 import random
 import socket
+import sys
 import threading
 import time
 
@@ -434,7 +435,16 @@ class Worker:
         self._ensure_resumed(v.get("resume_file", 0))
         with trace.span("regroup", epoch=v["epoch"], world=v["world"]):
             self._drop_graphs()  # a captured step may embed the old communicator
-            ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"])
+            # the drains above can take up to the exchange's peer timeout: form the view that is
+            # current NOW, not the one read before them (a stale epoch's rendezvous waits out its
+            # whole timeout for members that already moved on)
+            with self.view_lock:
+                v = dict(self.view)
+            if not self._needs_regroup(v):
+                return
+            epoch = v["epoch"]
+            ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"],
+                                   cancelled=lambda: self.view["epoch"] != epoch or self._stop.is_set())
             if not ok:
                 self._stop.wait(0.2)
                 return
@@ -902,6 +912,19 @@ class Worker:
                 self._after_external_update()
         return True
 
+    def _stall_watch(self) -> None:
+        """Diagnostics (``SL_STALL_DUMP_S`` seconds): dump every thread's stack to stderr when
+        the interpreter makes no progress that long.  A thread re-arms faulthandler's C
+        watchdog every quarter period; the watchdog fires only when this thread could not run
+        (the GIL held by a blocking call: the stall that silenced CheckUp in r06_full7)."""
+        import faulthandler
+
+        period = float(os.environ["SL_STALL_DUMP_S"])
+        while not self._stop.is_set():
+            faulthandler.dump_traceback_later(period, repeat=False, file=sys.stderr)
+            self._stop.wait(period / 4)
+        faulthandler.cancel_dump_traceback_later()
+
     # ---- lifecycle ---------------------------------------------------------------
     def start(self) -> "Worker":
         self.server = RpcServer(self.addr_requested, max_workers=16, max_message_bytes=self.cfg.max_message_bytes,
@@ -915,6 +938,8 @@ class Worker:
         loops = [self._register_loop, self._train_loop]
         if self.cfg.sync in ("gossip", "ps") or self.cfg.model == "simulate":
             loops.append(self._gossip_loop)
+        if float(os.environ.get("SL_STALL_DUMP_S", "0") or 0) > 0:
+            loops.append(self._stall_watch)
         for fn in loops:
             t = threading.Thread(target=fn, daemon=True, name="sl-worker-" + fn.__name__)
             t.start()

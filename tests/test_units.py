@@ -689,3 +689,99 @@ def test_reserve_port_stays_below_the_ephemeral_range_and_binds():
     s = socket.socket()
     s.bind(("127.0.0.1", ports[0]))
     s.close()
+
+
+def test_rendezvous_round_abandoned_by_rank0_is_left_by_a_late_rank():
+    """A rank arriving just as rank 0 gives up on a round (its check-in wait timed out) must
+    not wait out a whole timeout in that dead round: it checks in to the round rank 0 opens
+    next, and both build the group there (the r06_full7 elastic GPU failure: rank 1 joined
+    round 1 as rank 0 abandoned it, and each then waited 20 s for the other)."""
+    import datetime
+    import threading
+    import time
+
+    import torch.distributed as dist
+
+    from serverless_learn_amd.parallel.dp import ElasticGroup, GroupCancelled
+    from serverless_learn_amd.utils.ports import reserve_port
+
+    port = reserve_port()
+    master = dist.TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False,
+                           timeout=datetime.timedelta(seconds=30))
+    rdv = f"127.0.0.1:{port}"
+    g0, g1 = ElasticGroup(backend="gloo", timeout_s=0.6), ElasticGroup(backend="gloo", timeout_s=10)
+    ep0 = dist.PrefixStore("sl/e5", g0._store(rdv))
+    ep1 = dist.PrefixStore("sl/e5", g1._store(rdv))
+    with pytest.raises(TimeoutError):
+        g0._open_round(ep0, 5, 0, 2)  # nobody checks in to round 1: rank 0 abandons it
+    got = {}
+    t1 = threading.Thread(target=lambda: got.setdefault("r1", g1._open_round(ep1, 5, 1, 2)))
+    t1.start()  # rank 1 sees round 1 (the abandoned one) and checks in there
+    time.sleep(0.3)
+    assert int(ep0.add("in1", 0)) == 1 and "r1" not in got
+    t0 = time.monotonic()
+    assert g0._open_round(ep0, 5, 0, 2) == 2  # rank 0's retry: rank 1 moves over at once
+    t1.join(5)
+    assert got.get("r1") == 2 and time.monotonic() - t0 < 2.0
+
+    # end to end: both ranks build a gloo group after the abandoned round
+    gg = [ElasticGroup(backend="gloo", timeout_s=10) for _ in range(2)]
+    ok = {}
+    ths = [threading.Thread(target=lambda r=r: ok.setdefault(r, gg[r].reform(6, r, 2, rdv))) for r in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(30)
+    assert ok == {0: True, 1: True}
+    x = torch.tensor([float(1)])
+    y = torch.tensor([float(2)])
+    ws = [threading.Thread(target=gg[0].allreduce_, args=(x,)), threading.Thread(target=gg[1].allreduce_, args=(y,))]
+    for w in ws:
+        w.start()
+    for w in ws:
+        w.join(30)
+    assert float(x) == float(y) == 3.0
+
+    # a rendezvous for a membership that is no longer current ends as soon as that is seen
+    g2 = ElasticGroup(backend="gloo", timeout_s=20)
+    flag = {"stale": False}
+    threading.Timer(0.2, lambda: flag.update(stale=True)).start()
+    t0 = time.monotonic()
+    assert not g2.reform(7, 0, 2, rdv, cancelled=lambda: flag["stale"])
+    assert time.monotonic() - t0 < 2.0 and g2.broken
+    with pytest.raises(GroupCancelled):
+        g2._open_round(dist.PrefixStore("sl/e8", g2._store(rdv)), 8, 1, 2, cancelled=lambda: True)
+    del master
+
+
+def test_replaced_step_graphs_are_retired_until_a_sync_reaps_them():
+    """A trainer's replaced graph is kept alive (its destructor would wait for in-flight
+    launches with the GIL held, r06_full7) until ``reap_graphs`` -- after a device sync, or
+    in ``drop_graphs`` / ``capture`` -- frees it."""
+    import gc
+    import weakref
+
+    from serverless_learn_amd.utils.graphs import GraphSlots
+
+    class G:
+        pass
+
+    class T(GraphSlots):
+        device = torch.device("cpu")
+
+    t = T()
+    assert t.graph is None and t.graph_unrolled is None and t.retired_graphs == 0
+    a, b, k = G(), G(), G()
+    ra, rk = weakref.ref(a), weakref.ref(k)
+    t.graph, t.graph_unrolled = a, k
+    t.graph = a  # same object: nothing retired
+    assert t.retired_graphs == 0
+    del a, k
+    t.graph = None
+    t.graph_unrolled = None
+    t.graph = b
+    gc.collect()
+    assert ra() is not None and rk() is not None and t.retired_graphs == 2
+    t.reap_graphs()
+    gc.collect()
+    assert ra() is None and rk() is None and t.retired_graphs == 0 and t.graph is b
