@@ -399,9 +399,12 @@ def main(argv=None) -> int:
         tr.set_flat(flat)
         collective = "rccl" if args.dist_backend == "nccl" else "gloo"
         if mlp and args.allreduce in ("auto", "xgmi", "xgmi2"):
-            from serverless_learn_amd.parallel.xgmi import XgmiExchange, dist_collectives
+            from serverless_learn_amd.parallel.xgmi import XgmiExchange, dist_collectives, probe
 
             try:
+                bad = probe(rank, world, dev, *dist_collectives())
+                if bad:
+                    raise RuntimeError("exchange probe failed: " + bad)
                 xg = XgmiExchange(tr.n_pad, rank, world, dev, *dist_collectives(),
                                   two_shot=args.allreduce == "xgmi2")
                 tr.enable_xgmi(xg)

@@ -6,6 +6,7 @@ Launched by tests/test_xgmi_gpu.py as
 maps every other rank's exchange buffer over IPC (on one GPU the ranks share the
 device -- the same code path minus the xGMI links).  Checks, per rank:
 
+0. the setup-time probe (``parallel.xgmi.probe``) passes;
 1. the generic all-reduce (one-shot, or reduce-scatter + all-gather with ``--two-shot``) equals the rank-order fp32 sum, over several
    calls (both slot parities, device-side step counter);
 2. the MLP step with the all-reduce fused into its update kernel gives exactly the
@@ -41,6 +42,11 @@ def main() -> int:
     from serverless_learn_amd.data.synthetic import make_mnist_like
     from serverless_learn_amd.models.mlp import FusedMLPTrainer
     from serverless_learn_amd.parallel.xgmi import XgmiExchange, dist_collectives
+
+    # 0. the setup-time probe bench.py and the worker run before trusting the exchange
+    from serverless_learn_amd.parallel.xgmi import probe
+    bad = probe(rank, world, dev, *dist_collectives())
+    assert bad == "", bad
 
     # 1. generic all-reduce
     n = 100_000

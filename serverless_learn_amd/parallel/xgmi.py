@@ -220,6 +220,44 @@ class XgmiExchange:
             self._own = ctypes.c_void_p()
 
 
+def probe(rank: int, world: int, device: torch.device, allgather: Callable[[bytes], list],
+          all_ok: Callable[[bool], bool], n: int = 1 << 16) -> str:
+    """Setup-time functional check of the exchange between THESE devices, before a trainer
+    depends on it: a small one-shot and a small two-shot exchange each sum two payloads of
+    small integers (exact in fp32, both slot parities) and compare with the closed form.  The
+    verdict is agreed over the group.  Returns "" when every rank passed, otherwise the first
+    failure seen here (or "a peer failed"), so the caller keeps the process group's all-reduce
+    instead of finding out from a barrier timeout in every step.
+
+    The protocol has been exercised only by ranks sharing one GPU on this pool; on a real
+    multi-GPU node this is the first thing that crosses the xGMI links."""
+    err = ""
+    idx = torch.arange(n, device=device, dtype=torch.int64)
+    for two in (False, True):
+        ex = None
+        try:
+            ex = XgmiExchange(n, rank, world, device, allgather, all_ok, two_shot=two)
+            for call in range(2):
+                t = ((idx * (call + 3)) % 7 + rank + 1).to(torch.float32)
+                ex.allreduce_(t)
+                want = ((idx * (call + 3)) % 7 * world + world * (world + 1) // 2).to(torch.float32)
+                torch.cuda.synchronize(device)
+                if ex.error():
+                    err = err or f"{'two' if two else 'one'}-shot probe: barrier timed out"
+                elif not torch.equal(t, want):
+                    bad = int((t != want).sum())
+                    err = err or f"{'two' if two else 'one'}-shot probe call {call}: {bad} of {n} sums wrong"
+        except RuntimeError as e:
+            err = err or f"{'two' if two else 'one'}-shot probe: {e}"
+            ex = None  # the constructor agreed on its own failure and freed what it had
+        ok = all_ok(not err)  # every rank leaves this exchange together before anyone unmaps
+        if ex is not None:
+            ex.close()
+        if not ok:
+            return err or "a peer failed the exchange probe"
+    return ""
+
+
 def dist_collectives(group=None):
     """(allgather, all_ok) over a torch.distributed process group (default group)."""
     import torch.distributed as dist

@@ -495,10 +495,13 @@ class Worker:
             return
         t = self.trainer
         hsize = int(xgmi.N.lib().sl_ipc_handle_size())
+        gather = lambda b: self.group.allgather_fixed(b, hsize)  # noqa: E731
         try:
+            bad = xgmi.probe(self.group.rank, self.group.world, self.device, gather, self.group.all_true)
+            if bad:
+                raise RuntimeError("exchange probe failed: " + bad)
             ex = xgmi.XgmiExchange(t.n_pad, self.group.rank, self.group.world, self.device,
-                                   lambda b: self.group.allgather_fixed(b, hsize), self.group.all_true,
-                                   two_shot=xgmi.default_two_shot(self.group.world))
+                                   gather, self.group.all_true, two_shot=xgmi.default_two_shot(self.group.world))
         except (RuntimeError, GroupBroken) as e:
             self.log.warn("xgmi_unavailable", error=str(e))
             return
