@@ -439,9 +439,11 @@ class Worker:
             # current NOW, not the one read before them (a stale epoch's rendezvous waits out its
             # whole timeout for members that already moved on)
             with self.view_lock:
-                v = dict(self.view)
-            if not self._needs_regroup(v):
-                return
+                now = dict(self.view)
+            if now["epoch"] != v["epoch"]:
+                v = now  # (same epoch: same membership; re-asking would restart the broken-group window)
+                if not self._needs_regroup(v):
+                    return
             epoch = v["epoch"]
             ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"],
                                    cancelled=lambda: self.view["epoch"] != epoch or self._stop.is_set())

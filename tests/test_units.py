@@ -785,3 +785,35 @@ def test_replaced_step_graphs_are_retired_until_a_sync_reaps_them():
     t.reap_graphs()
     gc.collect()
     assert ra() is None and rk() is None and t.retired_graphs == 0 and t.graph is b
+
+
+def test_regroup_forms_the_view_current_after_its_drains(monkeypatch):
+    """The drains before a re-form (leaving the exchange, dropping graphs) can take up to the
+    exchange's dead-peer timeout.  The worker must then form the view current at that moment:
+    a newer epoch if one arrived, nothing while it re-registers (epoch 0), and the epoch read
+    before the drains when it is still current (r06_full7: w0 formed a stale epoch 4 for 20 s)."""
+    from serverless_learn_amd.runtime.local_cluster import fast_config
+    from serverless_learn_amd.runtime.worker import Worker
+
+    w = Worker("127.0.0.1:0", fast_config())
+    calls = []
+
+    class G:
+        backend, world, epoch, rank = "gloo", 3, 3, 0
+        broken, active = True, False
+
+        def reform(self, epoch, rank, world, rdv, cancelled=None):
+            calls.append((epoch, rank, world, cancelled()))
+            return False
+
+    def view(epoch, rank=0, world=2):
+        return {"epoch": epoch, "peers": [], "rank": rank, "world": world, "rendezvous": "x:1", "resume_file": 0}
+
+    for after, want in ((view(8, 1), [(8, 1, 2, False)]), (view(0, -1, 0), []), (view(4), [(4, 0, 2, False)])):
+        calls.clear()
+        w.group, w.view = G(), view(4)
+        monkeypatch.setattr(w, "_drop_xgmi", lambda healthy=False, after=after: setattr(w, "view", after))
+        monkeypatch.setattr(w, "_drop_graphs", lambda: None)
+        monkeypatch.setattr(w._stop, "wait", lambda s=None: None)
+        w._maybe_regroup()
+        assert calls == want, (after["epoch"], calls)
