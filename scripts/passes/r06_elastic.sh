@@ -5,7 +5,7 @@
 set -u
 cd "$(dirname "$0")/../.."
 export TMPDIR=/tmp
-O=gpurun_out/r06_elastic; mkdir -p $O
+O=gpurun_out/${PASS_TAG:-r06_elastic}; mkdir -p $O
 i=0
 for cfg in "mlp kill2 --xgmi-gloo" "mlp all --xgmi-gloo" "resnet18 kill2" "resnet18 all"; do
   set -- $cfg

@@ -8,9 +8,10 @@ process per GPU, the deployment shape, is unaffected.
 
 Not used for the elastic workers (scripts/elastic_demo.py). With 2 queues each, a surviving
 worker stopped answering CheckUp while its update kernel spun for the dead peer until the
-exchange's 10 s timeout. The likely cause is a graph replay blocking on a full queue while it
-holds the GIL. The master then evicted that healthy worker (r06_full5). With HIP's 4 queues
-the same test passes.
+exchange's 10 s timeout, and the master evicted that healthy worker (r06_full5). The same
+silence later came back with HIP's 4 queues (r06_full7). Its cause was a step graph destroyed
+while a replay was still in flight: the destructor waits with the GIL held. Trainers now retire
+replaced graphs and free them only after a sync (utils/graphs.py).
 """
 from __future__ import annotations
 
