@@ -817,3 +817,55 @@ def test_regroup_forms_the_view_current_after_its_drains(monkeypatch):
         monkeypatch.setattr(w._stop, "wait", lambda s=None: None)
         w._maybe_regroup()
         assert calls == want, (after["epoch"], calls)
+
+
+def test_xgmi_probe_decision_is_group_wide_and_always_unmaps(monkeypatch):
+    """parallel.xgmi.probe: every rank returns a failure when any rank's probe exchange fails
+    (wrong sums, a barrier timeout, or a mapping error), each probe exchange is closed only
+    after the group agreed, and a clean group returns "" (CPU: a fake exchange does the sums)."""
+    from serverless_learn_amd.parallel import xgmi
+
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    events = []
+
+    def fake(mode):
+        class Ex:
+            def __init__(self, n, rank, world, device, allgather, all_ok, two_shot=False):
+                if mode == "map":
+                    raise RuntimeError("xgmi exchange unavailable: hipIpcOpenMemHandle(rank 1) failed (1)")
+                self.rank, self.world, self.two = rank, world, two_shot
+
+            def allreduce_(self, t, scale=1.0):
+                w = self.world
+                t.copy_((t - self.rank - 1) * w + w * (w + 1) // 2)
+                if mode == "sums" and self.two:
+                    t[5] += 1
+
+            def error(self):
+                return mode == "timeout"
+
+            def close(self, sync=True):
+                events.append(("close", self.two))
+        return Ex
+
+    def all_ok_from(peer_ok):
+        def all_ok(ok):
+            events.append(("agree", ok))
+            return ok and peer_ok
+        return all_ok
+
+    dev = torch.device("cpu")
+    for mode, peer_ok, want_err in (("clean", True, ""), ("clean", False, "a peer failed"), ("sums", True, "two-shot probe call 0: 1 of"),
+                                    ("timeout", True, "one-shot probe: barrier timed out"), ("map", True, "one-shot probe: xgmi exchange unavailable")):
+        events.clear()
+        monkeypatch.setattr(xgmi, "XgmiExchange", fake(mode))
+        err = xgmi.probe(2, 4, dev, lambda b: [b] * 4, all_ok_from(peer_ok), n=64)
+        assert (err == "") if not want_err else err.startswith(want_err), (mode, peer_ok, err)
+        agrees = [e for e in events if e[0] == "agree"]
+        closes = [e for e in events if e[0] == "close"]
+        if mode == "map":
+            assert closes == [] and len(agrees) == 1
+        else:
+            # each exchange closes right after its agreement; a failed first one ends the probe
+            assert events[0][0] == "agree" and events[1] == ("close", False)
+            assert len(agrees) == (2 if (not want_err or mode == "sums") else 1)
