@@ -159,6 +159,7 @@ __device__ __forceinline__ void xg_signal_wait(const XgArgs& x, int set) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - s) < 0) {
       __builtin_amdgcn_s_sleep(2);
+      if (__hip_atomic_load(x.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;  // host abort
       if (__builtin_amdgcn_s_memrealtime() - t0 > XG_TIMEOUT_TICKS) {
         __hip_atomic_store(x.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -171,7 +172,8 @@ __device__ __forceinline__ void xg_signal_wait(const XgArgs& x, int set) {
 // Consumer side of the inline mode: workgroup 0 signals step s through `set` to every rank
 // (this rank's producer kernel has completed: stream order), then one lane of every workgroup
 // waits until every rank has signalled s (bounded: after XG_TIMEOUT_TICKS it records the error
-// word; a block that finds the word set -- another gave up -- stops waiting), and the workgroup
+// word; a block that finds the word set -- another gave up, or the host aborted the group
+// (xgmi_abort_kernel) -- stops waiting), and the workgroup
 // proceeds.  Every later read of a peer's bytes is a system-scope load (xg_load).
 __device__ __forceinline__ void xg_block_wait(const XgArgs& x, int set, unsigned s) {
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)x.world)

@@ -21,6 +21,13 @@ __global__ __launch_bounds__(256) void xgmi_copyin_kernel(XgArgs x, const float4
 
 __global__ __launch_bounds__(64) void xgmi_barrier_kernel(XgArgs x, int set) { xg_signal_wait(x, set); }
 
+// Host-requested abort (the runtime found the group broken): sets the error word the waits poll,
+// so a wait on a dead peer ends now instead of at XG_TIMEOUT_TICKS, and the steps still queued
+// skip theirs.  Launched on a stream of its own; the results since are void, as after a timeout.
+__global__ __launch_bounds__(64) void xgmi_abort_kernel(unsigned* ctl) {
+  if (threadIdx.x == 0) __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Two-shot reduce-scatter (after barrier set 0): this rank's chunk of the W slots,
 // summed in rank order into the same offsets of its own reduced slot.  Inline mode: workgroup 0
 // signals set 0 and every workgroup waits for it; the update kernel after it signals set 1.
@@ -174,6 +181,13 @@ int sl_xgmi_rs(char* const* bases, unsigned* ctl, long slot_bytes, int rank, int
   int grid = xg_grid(chunk4);
   if (inline_sync == 2) grid = xg_shared_grid(grid, world);
   hipLaunchKernelGGL(xgmi_rs_kernel, dim3(grid), dim3(256), 0, stream, x, n / 4);
+  SL_CHECK_LAUNCH();
+  return 0;
+}
+
+int sl_xgmi_abort(unsigned* ctl, hipStream_t stream) {
+  if (!ctl) return -1;
+  hipLaunchKernelGGL(xgmi_abort_kernel, dim3(1), dim3(64), 0, stream, ctl);
   SL_CHECK_LAUNCH();
   return 0;
 }

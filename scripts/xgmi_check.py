@@ -12,7 +12,9 @@ device -- the same code path minus the xGMI links).  Checks, per rank:
 2. the MLP step with the all-reduce fused into its update kernel gives exactly the
    parameters of the same step with gloo's all-reduce of the reduced gradient,
    eager and replayed from an 8-step hipGraph, and all replicas stay bit-identical;
-3. no barrier timed out.
+3. no barrier timed out;
+4. ``XgmiExchange.abort()`` ends a wait on peers that never signal within 3 s (processes with
+   HIP's default 4 hardware queues: the 2-rank runs).
 Prints ``XGMI_CHECK_OK rank=R`` on success; any failure raises (non-zero exit).
 """
 import os
@@ -132,6 +134,23 @@ def main() -> int:
     dist.barrier()
     torch.cuda.synchronize()
     xa.close()
+    # 4. host abort: rank 0 starts an exchange that no peer joins; XgmiExchange.abort() must end
+    # its wait at once (the elastic runtime calls it on a broken group) instead of at the 10 s timeout
+    # (only with HIP's default 4 hardware queues: capped ranks may share one queue with the spinner)
+    import time
+    xb = XgmiExchange(1024, rank, world, dev, *dist_collectives(), two_shot=False)
+    if rank == 0 and int(os.environ.get("GPU_MAX_HW_QUEUES") or 4) >= 4:
+        t = torch.ones(1024, device=dev)
+        xb.allreduce_(t)
+        time.sleep(0.3)  # the barrier is spinning on the peers by now
+        t0 = time.monotonic()
+        xb.abort()
+        torch.cuda.synchronize()
+        waited = time.monotonic() - t0
+        assert xb.error() and waited < 3.0, (xb.error(), waited)
+        print(f"XGMI_ABORT rank=0 drained_s={waited:.3f}", flush=True)
+    dist.barrier()  # rank 0's kernels are done with every peer's buffer before anyone unmaps
+    xb.close()
     print(f"XGMI_CHECK_OK rank={rank} two_shot={two} steps={done} loss={a.stats().loss:.4f}", flush=True)
     dist.destroy_process_group()
     return 0

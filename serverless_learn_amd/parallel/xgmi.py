@@ -52,6 +52,7 @@ N.register("sl_xgmi_buffer_bytes", [N.L], restype=ctypes.c_long)
 N.register("sl_xgmi_copyin", [N.P, N.P, N.L, N.I, N.I, N.L, N.P, N.L, N.P])
 N.register("sl_xgmi_barrier", [N.P, N.P, N.L, N.I, N.I, N.L, N.I, N.P])
 N.register("sl_xgmi_rs", [N.P, N.P, N.L, N.I, N.I, N.L, N.L, N.I, N.P])
+N.register("sl_xgmi_abort", [N.P, N.P])
 N.register("sl_xgmi_sum", [N.P, N.P, N.L, N.I, N.I, N.L, N.P, N.L, N.F, N.P])
 N.register("sl_xgmi_peek", [N.P, N.P, N.L, N.I, N.I, N.L, N.I, N.I, N.I, N.P, N.L, N.P])
 
@@ -118,6 +119,7 @@ class XgmiExchange:
         self._own = ctypes.c_void_p()
         self._opened: list[int] = []
         self.table = None
+        self._abort_stream = None
         ok = True
         err = ""
         with torch.cuda.device(device):
@@ -205,6 +207,20 @@ class XgmiExchange:
     def error(self) -> bool:
         """True if a barrier gave up waiting for a peer (the results since are invalid)."""
         return int(self.ctl[2].item()) != 0
+
+    def abort(self) -> None:
+        """The group is broken (a peer died): set the error word from a stream of its own, so
+        a consumer spinning on the dead peer stops now instead of at the 10 s timeout, and the
+        steps still queued skip their waits.  Their results are void, as after a timeout; the
+        runtime re-forms the group and re-syncs the state from rank 0.
+
+        Best effort: the abort kernel runs at once only if its (high-priority) stream does not
+        share a hardware queue with the spinning consumer.  A process capped to 1-2 queues
+        (several ranks on one GPU, utils/gpu_share.py) may have it queued behind the consumer
+        until the timeout; that is harmless, just not faster."""
+        if self._abort_stream is None:
+            self._abort_stream = torch.cuda.Stream(device=self.device, priority=-1)
+        N.call("sl_xgmi_abort", self.ctl.data_ptr(), N.stream_ptr(self._abort_stream))
 
     def close(self, sync: bool = True) -> None:
         """Unmap peers and free the buffer.  ``sync``: the caller has already made sure

@@ -521,6 +521,8 @@ class Worker:
         ex, self.xgmi = self.xgmi, None
         if ex is None:
             return
+        if not healthy:
+            ex.abort()  # queued consumers stop waiting on the dead peer (else up to 10 s each drain)
         with self.train_lock:
             if self.trainer is not None and hasattr(self.trainer, "enable_xgmi"):
                 self.trainer.enable_xgmi(None)
