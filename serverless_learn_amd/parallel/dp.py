@@ -62,6 +62,7 @@ class ElasticGroup:
         self.log = Logger("dp")
         self._stores = {}
         self._rounds: dict[int, int] = {}
+        self._retired: list = []
 
     @property
     def active(self) -> bool:
@@ -75,13 +76,25 @@ class ElasticGroup:
             self._stores[rendezvous] = st
         return st
 
+    RETIRED_KEEP = 8  # torn-down gloo groups kept alive (see teardown)
+
     def teardown(self) -> None:
         pg, self.pg = self.pg, None
-        if pg is not None and self.backend == "nccl":
+        if pg is None:
+            return
+        if self.backend == "nccl":
             try:
                 pg.abort()  # ncclCommAbort: never block on a dead peer
             except Exception as e:
                 self.log.warn("abort_failed", error=repr(e))
+            return
+        # A gloo group's destructor waits for the collectives still queued on it, and one posted
+        # to a dead peer ends only at the group timeout: a survivor's regroup sat 17 s in that
+        # destructor (profiles/r06_elastic_abort, ResNet kill2).  Keep the group alive instead;
+        # its threads fail those collectives on their own.  The oldest of RETIRED_KEEP is freed
+        # once a newer one is retired, long after its timeout has passed.
+        self._retired.append(pg)
+        del self._retired[:-self.RETIRED_KEEP]
 
     def _open_round(self, ep_store, epoch: int, rank: int, world: int, cancelled=None) -> int:
         """Agree on a fresh rendezvous round for this epoch, with every rank checked in.

@@ -869,3 +869,36 @@ def test_xgmi_probe_decision_is_group_wide_and_always_unmaps(monkeypatch):
             # each exchange closes right after its agreement; a failed first one ends the probe
             assert events[0][0] == "agree" and events[1] == ("close", False)
             assert len(agrees) == (2 if (not want_err or mode == "sums") else 1)
+
+
+def test_gloo_teardown_does_not_wait_for_collectives_queued_on_a_dead_peer():
+    """A survivor tearing down its broken gloo group must not sit in the group's destructor
+    until a collective it posted to a dead peer times out (r06_elastic_abort: a 17 s regroup)."""
+    import datetime
+    import threading
+    import time
+
+    import torch.distributed as dist
+
+    from serverless_learn_amd.parallel.dp import ElasticGroup
+    from serverless_learn_amd.utils.ports import reserve_port
+
+    port = reserve_port()
+    master = dist.TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False,
+                           timeout=datetime.timedelta(seconds=30))
+    gg = [ElasticGroup(backend="gloo", timeout_s=8) for _ in range(2)]
+    ok = {}
+    ths = [threading.Thread(target=lambda r=r: ok.setdefault(r, gg[r].reform(1, r, 2, f"127.0.0.1:{port}")))
+           for r in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(30)
+    assert ok == {0: True, 1: True}
+    work = gg[0].allreduce_async(torch.ones(4))  # rank 1 never joins: pending until the timeout
+    assert work is not None
+    t0 = time.monotonic()
+    gg[0].teardown()
+    assert time.monotonic() - t0 < 2.0 and not gg[0].active and len(gg[0]._retired) == 1
+    gg[1].teardown()
+    del master
