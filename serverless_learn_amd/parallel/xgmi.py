@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from typing import Callable
 
 import torch
@@ -120,6 +121,8 @@ class XgmiExchange:
         self._opened: list[int] = []
         self.table = None
         self._abort_stream = None
+        self._abort_lock = threading.Lock()
+        self._aborted = False
         ok = True
         err = ""
         with torch.cuda.device(device):
@@ -218,9 +221,19 @@ class XgmiExchange:
         share a hardware queue with the spinning consumer.  A process capped to 1-2 queues
         (several ranks on one GPU, utils/gpu_share.py) may have it queued behind the consumer
         until the timeout; that is harmless, just not faster."""
-        if self._abort_stream is None:
-            self._abort_stream = torch.cuda.Stream(device=self.device, priority=-1)
-        N.call("sl_xgmi_abort", self.ctl.data_ptr(), N.stream_ptr(self._abort_stream))
+        with torch.cuda.device(self.device):  # callable from any thread (the runtime's CheckUp handler)
+            if self._abort_stream is None:
+                self._abort_stream = torch.cuda.Stream(device=self.device, priority=-1)
+            N.call("sl_xgmi_abort", self.ctl.data_ptr(), N.stream_ptr(self._abort_stream))
+
+    def abort_once(self) -> None:
+        """:meth:`abort` unless already requested (the runtime may ask from its CheckUp thread
+        and again from the training thread)."""
+        with self._abort_lock:
+            if self._aborted or not self._own.value:
+                return
+            self._aborted = True
+        self.abort()
 
     def close(self, sync: bool = True) -> None:
         """Unmap peers and free the buffer.  ``sync``: the caller has already made sure

@@ -114,6 +114,7 @@ class Worker:
         self._agreed_epoch = -1   # newest membership epoch the whole lock-step group has agreed to see
         self._broken_since = None  # when the live group was first seen broken (monotonic s)
         self._agree_stream = None  # side stream of the epoch agreement on RCCL groups
+        self._group_peers: list[str] = []  # membership of the group last formed (exchange abort on eviction)
         self.bytes_ingested = 0
         self._log_param_sum = os.environ.get("SL_LOG_PARAM_SUM", "0") == "1"
         self.files_received: list[int] = []
@@ -236,6 +237,12 @@ class Worker:
         with self.view_lock:
             self.view = {"epoch": pl.epoch, "peers": list(pl.peer_addrs), "rank": pl.rank,
                          "world": pl.world_size, "rendezvous": pl.rendezvous, "resume_file": pl.resume_file}
+        ex = self.xgmi
+        if ex is not None and pl.epoch > 0 and not set(self._group_peers) <= set(pl.peer_addrs):
+            # a member of the live exchange was evicted (dead): release the queued consumers that
+            # wait on it now -- the training thread is blocked on them, so it cannot do it itself
+            # until the 10 s timeout (XgmiExchange.abort; the results since are void either way)
+            ex.abort_once()
         gm = self.group_metrics
         fb = pb.FlowFeedback(step=self.step, samples_per_sec=self.rate,
                              loss=self.loss if self.loss == self.loss else 0.0,
@@ -445,6 +452,7 @@ class Worker:
                 if not self._needs_regroup(v):
                     return
             epoch = v["epoch"]
+            self._group_peers = list(v["peers"])
             ok = self.group.reform(v["epoch"], v["rank"], v["world"], v["rendezvous"],
                                    cancelled=lambda: self.view["epoch"] != epoch or self._stop.is_set())
             if not ok:
@@ -522,7 +530,7 @@ class Worker:
         if ex is None:
             return
         if not healthy:
-            ex.abort()  # queued consumers stop waiting on the dead peer (else up to 10 s each drain)
+            ex.abort_once()  # queued consumers stop waiting on the dead peer (else up to 10 s each drain)
         with self.train_lock:
             if self.trainer is not None and hasattr(self.trainer, "enable_xgmi"):
                 self.trainer.enable_xgmi(None)
